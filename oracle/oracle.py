@@ -1,0 +1,387 @@
+"""oracle/oracle.py -- TEST INFRASTRUCTURE ONLY (the parity checker).
+
+CPU restatement of the reference's per-frame Mask R-CNN hot path, used to check
+the HIP kernels in ``vosdetectron_amd``.  Only ``tests/``, ``__graft_entry__.smoke()``
+and ``bench.py``'s ``cpu_baseline`` leg may import this module; the product path
+never does (it fails loudly when its HIP library is missing).
+
+Byte/index semantics follow the reference functions cited on each function, as
+executed by numpy 2.2 (this image).  Two deliberate, documented readings:
+
+* Sorting.  The reference uses numpy's default (unstable) ``argsort`` /
+  ``argpartition``; with tied keys their order is implementation-defined.  The
+  oracle uses the *stable* reading: ``argsort(-s)`` keeps ties in index order,
+  ``s.argsort()[::-1]`` (the NMS order) visits ties highest-index-first -- the
+  order the survey observed for the reference (``keep=[1, 2]`` for two
+  identical boxes).  Golden fixtures generated from the reference itself use
+  tie-free scores, where every reading agrees.
+* dtype promotion.  ``BBOX_XFORM_CLIP`` is an ``np.float64`` scalar
+  (``lib/core/config.py:1009``), so under numpy 2 (NEP 50) ``np.minimum(dw,
+  clip)`` promotes ``dw``/``dh`` -- and with them ``exp(dw) * w`` and the box
+  corners -- to float64 before the float32 store.  The oracle (and the HIP
+  decode kernel) reproduce that.
+
+Pinning: the functions marked ``[pinned]`` are checked against golden vectors
+produced by importing the reference's own Python (``tools/gen_goldens.py`` ->
+``tests/golden/``) and against the anchor known-answer table in
+``lib/modeling/generate_anchors.py:26-51``.  The C kernels in ``roi_ops.c`` are
+"parity unpinned" against an executed reference (see that file's header).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+BBOX_XFORM_CLIP = np.log(1000. / 16.)  # lib/core/config.py:1009 (np.float64)
+PIXEL_MEANS = np.array([[[102.9801, 115.9465, 122.7717]]])  # config.py:1015
+
+
+def build(force: bool = False) -> str:
+    """Compile roi_ops.c into oracle/liboracle.so (gcc, no FMA contraction)."""
+    src = os.path.join(_HERE, "roi_ops.c")
+    if force or not os.path.exists(_LIB_PATH) or \
+            os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        f32p = ctypes.POINTER(ctypes.c_float)
+        i32p = ctypes.POINTER(ctypes.c_int32)
+        i64p = ctypes.POINTER(ctypes.c_int64)
+        ci, cf = ctypes.c_int, ctypes.c_float
+        L.or_roi_align_fwd.argtypes = [f32p, ci, ci, ci, ci, f32p, ci, ci, ci, cf, ci, f32p]
+        L.or_roi_align_bwd.argtypes = [f32p, ci, ci, ci, ci, f32p, ci, ci, ci, cf, ci, f32p]
+        L.or_roi_align_legacy_fwd.argtypes = [f32p, ci, ci, ci, ci, f32p, ci, ci, ci, cf, f32p]
+        L.or_roi_pool_fwd.argtypes = [f32p, ci, ci, ci, ci, f32p, ci, ci, ci, cf, f32p, i32p]
+        L.or_roi_crop_fwd.argtypes = [f32p, ci, ci, ci, ci, f32p, ci, ci, ci, f32p]
+        L.or_nms.argtypes = [f32p, ci, ci, cf, i64p]
+        L.or_nms.restype = ci
+        _lib = L
+    return _lib
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _p(a, t=ctypes.c_float):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+# --------------------------------------------------------------------------- #
+# RoI operators (C restatements, see roi_ops.c)                                #
+# --------------------------------------------------------------------------- #
+def roi_align(features, rois, ph, pw, spatial_scale, sampling_ratio):
+    """Caffe2 RoIAlign fwd, roi_align_kernel.cu:65-121. features NCHW f32."""
+    f, r = _f32(features), _f32(rois)
+    B, C, H, W = f.shape
+    R = r.shape[0]
+    out = np.zeros((R, C, ph, pw), np.float32)
+    if R:
+        lib().or_roi_align_fwd(_p(f), B, C, H, W, _p(r), R, ph, pw,
+                               float(spatial_scale), int(sampling_ratio), _p(out))
+    return out
+
+
+def roi_align_backward(top_diff, rois, feat_shape, spatial_scale, sampling_ratio):
+    """Caffe2 RoIAlign bwd, roi_align_kernel.cu:195-270 (serial sum order)."""
+    g, r = _f32(top_diff), _f32(rois)
+    B, C, H, W = feat_shape
+    R, _, ph, pw = g.shape
+    out = np.zeros((B, C, H, W), np.float32)
+    if R:
+        lib().or_roi_align_bwd(_p(g), B, C, H, W, _p(r), R, ph, pw,
+                               float(spatial_scale), int(sampling_ratio), _p(out))
+    return out
+
+
+def roi_align_legacy(features, rois, ph, pw, spatial_scale):
+    """jwyang RoIAlign fwd, lib/model/roi_align/src/roi_align_kernel.cu:15-70."""
+    f, r = _f32(features), _f32(rois)
+    B, C, H, W = f.shape
+    R = r.shape[0]
+    out = np.zeros((R, C, ph, pw), np.float32)
+    if R:
+        lib().or_roi_align_legacy_fwd(_p(f), B, C, H, W, _p(r), R, ph, pw,
+                                      float(spatial_scale), _p(out))
+    return out
+
+
+def roi_pool(features, rois, ph, pw, spatial_scale):
+    """RoIPool fwd (CUDA semantics), roi_pooling_kernel.cu:24-93."""
+    f, r = _f32(features), _f32(rois)
+    B, C, H, W = f.shape
+    R = r.shape[0]
+    out = np.zeros((R, C, ph, pw), np.float32)
+    arg = np.zeros((R, C, ph, pw), np.int32)
+    if R:
+        lib().or_roi_pool_fwd(_p(f), B, C, H, W, _p(r), R, ph, pw,
+                              float(spatial_scale), _p(out), _p(arg, ctypes.c_int32))
+    return out, arg
+
+
+def roi_crop(features, grid_yx):
+    """RoICrop bilinear sampler fwd, roi_crop_cuda_kernel.cu:47-109."""
+    f, g = _f32(features), _f32(grid_yx)
+    B, C, H, W = f.shape
+    R, GH, GW, _ = g.shape
+    out = np.zeros((R, C, GH, GW), np.float32)
+    if R:
+        lib().or_roi_crop_fwd(_p(f), B, C, H, W, _p(g), R, GH, GW, _p(out))
+    return out
+
+
+def nms(dets, thresh):
+    """utils.boxes.nms -> cython_nms.nms (boxes.py:329-333, cython_nms.pyx:37-87).
+
+    Returns kept indices, ascending, int64 (``[]`` -> empty array)."""
+    d = _f32(dets)
+    n = d.shape[0]
+    if n == 0:
+        return np.zeros((0,), np.int64)
+    keep = np.empty((n,), np.int64)
+    k = lib().or_nms(_p(d), n, d.shape[1], float(np.float32(thresh)),
+                     _p(keep, ctypes.c_int64))
+    return keep[:k]
+
+
+# --------------------------------------------------------------------------- #
+# Anchors, box decode, proposals                                   [pinned]    #
+# --------------------------------------------------------------------------- #
+def generate_anchors(stride=16, sizes=(32, 64, 128, 256, 512), aspect_ratios=(0.5, 1, 2)):
+    """lib/modeling/generate_anchors.py:54-123 (float64)."""
+    scales = np.array(sizes, dtype=np.float64) / stride
+    ratios = np.array(aspect_ratios, dtype=np.float64)
+    anchor = np.array([1, 1, stride, stride], dtype=np.float64) - 1
+
+    def whctrs(a):
+        w = a[2] - a[0] + 1
+        h = a[3] - a[1] + 1
+        return w, h, a[0] + 0.5 * (w - 1), a[1] + 0.5 * (h - 1)
+
+    def mk(ws, hs, xc, yc):
+        ws, hs = ws[:, None], hs[:, None]
+        return np.hstack((xc - 0.5 * (ws - 1), yc - 0.5 * (hs - 1),
+                          xc + 0.5 * (ws - 1), yc + 0.5 * (hs - 1)))
+
+    w, h, xc, yc = whctrs(anchor)
+    ws = np.round(np.sqrt(w * h / ratios))
+    hs = np.round(ws * ratios)
+    base = mk(ws, hs, xc, yc)
+    out = []
+    for i in range(base.shape[0]):
+        w, h, xc, yc = whctrs(base[i])
+        out.append(mk(w * scales, h * scales, xc, yc))
+    return np.vstack(out)
+
+
+def fpn_level_anchors(lvl, k_min=2, start_size=32, ratios=(0.5, 1, 2)):
+    """Per-level anchors as built in lib/modeling/FPN.py:340-350."""
+    return generate_anchors(stride=2. ** lvl, sizes=(start_size * 2. ** (lvl - k_min),),
+                            aspect_ratios=ratios)
+
+
+def bbox_transform(boxes, deltas, weights=(1.0, 1.0, 1.0, 1.0), clip=BBOX_XFORM_CLIP):
+    """lib/utils/boxes.py:156-205, numpy-2 promotion semantics (see module doc)."""
+    if boxes.shape[0] == 0:
+        return np.zeros((0, deltas.shape[1]), dtype=deltas.dtype)
+    boxes = boxes.astype(deltas.dtype, copy=False)
+    widths = boxes[:, 2] - boxes[:, 0] + 1.0
+    heights = boxes[:, 3] - boxes[:, 1] + 1.0
+    ctr_x = boxes[:, 0] + 0.5 * widths
+    ctr_y = boxes[:, 1] + 0.5 * heights
+    wx, wy, ww, wh = weights
+    dx = deltas[:, 0::4] / wx
+    dy = deltas[:, 1::4] / wy
+    dw = np.minimum(deltas[:, 2::4] / ww, clip)
+    dh = np.minimum(deltas[:, 3::4] / wh, clip)
+    pred_ctr_x = dx * widths[:, None] + ctr_x[:, None]
+    pred_ctr_y = dy * heights[:, None] + ctr_y[:, None]
+    pred_w = np.maximum(np.exp(dw) * widths[:, None], 1.0)
+    pred_h = np.maximum(np.exp(dh) * heights[:, None], 1.0)
+    out = np.zeros(deltas.shape, dtype=deltas.dtype)
+    out[:, 0::4] = pred_ctr_x - 0.5 * pred_w
+    out[:, 1::4] = pred_ctr_y - 0.5 * pred_h
+    out[:, 2::4] = pred_ctr_x + 0.5 * pred_w - 1
+    out[:, 3::4] = pred_ctr_y + 0.5 * pred_h - 1
+    return out
+
+
+def clip_tiled_boxes(boxes, im_shape):
+    """lib/utils/boxes.py:138-153 (in place, returns boxes)."""
+    boxes[:, 0::4] = np.maximum(np.minimum(boxes[:, 0::4], im_shape[1] - 1), 0)
+    boxes[:, 1::4] = np.maximum(np.minimum(boxes[:, 1::4], im_shape[0] - 1), 0)
+    boxes[:, 2::4] = np.maximum(np.minimum(boxes[:, 2::4], im_shape[1] - 1), 0)
+    boxes[:, 3::4] = np.maximum(np.minimum(boxes[:, 3::4], im_shape[0] - 1), 0)
+    return boxes
+
+
+def filter_boxes(boxes, min_size, im_info):
+    """lib/modeling/generate_proposals.py:171-182."""
+    min_size = min_size * im_info[2]
+    ws = boxes[:, 2] - boxes[:, 0] + 1
+    hs = boxes[:, 3] - boxes[:, 1] + 1
+    x_ctr = boxes[:, 0] + ws / 2.
+    y_ctr = boxes[:, 1] + hs / 2.
+    return np.where((ws >= min_size) & (hs >= min_size) &
+                    (x_ctr < im_info[1]) & (y_ctr < im_info[0]))[0]
+
+
+def shifted_anchors(anchors, feat_stride, height, width):
+    """generate_proposals.py:69-89: (K*A, 4) float64, rows ordered (h, w, a)."""
+    sx = np.arange(0, width) * feat_stride
+    sy = np.arange(0, height) * feat_stride
+    sx, sy = np.meshgrid(sx, sy, copy=False)
+    shifts = np.vstack((sx.ravel(), sy.ravel(), sx.ravel(), sy.ravel())).transpose()
+    A, K = anchors.shape[0], shifts.shape[0]
+    return (anchors[None, :, :] + shifts[:, None, :]).reshape((K * A, 4))
+
+
+def proposals_for_one_image(im_info, all_anchors, bbox_deltas, scores,
+                            pre_nms_topN, post_nms_topN, nms_thresh, min_size):
+    """generate_proposals.py:104-168 (stable top-k reading)."""
+    bbox_deltas = bbox_deltas.transpose((1, 2, 0)).reshape((-1, 4))
+    scores = scores.transpose((1, 2, 0)).reshape((-1, 1))
+    order = np.argsort(-scores.squeeze(axis=1), kind="stable")
+    if not (pre_nms_topN <= 0 or pre_nms_topN >= len(scores)):
+        order = order[:pre_nms_topN]
+    bbox_deltas = bbox_deltas[order, :]
+    all_anchors = all_anchors[order, :]
+    scores = scores[order]
+    proposals = bbox_transform(all_anchors, bbox_deltas, (1.0, 1.0, 1.0, 1.0))
+    proposals = clip_tiled_boxes(proposals, im_info[:2])
+    keep = filter_boxes(proposals, min_size, im_info)
+    proposals = proposals[keep, :]
+    scores = scores[keep]
+    if nms_thresh > 0:
+        keep = nms(np.hstack((proposals, scores)), nms_thresh)
+        if post_nms_topN > 0:
+            keep = keep[:post_nms_topN]
+        proposals = proposals[keep, :]
+        scores = scores[keep]
+    return proposals, scores
+
+
+def generate_proposals(anchors, spatial_scale, cls_prob, bbox_pred, im_info,
+                       pre_nms_topN=1000, post_nms_topN=1000, nms_thresh=0.7, min_size=0):
+    """GenerateProposalsOp.forward (generate_proposals.py:20-102) on ndarrays."""
+    scores = np.asarray(cls_prob, np.float32)
+    deltas = np.asarray(bbox_pred, np.float32)
+    im_info = np.asarray(im_info, np.float32)
+    height, width = scores.shape[-2:]
+    all_anchors = shifted_anchors(anchors, 1. / spatial_scale, height, width)
+    rois = np.empty((0, 5), np.float32)
+    probs = np.empty((0, 1), np.float32)
+    for i in range(scores.shape[0]):
+        b, p = proposals_for_one_image(im_info[i, :], all_anchors, deltas[i], scores[i],
+                                       pre_nms_topN, post_nms_topN, nms_thresh, min_size)
+        bi = i * np.ones((b.shape[0], 1), dtype=np.float32)
+        rois = np.append(rois, np.hstack((bi, b)), axis=0)
+        probs = np.append(probs, p, axis=0)
+    return rois, probs
+
+
+def collect(roi_list, score_list, post_nms_topN=1000):
+    """collect_and_distribute_fpn_rpn_proposals.py:91-106 (stable)."""
+    rois = np.concatenate(roi_list)
+    scores = np.concatenate(score_list).squeeze(axis=1)
+    inds = np.argsort(-scores, kind="stable")[:post_nms_topN]
+    return rois[inds, :]
+
+
+def map_rois_to_fpn_levels(rois, k_min, k_max, s0=224, lvl0=4):
+    """lib/utils/fpn.py:11-28 (float32 arithmetic as numpy evaluates it)."""
+    w = rois[:, 2] - rois[:, 0] + 1
+    h = rois[:, 3] - rois[:, 1] + 1
+    areas = w * h
+    areas[areas < 0] = 0
+    s = np.sqrt(areas)
+    lv = np.floor(lvl0 + np.log2(s / s0 + 1e-6))
+    return np.clip(lv, k_min, k_max)
+
+
+def distribute(rois, lvl_min=2, lvl_max=5, prefix="rois"):
+    """distribute() (collect_and_distribute...py:109-138) / add_multilevel_roi_blobs
+    (lib/utils/fpn.py:31-58): per-level rois + int32 restore index."""
+    lvls = map_rois_to_fpn_levels(rois[:, 1:5], lvl_min, lvl_max)
+    out = {prefix: rois}
+    order = np.empty((0,))
+    for lvl in range(lvl_min, lvl_max + 1):
+        idx = np.where(lvls == lvl)[0]
+        out[prefix + "_fpn" + str(lvl)] = rois[idx, :]
+        order = np.concatenate((order, idx))
+    out[prefix + "_idx_restore_int32"] = np.argsort(order, kind="stable").astype(np.int32)
+    return out
+
+
+def roi_feature_transform(blobs_in, rpn_ret, blob_rois, resolution, spatial_scales,
+                          sampling_ratio, k_min=2, k_max=5):
+    """Generalized_RCNN.roi_feature_transform, RoIAlign FPN branch
+    (lib/modeling/model_builder.py:252-303): blobs_in coarsest first."""
+    outs = []
+    for lvl in range(k_min, k_max + 1):
+        bl = blobs_in[k_max - lvl]
+        sc = spatial_scales[k_max - lvl]
+        r = rpn_ret[blob_rois + "_fpn" + str(lvl)]
+        if len(r):
+            outs.append(roi_align(bl, r, resolution, resolution, sc, sampling_ratio))
+    sh = np.concatenate(outs, axis=0)
+    return sh[rpn_ret[blob_rois + "_idx_restore_int32"].astype(np.int64)]
+
+
+# --------------------------------------------------------------------------- #
+# Detection post-processing                                                    #
+# --------------------------------------------------------------------------- #
+def box_results_with_nms_and_limit(scores, boxes, num_classes=81, score_thresh=0.05,
+                                   nms_thresh=0.5, dets_per_im=100):
+    """lib/core/test.py:733-797 with the fork's NUM_DET_PER_CLASS fix
+    (lib_vos/tools/vos_test.py:748-865, NMS_CROSS_CLASS=0, *_PRE=0)."""
+    cls_boxes = [[] for _ in range(num_classes)]
+    for j in range(1, num_classes):
+        inds = np.where(scores[:, j] >= score_thresh)[0]
+        sj = scores[inds, j]
+        bj = boxes[inds, j * 4:(j + 1) * 4]
+        dj = np.hstack((bj, sj[:, None])).astype(np.float32, copy=False)
+        keep = nms(dj, nms_thresh)
+        cls_boxes[j] = dj[keep, :]
+    if dets_per_im > 0:
+        image_scores = np.hstack([cls_boxes[j][:, -1] for j in range(1, num_classes)])
+        if len(image_scores) > dets_per_im:
+            thr = np.sort(image_scores)[-dets_per_im]
+            for j in range(1, num_classes):
+                keep = np.where(cls_boxes[j][:, -1] >= thr)[0]
+                cls_boxes[j] = cls_boxes[j][keep, :]
+    im_results = np.vstack([cls_boxes[j] for j in range(1, num_classes)])
+    return im_results[:, -1], im_results[:, :-1], cls_boxes
+
+
+def get_image_blob(im, target_scale=800, max_size=1333, stride=32):
+    """lib/utils/blob.py:37-161 at identity scale (cv2.resize is absent here; an
+    800x1333 frame has im_scale 1.0, so the resize is the identity)."""
+    im = im.astype(np.float32, copy=False) - PIXEL_MEANS
+    im = im.astype(np.float32)
+    smin, smax = min(im.shape[:2]), max(im.shape[:2])
+    scale = float(target_scale) / float(smin)
+    if np.round(scale * smax) > max_size:
+        scale = float(max_size) / float(smax)
+    if scale != 1.0:
+        raise NotImplementedError("oracle supports identity-scale frames only")
+    H = int(np.ceil(im.shape[0] / stride) * stride)
+    W = int(np.ceil(im.shape[1] / stride) * stride)
+    blob = np.zeros((1, H, W, 3), np.float32)
+    blob[0, :im.shape[0], :im.shape[1], :] = im
+    blob = blob.transpose(0, 3, 1, 2)
+    im_info = np.array([[H, W, scale]], np.float32)
+    return blob, scale, im_info

@@ -1,0 +1,367 @@
+/*
+ * oracle/roi_ops.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C, single-threaded restatement of the reference's RoI operators and of
+ * its greedy NMS, used as the parity checker for the HIP kernels in
+ * vosdetectron_amd/csrc.  Nothing in the product path links or calls this
+ * file: only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * load it (through oracle/oracle.py).
+ *
+ * Every function restates the arithmetic of one reference function, in the
+ * same evaluation order and the same floating-point types, so that it can be
+ * compared bit for bit.  Build flags: -O2 -ffp-contract=off (no FMA
+ * contraction; the reference Cython NMS is built without FMA on x86-64, and the
+ * CUDA kernels' own nvcc build would contract -- see DESIGN.md "Parity").
+ *
+ * Pinning status:
+ *   - The reference CUDA kernels cannot be built in this image (they need the
+ *     CUDA runtime headers/THC), and the Cython NMS does not compile unmodified
+ *     against numpy 2, so these restatements are pinned by analytic known
+ *     answers (bilinear exactness on affine ramps, hand-derived NMS cases, the
+ *     survey-observed tie order) rather than by executing the reference.
+ *     -> "parity unpinned" against an executed reference for these functions.
+ */
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------ */
+/* Caffe2 RoIAlign forward                                                   */
+/* lib/modeling/roi_xfrom/roi_align/src/roi_align_kernel.cu:16-63 (bilinear) */
+/* and :65-121 (ROIAlignForward).                                            */
+/* ------------------------------------------------------------------------ */
+static float caffe2_bilinear(const float *plane, int height, int width, float y,
+                             float x) {
+    /* roi_align_kernel.cu:19-22: sample entirely outside -> 0 */
+    if (y < -1.0 || y > height || x < -1.0 || x > width) return 0;
+    if (y <= 0) y = 0; /* :24-29 */
+    if (x <= 0) x = 0;
+    int y_low = (int)y, x_low = (int)x, y_high, x_high;
+    if (y_low >= height - 1) { /* :34-39 clamp to the last row */
+        y_high = y_low = height - 1;
+        y = (float)y_low;
+    } else {
+        y_high = y_low + 1;
+    }
+    if (x_low >= width - 1) { /* :41-46 */
+        x_high = x_low = width - 1;
+        x = (float)x_low;
+    } else {
+        x_high = x_low + 1;
+    }
+    float ly = y - y_low, lx = x - x_low;
+    float hy = (float)(1. - ly), hx = (float)(1. - lx); /* :50 double then float */
+    float v1 = plane[y_low * width + x_low];
+    float v2 = plane[y_low * width + x_high];
+    float v3 = plane[y_high * width + x_low];
+    float v4 = plane[y_high * width + x_high];
+    float w1 = hy * hx, w2 = hy * lx, w3 = ly * hx, w4 = ly * lx;
+    return (w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4); /* :60 left to right */
+}
+
+/* features: B x C x H x W (NCHW, contiguous) ; rois: R x 5 [b, x1, y1, x2, y2]
+ * out: R x C x ph x pw.  Mirrors ROIAlignForward's per-output-element loop. */
+void or_roi_align_fwd(const float *features, int B, int C, int H, int W,
+                      const float *rois, int R, int aligned_h, int aligned_w,
+                      float spatial_scale, int sampling_ratio, float *out) {
+    (void)B;
+    for (int n = 0; n < R; ++n) {
+        const float *r = rois + (size_t)n * 5;
+        int roi_batch_ind = (int)r[0];
+        float roi_start_w = r[1] * spatial_scale; /* :79-82 no rounding */
+        float roi_start_h = r[2] * spatial_scale;
+        float roi_end_w = r[3] * spatial_scale;
+        float roi_end_h = r[4] * spatial_scale;
+        float roi_width = fmaxf(roi_end_w - roi_start_w, 1.f); /* :85-86 */
+        float roi_height = fmaxf(roi_end_h - roi_start_h, 1.f);
+        float bin_size_h = roi_height / aligned_h;
+        float bin_size_w = roi_width / aligned_w;
+        int grid_h = (sampling_ratio > 0) ? sampling_ratio
+                                          : (int)ceilf(roi_height / aligned_h);
+        int grid_w = (sampling_ratio > 0) ? sampling_ratio
+                                          : (int)ceilf(roi_width / aligned_w);
+        const float count = (float)(grid_h * grid_w); /* :101 */
+        for (int c = 0; c < C; ++c) {
+            const float *plane =
+                features + ((size_t)roi_batch_ind * C + c) * (size_t)H * W;
+            for (int ph = 0; ph < aligned_h; ++ph) {
+                for (int pw = 0; pw < aligned_w; ++pw) {
+                    float acc = 0.f;
+                    for (int iy = 0; iy < grid_h; ++iy) { /* :104-116 */
+                        const float y = roi_start_h + ph * bin_size_h +
+                                        (iy + .5f) * bin_size_h / grid_h;
+                        for (int ix = 0; ix < grid_w; ++ix) {
+                            const float x = roi_start_w + pw * bin_size_w +
+                                            (ix + .5f) * bin_size_w / grid_w;
+                            acc += caffe2_bilinear(plane, H, W, y, x);
+                        }
+                    }
+                    acc /= count; /* :117 */
+                    out[(((size_t)n * C + c) * aligned_h + ph) * aligned_w + pw] = acc;
+                }
+            }
+        }
+    }
+}
+
+/* Caffe2 RoIAlign backward: roi_align_kernel.cu:150-193 (gradient weights) and
+ * :195-270 (ROIAlignBackward).  Serial accumulation in (n, c, ph, pw, iy, ix)
+ * order, so the sum order differs from the reference's atomics (tolerance). */
+void or_roi_align_bwd(const float *top_diff, int B, int C, int H, int W,
+                      const float *rois, int R, int aligned_h, int aligned_w,
+                      float spatial_scale, int sampling_ratio, float *bottom_diff) {
+    (void)B;
+    for (int n = 0; n < R; ++n) {
+        const float *r = rois + (size_t)n * 5;
+        int roi_batch_ind = (int)r[0];
+        float roi_start_w = r[1] * spatial_scale, roi_start_h = r[2] * spatial_scale;
+        float roi_end_w = r[3] * spatial_scale, roi_end_h = r[4] * spatial_scale;
+        float roi_width = fmaxf(roi_end_w - roi_start_w, 1.f);
+        float roi_height = fmaxf(roi_end_h - roi_start_h, 1.f);
+        float bin_size_h = roi_height / aligned_h, bin_size_w = roi_width / aligned_w;
+        int grid_h = (sampling_ratio > 0) ? sampling_ratio
+                                          : (int)ceilf(roi_height / aligned_h);
+        int grid_w = (sampling_ratio > 0) ? sampling_ratio
+                                          : (int)ceilf(roi_width / aligned_w);
+        const float count = (float)(grid_h * grid_w);
+        for (int c = 0; c < C; ++c) {
+            float *plane = bottom_diff + ((size_t)roi_batch_ind * C + c) * (size_t)H * W;
+            for (int ph = 0; ph < aligned_h; ++ph)
+                for (int pw = 0; pw < aligned_w; ++pw) {
+                    float g = top_diff[(((size_t)n * C + c) * aligned_h + ph) * aligned_w + pw];
+                    for (int iy = 0; iy < grid_h; ++iy) {
+                        const float y0 = roi_start_h + ph * bin_size_h +
+                                         (iy + .5f) * bin_size_h / grid_h;
+                        for (int ix = 0; ix < grid_w; ++ix) {
+                            float y = y0;
+                            float x = roi_start_w + pw * bin_size_w +
+                                      (ix + .5f) * bin_size_w / grid_w;
+                            if (y < -1.0 || y > H || x < -1.0 || x > W) continue;
+                            if (y <= 0) y = 0;
+                            if (x <= 0) x = 0;
+                            int y_low = (int)y, x_low = (int)x, y_high, x_high;
+                            if (y_low >= H - 1) { y_high = y_low = H - 1; y = (float)y_low; }
+                            else y_high = y_low + 1;
+                            if (x_low >= W - 1) { x_high = x_low = W - 1; x = (float)x_low; }
+                            else x_high = x_low + 1;
+                            float ly = y - y_low, lx = x - x_low;
+                            float hy = (float)(1. - ly), hx = (float)(1. - lx);
+                            float w1 = hy * hx, w2 = hy * lx, w3 = ly * hx, w4 = ly * lx;
+                            plane[y_low * W + x_low] += g * w1 / count;
+                            plane[y_low * W + x_high] += g * w2 / count;
+                            plane[y_high * W + x_low] += g * w3 / count;
+                            plane[y_high * W + x_high] += g * w4 / count;
+                        }
+                    }
+                }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* jwyang RoIAlign (legacy, lib/model/roi_align/src/roi_align_kernel.cu:15-70) */
+/* One sample per output, (P-1) bins, +1 RoI extent, fp64 weight products.   */
+/* ------------------------------------------------------------------------ */
+void or_roi_align_legacy_fwd(const float *features, int B, int C, int H, int W,
+                             const float *rois, int R, int aligned_h, int aligned_w,
+                             float spatial_scale, float *out) {
+    (void)B;
+    for (int n = 0; n < R; ++n) {
+        const float *r = rois + (size_t)n * 5;
+        /* :30 roi_batch_ind is a float; img_start is computed in float
+         * (:46) -- restated in integer arithmetic (identical while the float
+         * product is exact, i.e. below 2^24 elements per image-offset) */
+        int b = (int)r[0];
+        float roi_start_w = r[1] * spatial_scale, roi_start_h = r[2] * spatial_scale;
+        float roi_end_w = r[3] * spatial_scale, roi_end_h = r[4] * spatial_scale;
+        float roi_width = fmaxf((float)((double)(roi_end_w - roi_start_w) + 1.), 0.f);
+        float roi_height = fmaxf((float)((double)(roi_end_h - roi_start_h) + 1.), 0.f);
+        float bin_size_h = (float)(roi_height / (aligned_h - 1.));
+        float bin_size_w = (float)(roi_width / (aligned_w - 1.));
+        for (int c = 0; c < C; ++c)
+            for (int ph = 0; ph < aligned_h; ++ph)
+                for (int pw = 0; pw < aligned_w; ++pw) {
+                    float h = (float)ph * bin_size_h + roi_start_h; /* :40-41 */
+                    float w = (float)pw * bin_size_w + roi_start_w;
+                    int hstart = (int)fminf(floorf(h), (float)(H - 2));
+                    int wstart = (int)fminf(floorf(w), (float)(W - 2));
+                    size_t o = (((size_t)n * C + c) * aligned_h + ph) * aligned_w + pw;
+                    if (h < 0 || h >= H || w < 0 || w >= W) {
+                        out[o] = 0.f;
+                        continue;
+                    }
+                    float h_ratio = h - (float)hstart, w_ratio = w - (float)wstart;
+                    size_t upleft = ((size_t)b * C * H * W) + ((size_t)c * H + hstart) * W + wstart;
+                    size_t upright = upleft + 1, downleft = upleft + W, downright = downleft + 1;
+                    out[o] = (float)(features[upleft] * (1. - h_ratio) * (1. - w_ratio) +
+                                     features[upright] * (1. - h_ratio) * w_ratio +
+                                     features[downleft] * h_ratio * (1. - w_ratio) +
+                                     features[downright] * h_ratio * w_ratio);
+                }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* RoIPool forward: lib/model/roi_pooling/src/roi_pooling_kernel.cu:24-93    */
+/* (the CUDA semantics; the CPU C file initialises with -1, not -FLT_MAX).   */
+/* ------------------------------------------------------------------------ */
+void or_roi_pool_fwd(const float *features, int B, int C, int H, int W,
+                     const float *rois, int R, int pooled_h, int pooled_w,
+                     float spatial_scale, float *out, int32_t *argmax) {
+    (void)B;
+    for (int n = 0; n < R; ++n) {
+        const float *r = rois + (size_t)n * 5;
+        int roi_batch_ind = (int)r[0];
+        int roi_start_w = (int)roundf(r[1] * spatial_scale); /* :45-48 */
+        int roi_start_h = (int)roundf(r[2] * spatial_scale);
+        int roi_end_w = (int)roundf(r[3] * spatial_scale);
+        int roi_end_h = (int)roundf(r[4] * spatial_scale);
+        int roi_width = (int)fmaxf((float)(roi_end_w - roi_start_w + 1), 1.f);
+        int roi_height = (int)fmaxf((float)(roi_end_h - roi_start_h + 1), 1.f);
+        float bin_size_h = (float)roi_height / (float)pooled_h;
+        float bin_size_w = (float)roi_width / (float)pooled_w;
+        for (int c = 0; c < C; ++c)
+            for (int ph = 0; ph < pooled_h; ++ph)
+                for (int pw = 0; pw < pooled_w; ++pw) {
+                    int hstart = (int)floorf((float)ph * bin_size_h);
+                    int wstart = (int)floorf((float)pw * bin_size_w);
+                    int hend = (int)ceilf((float)(ph + 1) * bin_size_h);
+                    int wend = (int)ceilf((float)(pw + 1) * bin_size_w);
+                    hstart = (int)fminf(fmaxf((float)(hstart + roi_start_h), 0.f), (float)H);
+                    hend = (int)fminf(fmaxf((float)(hend + roi_start_h), 0.f), (float)H);
+                    wstart = (int)fminf(fmaxf((float)(wstart + roi_start_w), 0.f), (float)W);
+                    wend = (int)fminf(fmaxf((float)(wend + roi_start_w), 0.f), (float)W);
+                    int is_empty = (hend <= hstart) || (wend <= wstart);
+                    float maxval = is_empty ? 0.f : -FLT_MAX;
+                    int maxidx = -1;
+                    size_t off = ((size_t)roi_batch_ind * C + c) * (size_t)H * W;
+                    for (int h = hstart; h < hend; ++h)
+                        for (int w = wstart; w < wend; ++w) {
+                            float v = features[off + (size_t)h * W + w];
+                            if (v > maxval) {
+                                maxval = v;
+                                maxidx = (int)(off + (size_t)h * W + w);
+                            }
+                        }
+                    size_t o = (((size_t)n * C + c) * pooled_h + ph) * pooled_w + pw;
+                    out[o] = maxval;
+                    if (argmax) argmax[o] = maxidx;
+                }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* RoICrop bilinear sampler forward:                                        */
+/* lib/model/roi_crop/src/roi_crop_cuda_kernel.cu:11-21 (getTopLeft),        */
+/* :47-109 (bilinearSamplingFromGrid), launcher :201-255 (roiPerImage=ob/ib) */
+/* input B x C x H x W, grid R x G x G x 2 in (y, x) order, out R x C x G x G */
+/* (caller zero-fills: taps all outside leave the zero, :93-94).            */
+/* ------------------------------------------------------------------------ */
+static void top_left(float x, int width, int *point, float *weight) {
+    float xcoord = (x + 1) * (width - 1) / 2;
+    *point = (int)floorf(xcoord);
+    *weight = 1 - (xcoord - *point);
+}
+static int between(int v, int lo, int hi) { return v >= lo && v <= hi; }
+
+void or_roi_crop_fwd(const float *input, int B, int C, int H, int W,
+                     const float *grid, int R, int GH, int GW, float *out) {
+    int roi_per_image = R / B;
+    for (int b = 0; b < R; ++b) {
+        int b_in = b / roi_per_image;
+        for (int c = 0; c < C; ++c)
+            for (int yo = 0; yo < GH; ++yo)
+                for (int xo = 0; xo < GW; ++xo) {
+                    const float *g = grid + (((size_t)b * GH + yo) * GW + xo) * 2;
+                    float yf = g[0], xf = g[1];
+                    int yTL, xTL;
+                    float yW, xW;
+                    top_left(xf, W, &xTL, &xW);
+                    top_left(yf, H, &yTL, &yW);
+                    int tl = between(xTL, 0, W - 1) && between(yTL, 0, H - 1);
+                    int tr = between(xTL + 1, 0, W - 1) && between(yTL, 0, H - 1);
+                    int bl = between(xTL, 0, W - 1) && between(yTL + 1, 0, H - 1);
+                    int br = between(xTL + 1, 0, W - 1) && between(yTL + 1, 0, H - 1);
+                    if (!tl && !tr && !bl && !br) continue;
+                    const float *plane = input + ((size_t)b_in * C + c) * (size_t)H * W;
+                    float vTL = tl ? plane[(size_t)yTL * W + xTL] : 0.f;
+                    float vTR = tr ? plane[(size_t)yTL * W + xTL + 1] : 0.f;
+                    float vBL = bl ? plane[(size_t)(yTL + 1) * W + xTL] : 0.f;
+                    float vBR = br ? plane[(size_t)(yTL + 1) * W + xTL + 1] : 0.f;
+                    float v = xW * yW * vTL + (1 - xW) * yW * vTR + xW * (1 - yW) * vBL +
+                              (1 - xW) * (1 - yW) * vBR;
+                    out[(((size_t)b * C + c) * GH + yo) * GW + xo] = v;
+                }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Greedy NMS with cython_nms semantics: lib/utils/cython_nms.pyx:37-87.     */
+/* areas (x2-x1+1)(y2-y1+1) in float32; processing order = scores.argsort() */
+/* reversed, with a STABLE argsort (ties: higher index first); suppress when */
+/* ovr >= thresh; returns kept indices ascending.  Returns the keep count.   */
+/* ------------------------------------------------------------------------ */
+static const float *g_sort_scores;
+static int cmp_stable_asc(const void *a, const void *b) {
+    int ia = *(const int *)a, ib = *(const int *)b;
+    float sa = g_sort_scores[ia], sb = g_sort_scores[ib];
+    if (sa < sb) return -1;
+    if (sa > sb) return 1;
+    return (ia > ib) - (ia < ib);
+}
+static inline float cy_max(float a, float b) { return a >= b ? a : b; }
+static inline float cy_min(float a, float b) { return a <= b ? a : b; }
+
+int or_nms(const float *dets, int n, int stride, float thresh, int64_t *keep) {
+    if (n <= 0) return 0;
+    float *x1 = malloc(sizeof(float) * 6 * (size_t)n);
+    float *y1 = x1 + n, *x2 = y1 + n, *y2 = x2 + n, *sc = y2 + n, *areas = sc + n;
+    int *order = malloc(sizeof(int) * (size_t)n);
+    unsigned char *sup = calloc((size_t)n, 1);
+    for (int i = 0; i < n; ++i) {
+        x1[i] = dets[(size_t)i * stride + 0];
+        y1[i] = dets[(size_t)i * stride + 1];
+        x2[i] = dets[(size_t)i * stride + 2];
+        y2[i] = dets[(size_t)i * stride + 3];
+        sc[i] = dets[(size_t)i * stride + 4];
+        areas[i] = (x2[i] - x1[i] + 1) * (y2[i] - y1[i] + 1); /* :44 */
+        order[i] = i;
+    }
+    g_sort_scores = sc;
+    qsort(order, (size_t)n, sizeof(int), cmp_stable_asc); /* :45 argsort */
+    for (int a = 0, b = n - 1; a < b; ++a, --b) {         /* [::-1] */
+        int t = order[a];
+        order[a] = order[b];
+        order[b] = t;
+    }
+    for (int _i = 0; _i < n; ++_i) { /* :63-85 */
+        int i = order[_i];
+        if (sup[i]) continue;
+        float ix1 = x1[i], iy1 = y1[i], ix2 = x2[i], iy2 = y2[i], iarea = areas[i];
+        for (int _j = _i + 1; _j < n; ++_j) {
+            int j = order[_j];
+            if (sup[j]) continue;
+            float xx1 = cy_max(ix1, x1[j]);
+            float yy1 = cy_max(iy1, y1[j]);
+            float xx2 = cy_min(ix2, x2[j]);
+            float yy2 = cy_min(iy2, y2[j]);
+            float w = cy_max(0.0f, xx2 - xx1 + 1);
+            float h = cy_max(0.0f, yy2 - yy1 + 1);
+            float inter = w * h;
+            float ovr = inter / (iarea + areas[j] - inter);
+            if (ovr >= thresh) sup[j] = 1;
+        }
+    }
+    int k = 0;
+    for (int i = 0; i < n; ++i)
+        if (!sup[i]) keep[k++] = i; /* :87 np.where(suppressed == 0) */
+    free(x1);
+    free(order);
+    free(sup);
+    return k;
+}
+
+/* Soft-NMS restatement (lib/utils/cython_nms.pyx:98-203) is not on the
+ * default inference path (TEST.SOFT_NMS.ENABLED = False, config.py:359). */

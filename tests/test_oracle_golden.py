@@ -1,0 +1,64 @@
+"""Pin the oracle (oracle/oracle.py) against fixtures produced by executing the
+reference's own Python (tools/gen_goldens.py) and the reference-authored anchor
+known-answer table (lib/modeling/generate_anchors.py:26-51)."""
+import numpy as np
+
+from oracle import oracle as orc
+
+
+def test_anchor_kat(golden):
+    g = golden("anchors")
+    # The KAT in the comment is 1-based (py-faster-rcnn); the code is 0-based.
+    assert np.array_equal(g["kat_comment"] - 1, g["kat_ref"])
+    ours = orc.generate_anchors(stride=16, sizes=(128, 256, 512), aspect_ratios=(0.5, 1, 2))
+    assert np.array_equal(ours, g["kat_ref"])
+    for lvl in range(2, 7):
+        assert np.array_equal(orc.fpn_level_anchors(lvl), g["fpn%d" % lvl])
+
+
+def test_bbox_transform_and_clip(golden):
+    g = golden("bbox_transform")
+    out1 = orc.bbox_transform(g["boxes"].astype(np.float64), g["deltas1"], (1., 1., 1., 1.))
+    assert out1.dtype == np.float32
+    assert np.array_equal(out1, g["out1"])
+    out81 = orc.bbox_transform(g["boxes"][:128], g["deltas81"], (10., 10., 5., 5.))
+    assert np.array_equal(out81, g["out81"])
+    im_info = np.array([800, 1344, 1.0], np.float32)
+    assert np.array_equal(orc.clip_tiled_boxes(out1.copy(), im_info[:2]), g["clip1"])
+    assert np.array_equal(orc.clip_tiled_boxes(out81.copy(), (800, 1333, 3)), g["clip81"])
+
+
+def test_fpn_level_map(golden):
+    g = golden("fpn_levels")
+    assert np.array_equal(orc.map_rois_to_fpn_levels(g["boxes"], 2, 5), g["lvls"])
+
+
+def test_generate_proposals(golden):
+    g = golden("proposals")
+    for lvl in range(2, 7):
+        anchors = orc.fpn_level_anchors(lvl)
+        rois, probs = orc.generate_proposals(anchors, 1. / 2 ** lvl, g["probs_fpn%d" % lvl],
+                                             g["deltas_fpn%d" % lvl], g["im_info"])
+        assert np.array_equal(rois, g["rois_fpn%d" % lvl]), lvl
+        assert np.array_equal(probs, g["roi_probs_fpn%d" % lvl]), lvl
+
+
+def test_collect_distribute(golden):
+    g = golden("proposals")
+    rois = [g["rois_fpn%d" % l] for l in range(2, 7)]
+    probs = [g["roi_probs_fpn%d" % l] for l in range(2, 7)]
+    c = golden("collect_distribute")
+    col = orc.collect(rois, probs, 1000)
+    assert np.array_equal(col, c["collected"])
+    d = orc.distribute(col)
+    for k in ["rois", "rois_fpn2", "rois_fpn3", "rois_fpn4", "rois_fpn5",
+              "rois_idx_restore_int32"]:
+        assert np.array_equal(d[k], c[k]), k
+
+
+def test_multilevel_mask_rois(golden):
+    g = golden("multilevel_mask_rois")
+    d = orc.distribute(g["mask_rois"], prefix="mask_rois")
+    for lvl in range(2, 6):
+        assert np.array_equal(d["mask_rois_fpn%d" % lvl], g["mask_rois_fpn%d" % lvl])
+    assert np.array_equal(d["mask_rois_idx_restore_int32"], g["mask_rois_idx_restore_int32"])

@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by importing the REFERENCE's
+own Python (read-only, from /root/reference) in this container.
+
+Only data (inputs + expected outputs) is written; no reference source is copied.
+Runs here only -- /root/reference does not exist on the GPU box; the committed
+.npz fixtures travel instead.
+
+Runtime-only import shims (nothing under /root/reference is modified):
+  * ``np.float`` / ``np.int`` aliases (removed in numpy >= 1.24; used by
+    generate_anchors.py:63,72, core/test.py:904-905);
+  * ``torch._six`` stub (lib/nn/parallel/scatter_gather.py:7);
+  * ``utils.cython_nms`` / ``utils.cython_bbox``: the vendored Cython does not
+    build against numpy 2, so ``nms`` is bound to the oracle's C restatement
+    (oracle/roi_ops.c).  Fixtures that run through NMS therefore pin everything
+    around the NMS call (top-k, decode, clip, filter, keep[:post]) to the
+    reference, and the NMS itself to the oracle.  This is recorded in
+    DESIGN.md ("Parity").
+  * ``cv2`` / ``pycocotools`` stubs (imported at module level by core/test.py,
+    never called on the functions used here).
+
+Usage: python tools/gen_goldens.py   (writes tests/golden/*.npz)
+"""
+import os
+import sys
+import types
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+OUT = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, REPO)
+
+
+def install_shims():
+    np.float = float
+    np.int = int
+    sys.path.insert(0, os.path.join(REF, "lib"))
+    six_mod = types.ModuleType("torch._six")
+    six_mod.string_classes = (str, bytes)
+    six_mod.int_classes = int
+    sys.modules["torch._six"] = six_mod
+    import torch.utils.data.dataloader as dl
+    if not hasattr(dl, "numpy_type_map"):
+        dl.numpy_type_map = {}
+    from oracle import oracle as orc
+    cy_nms = types.ModuleType("utils.cython_nms")
+    cy_nms.nms = lambda dets, thresh: orc.nms(dets, thresh)
+    sys.modules["utils.cython_nms"] = cy_nms
+    cy_bbox = types.ModuleType("utils.cython_bbox")
+    cy_bbox.bbox_overlaps = None  # not on the inference path
+    sys.modules["utils.cython_bbox"] = cy_bbox
+    cv2 = types.ModuleType("cv2")
+    cv2.INTER_LINEAR = 1
+    sys.modules["cv2"] = cv2
+    class _Stub(types.ModuleType):
+        def __getattr__(self, attr):  # any attribute: an inert placeholder
+            if attr.startswith("__"):
+                raise AttributeError(attr)
+            return type(attr, (), {})
+    for name in ("pycocotools", "pycocotools.mask", "pycocotools.coco",
+                 "pycocotools.cocoeval", "scipy.misc", "imdb", "imdb.vos",
+                 "imdb.vos.davis_db", "datasets.json_dataset"):
+        sys.modules[name] = _Stub(name)
+    sys.modules["imdb.vos"].davis_db = sys.modules["imdb.vos.davis_db"]
+    import yaml
+    _load = yaml.load
+    yaml.load = lambda s, Loader=yaml.SafeLoader: _load(s, Loader=Loader)
+
+
+def distinct_scores(rng, n):
+    """Tie-free scores in (0, 1): a random permutation of n distinct float32s."""
+    vals = np.linspace(0.001, 0.999, n, dtype=np.float64).astype(np.float32)
+    vals = np.unique(vals)
+    assert vals.size == n
+    return rng.permutation(vals).astype(np.float32)
+
+
+def main():
+    install_shims()
+    from core.config import cfg
+    from modeling.generate_anchors import generate_anchors
+    import utils.boxes as box_utils
+    import utils.fpn as fpn_utils
+    from modeling.generate_proposals import GenerateProposalsOp
+    import modeling.collect_and_distribute_fpn_rpn_proposals as cdp
+
+    os.makedirs(OUT, exist_ok=True)
+    rng = np.random.default_rng(20241015)
+
+    # ---- anchors: reference output + the comment KAT (generate_anchors.py:26-51)
+    kat_comment = np.array([[-83, -39, 100, 56], [-175, -87, 192, 104], [-359, -183, 376, 200],
+                            [-55, -55, 72, 72], [-119, -119, 136, 136], [-247, -247, 264, 264],
+                            [-35, -79, 52, 96], [-79, -167, 96, 184], [-167, -343, 184, 360]],
+                           np.float64)
+    kat_ref = generate_anchors(stride=16, sizes=(128, 256, 512), aspect_ratios=(0.5, 1, 2))
+    lvl_anchors = {}
+    for lvl in range(2, 7):
+        lvl_anchors["fpn%d" % lvl] = generate_anchors(
+            stride=2. ** lvl, sizes=(32 * 2. ** (lvl - 2),), aspect_ratios=(0.5, 1, 2))
+    np.savez(os.path.join(OUT, "anchors.npz"), kat_comment=kat_comment, kat_ref=kat_ref,
+             **lvl_anchors)
+
+    # ---- bbox_transform + clip_tiled_boxes (boxes.py:138-205)
+    N = 512
+    xy = rng.uniform(-50, 1300, (N, 2))
+    wh = rng.uniform(0.5, 400, (N, 2))
+    boxes = np.hstack([xy, xy + wh]).astype(np.float32)
+    deltas1 = rng.normal(0, 1.0, (N, 4)).astype(np.float32)
+    deltas1[:8, 2:] = 9.0  # exercise BBOX_XFORM_CLIP
+    deltas81 = rng.normal(0, 2.0, (128, 4 * 81)).astype(np.float32)
+    cfg.immutable(False) if hasattr(cfg, "immutable") else None
+    out1 = box_utils.bbox_transform(boxes.astype(np.float64), deltas1, (1.0, 1.0, 1.0, 1.0))
+    out81 = box_utils.bbox_transform(boxes[:128], deltas81, (10., 10., 5., 5.))
+    im_info = np.array([800, 1344, 1.0], np.float32)
+    clip1 = box_utils.clip_tiled_boxes(out1.copy(), im_info[:2])
+    clip81 = box_utils.clip_tiled_boxes(out81.copy(), (800, 1333, 3))
+    np.savez(os.path.join(OUT, "bbox_transform.npz"), boxes=boxes, deltas1=deltas1,
+             deltas81=deltas81, out1=out1, out81=out81, clip1=clip1, clip81=clip81)
+
+    # ---- map_rois_to_fpn_levels (utils/fpn.py:11-28), incl. near-boundary sizes
+    s = np.concatenate([np.exp(rng.uniform(np.log(4), np.log(1400), 2000)),
+                        224. * 2. ** np.arange(-3, 3) - 1, 224. * 2. ** np.arange(-3, 3)])
+    a = np.exp(rng.uniform(np.log(0.5), np.log(2), s.size))
+    w, h = s / np.sqrt(a), s * np.sqrt(a)
+    cx, cy = rng.uniform(0, 1333, s.size), rng.uniform(0, 800, s.size)
+    lv_boxes = np.stack([cx - w / 2, cy - h / 2, cx + w / 2 - 1, cy + h / 2 - 1], 1).astype(np.float32)
+    square = np.array(224. * 2. ** np.arange(-3, 3), np.float32)
+    sq = np.stack([np.zeros_like(square), np.zeros_like(square), square - 1, square - 1], 1)
+    lv_boxes = np.concatenate([lv_boxes, sq]).astype(np.float32)
+    lvls = fpn_utils.map_rois_to_fpn_levels(lv_boxes, 2, 5)
+    np.savez(os.path.join(OUT, "fpn_levels.npz"), boxes=lv_boxes, lvls=lvls)
+
+    # ---- GenerateProposalsOp per FPN level (generate_proposals.py:20-168)
+    cfg.TEST.RPN_PRE_NMS_TOP_N = 1000
+    cfg.TEST.RPN_POST_NMS_TOP_N = 1000
+    cfg.TEST.RPN_NMS_THRESH = 0.7
+    cfg.TEST.RPN_MIN_SIZE = 0
+    prop = {}
+    im_info = np.array([[800, 1344, 1.0]], np.float32)
+    shapes = {2: (100, 168), 3: (50, 84), 4: (25, 42), 5: (13, 21), 6: (7, 11)}
+    per_level_rois, per_level_probs = [], []
+    # one pool of distinct values so scores are tie-free across levels too
+    total = sum(3 * H * W for (H, W) in shapes.values())
+    pool, used = distinct_scores(rng, total), 0
+    for lvl, (H, W) in shapes.items():
+        anchors = generate_anchors(stride=2. ** lvl, sizes=(32 * 2. ** (lvl - 2),),
+                                   aspect_ratios=(0.5, 1, 2))
+        A = anchors.shape[0]
+        probs = pool[used:used + A * H * W].reshape(1, A, H, W)
+        used += A * H * W
+        deltas = rng.normal(0, 0.3, (1, 4 * A, H, W)).astype(np.float32)
+        op = GenerateProposalsOp(anchors, 1. / 2 ** lvl)
+        op.eval()
+        import torch
+        rois, rprobs = op(torch.from_numpy(probs), torch.from_numpy(deltas), torch.from_numpy(im_info))
+        prop["probs_fpn%d" % lvl] = probs
+        prop["deltas_fpn%d" % lvl] = deltas
+        prop["rois_fpn%d" % lvl] = rois
+        prop["roi_probs_fpn%d" % lvl] = rprobs
+        per_level_rois.append(rois)
+        per_level_probs.append(rprobs)
+    prop["im_info"] = im_info
+    np.savez(os.path.join(OUT, "proposals.npz"), **prop)
+
+    # ---- collect + distribute (collect_and_distribute...py:91-138)
+    cfg.FPN.RPN_COLLECT_SCALE = 1
+    cfg.FPN.RPN_MIN_LEVEL, cfg.FPN.RPN_MAX_LEVEL = 2, 6
+    cfg.FPN.ROI_MIN_LEVEL, cfg.FPN.ROI_MAX_LEVEL = 2, 5
+    cfg.FPN.FPN_ON = True
+    cfg.FPN.MULTILEVEL_ROIS = True
+    cfg.MODEL.KEYPOINTS_ON = False
+    cfg.MODEL.MASK_ON = False
+    # collect() needs the score inputs tie-free across levels too
+    rois_c = cdp.collect(per_level_rois + per_level_probs, False)
+    dist = cdp.distribute(rois_c, None)
+    np.savez(os.path.join(OUT, "collect_distribute.npz"), collected=rois_c,
+             **{k: np.asarray(v) for k, v in dist.items()})
+
+    # ---- add_multilevel_roi_blobs (mask rois path, utils/fpn.py:31-58)
+    blobs = {}
+    mrois = np.hstack([np.zeros((100, 1), np.float32), lv_boxes[:100]]).astype(np.float32)
+    lv = fpn_utils.map_rois_to_fpn_levels(mrois[:, 1:5], 2, 5)
+    fpn_utils.add_multilevel_roi_blobs(blobs, "mask_rois", mrois, lv, 2, 5)
+    np.savez(os.path.join(OUT, "multilevel_mask_rois.npz"), mask_rois=mrois,
+             **{k: np.asarray(v) for k, v in blobs.items()})
+
+    print("wrote", sorted(os.listdir(OUT)))
+
+
+if __name__ == "__main__":
+    main()
