@@ -1,0 +1,211 @@
+/*
+ * vosdet.h -- C ABI of the MI355X (gfx950) per-frame Mask R-CNN hot path.
+ *
+ * Library: vosdetectron_amd/libvosdet.so (built by __graft_entry__.build()).
+ * Plain C: raw device pointers, sizes and an explicit stream (a hipStream_t
+ * passed as void*, NULL = the null stream).  No torch types.  Every call is
+ * asynchronous on `stream`, performs no allocation, no host<->device copy and
+ * no synchronisation (graph-capturable), and returns a status code instead of
+ * the reference's fprintf + exit(-1) (roi_align_kernel.cu:135-139).
+ *
+ * Each entry point cites the reference interface it replaces.  Numerics follow
+ * the reference functions cited in the kernel sources; see DESIGN.md.
+ */
+#ifndef VOSDET_H_
+#define VOSDET_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VD_MAX_LEVELS 5
+
+enum {
+    VD_OK = 0,
+    VD_ERR_ARG = 1,       /* bad argument (e.g. rois row width != 5) */
+    VD_ERR_SHAPE = 2,     /* shape outside what the kernel supports */
+    VD_ERR_LAUNCH = 3,    /* kernel launch failed */
+    VD_ERR_WORKSPACE = 4  /* workspace too small */
+};
+
+enum { VD_LAYOUT_NCHW = 0, VD_LAYOUT_NHWC = 1 };
+
+int vd_version(void);
+const char *vd_status_string(int status);
+
+/* ---------------------------------------------------------------------------
+ * RoIAlign (Caffe2-exact).  Replaces
+ *   int roi_align_forward_cuda(int aligned_height, int aligned_width,
+ *       float spatial_scale, int sampling_ratio, THCudaTensor *features,
+ *       THCudaTensor *rois, THCudaTensor *output)
+ *   lib/modeling/roi_xfrom/roi_align/src/roi_align_cuda.h:1-2, .c:7-40.
+ * features: B x C x H x W fp32 NCHW contiguous; rois: num_rois x roi_cols fp32
+ * [batch, x1, y1, x2, y2] in input-image coordinates; output: num_rois x C x
+ * aligned_height x aligned_width (written entirely).  roi_cols != 5 ->
+ * VD_ERR_ARG (the reference silently returns 0 with the output untouched).
+ * ------------------------------------------------------------------------- */
+int vd_roi_align_forward(int aligned_height, int aligned_width, float spatial_scale,
+                         int sampling_ratio, const float *features, int B, int C, int H, int W,
+                         const float *rois, int num_rois, int roi_cols, float *output,
+                         void *stream);
+
+/* Replaces roi_align_backward_cuda (roi_align_cuda.h:4-5, .c:42-76).
+ * bottom_grad (B x C x H x W) must be zero-filled by the caller (as the
+ * reference's RoIAlignFunction.backward does, functions/roi_align.py:40-45);
+ * contributions are accumulated with fp32 atomics. */
+int vd_roi_align_backward(int aligned_height, int aligned_width, float spatial_scale,
+                          int sampling_ratio, const float *top_grad, int B, int C, int H, int W,
+                          const float *rois, int num_rois, int roi_cols, float *bottom_grad,
+                          void *stream);
+
+/* Multi-level FPN RoIAlign: the whole per-level loop + cat + unshuffle of
+ * Generalized_RCNN.roi_feature_transform (lib/modeling/model_builder.py:252-303)
+ * in one launch.  Level l of the pyramid is levels[l]; roi r is pooled from
+ * levels[roi_level[r]] (roi_level == NULL -> level 0) and written to output
+ * row r, i.e. already in the order the reference restores with
+ * `_idx_restore_int32`.  layout: VD_LAYOUT_NHWC (B x H x W x C, the product
+ * layout; C % 4 == 0) or VD_LAYOUT_NCHW.  roi_order (optional, NHWC with a
+ * pooled size of 7, 14 or 28): a permutation that only changes the order in
+ * which RoIs are scheduled (locality), never the output placement. */
+typedef struct {
+    const float *data;
+    int H;
+    int W;
+    float spatial_scale;
+} VdFeatLevel;
+
+int vd_roi_align_fpn_forward(const VdFeatLevel *levels, int num_levels, int B, int C, int layout,
+                             const float *rois, const int32_t *roi_level,
+                             const int32_t *roi_order, int num_rois, int aligned_height,
+                             int aligned_width, int sampling_ratio, float *output, void *stream);
+
+/* jwyang RoIAlign (legacy, lib/model/roi_align).  Replaces
+ * roi_align_forward_cuda(int aligned_height, int aligned_width, float
+ * spatial_scale, THCudaTensor *features, THCudaTensor *rois, THCudaTensor
+ * *output)  lib/model/roi_align/src/roi_align_cuda.c. */
+int vd_roi_align_legacy_forward(int aligned_height, int aligned_width, float spatial_scale,
+                                const float *features, int B, int C, int H, int W,
+                                const float *rois, int num_rois, float *output, void *stream);
+
+/* RoIPool.  Replaces roi_pooling_forward_cuda(int pooled_height, int
+ * pooled_width, float spatial_scale, THCudaTensor *features, THCudaTensor
+ * *rois, THCudaTensor *output, THCudaIntTensor *argmax)
+ * lib/model/roi_pooling/src/roi_pooling_cuda.c:7.  argmax may be NULL. */
+int vd_roi_pool_forward(int pooled_height, int pooled_width, float spatial_scale,
+                        const float *features, int B, int C, int H, int W, const float *rois,
+                        int num_rois, float *output, int32_t *argmax, void *stream);
+/* Replaces roi_pooling_backward_cuda (roi_pooling_cuda.c): scatter top_grad
+ * into the zero-filled bottom_grad at argmax (fp32 atomics). */
+int vd_roi_pool_backward(const float *top_grad, const int32_t *argmax, int64_t num_outputs,
+                         float *bottom_grad, void *stream);
+
+/* RoICrop bilinear sampler.  Replaces BilinearSamplerBHWD_updateOutput_cuda(
+ * THCudaTensor *inputImages, THCudaTensor *grids, THCudaTensor *output)
+ * lib/model/roi_crop/src/roi_crop_cuda.c:15.  input B x C x H x W, grid
+ * R x GH x GW x 2 in (y, x) order in [-1, 1]; output R x C x GH x GW must be
+ * zero-filled by the caller (samples with every tap outside keep the zero). */
+int vd_roi_crop_forward(const float *input, int B, int C, int H, int W, const float *grid_yx,
+                        int num_rois, int GH, int GW, float *output, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * NMS with the semantics of the NMS the reference executes,
+ * utils.boxes.nms -> cython_nms.nms (lib/utils/boxes.py:329-333,
+ * lib/utils/cython_nms.pyx:37-87): dets n x det_stride fp32 [x1,y1,x2,y2,score,..],
+ * processing order score-descending (ties: higher index first), suppression
+ * when IoU (+1 convention) >= thresh, kept indices written ascending to
+ * keep_out (int64), their count to *num_out (device int32).  Also replaces the
+ * unused GPU path nms_cuda(THCudaIntTensor *keep_out, THCudaTensor *boxes,
+ * THCudaIntTensor *num_out, float thresh)  lib/model/nms/src/nms_cuda.c:8-19.
+ * n <= 8192. */
+size_t vd_nms_workspace_size(int n);
+int vd_nms(const float *dets, int n, int det_stride, float thresh, int64_t *keep_out,
+           int32_t *num_out, void *workspace, size_t workspace_bytes, void *stream);
+
+/* FPN level of each RoI: utils/fpn.py:11-28 map_rois_to_fpn_levels
+ * (floor(lvl0 + log2(sqrt(area)/s0 + 1e-6)) clipped to [k_min, k_max]).
+ * rois: R x roi_stride, the box at columns [col0, col0+4). */
+int vd_map_rois_to_fpn_levels(const float *rois, int roi_stride, int col0, int R, int k_min,
+                              int k_max, float canonical_scale, float canonical_level,
+                              int32_t *lvl_out, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * RPN proposals for all FPN levels and images in one launch: per (image,
+ * level) GenerateProposalsOp.forward / proposals_for_one_image
+ * (lib/modeling/generate_proposals.py:20-168): top pre_nms_topN by score,
+ * anchor shift + bbox_transform (boxes.py:156-205), clip to im_info
+ * (boxes.py:138-153), _filter_boxes (:171-182), NMS, keep[:post_nms_topN].
+ * cls_prob: N x A x H x W, bbox_pred: N x 4A x H x W (conv outputs, NCHW),
+ * anchors: A x 4 float64 (generate_anchors.py), im_info: N x 3 device fp32.
+ * Outputs per (image i, level l), slot base (i*num_levels + l)*post_nms_topN:
+ * rois_out [.][5] = (i, x1, y1, x2, y2), probs_out [.], counts_out[i*L+l].
+ * pre_nms_topN <= 2048 per level. */
+typedef struct {
+    const float *cls_prob;
+    const float *bbox_pred;
+    const double *anchors;
+    int A;
+    int H;
+    int W;
+    float spatial_scale;
+} VdRpnLevel;
+
+size_t vd_generate_proposals_workspace_size(const VdRpnLevel *levels, int num_levels,
+                                            int num_images, int pre_nms_topN);
+int vd_generate_proposals(const VdRpnLevel *levels, int num_levels, int num_images,
+                          const float *im_info, int pre_nms_topN, int post_nms_topN,
+                          float nms_thresh, float min_size, float *rois_out, float *probs_out,
+                          int32_t *counts_out, void *workspace, size_t workspace_bytes,
+                          void *stream);
+
+/* collect() + distribute() of CollectAndDistributeFpnRpnProposalsOp at
+ * inference (lib/modeling/collect_and_distribute_fpn_rpn_proposals.py:91-138),
+ * per image: concatenate the per-level proposals (level-major), keep the top
+ * post_nms_topN by score (ties: lower concatenation index first), and give
+ * each kept RoI its FPN level (utils/fpn.py:11-28).  Inputs are the outputs of
+ * vd_generate_proposals (level_cap = its post_nms_topN).  Outputs per image i:
+ * rois_out[i*post_nms_topN + r][5], lvl_out[.] (level index k - k_min),
+ * count_out[i]. */
+int vd_collect_distribute(const float *level_rois, const float *level_probs,
+                          const int32_t *level_counts, int num_levels, int level_cap,
+                          int num_images, int post_nms_topN, int k_min, int k_max,
+                          float *rois_out, int32_t *lvl_out, int32_t *count_out, void *stream);
+
+/* Box-head post-processing for each image: im_detect_bbox's decode + clip
+ * (lib/core/test.py:157-184; bbox_transform with BBOX_REG_WEIGHTS, clip to the
+ * original image) followed by box_results_with_nms_and_limit (test.py:733-797;
+ * fork fix lib_vos/tools/vos_test.py:748-865): per class j >= 1 score >=
+ * score_thresh, NMS, then the top dets_per_im over all classes (score >= the
+ * dets_per_im-th largest).  rois: num_images x R_cap x 5 (first roi_count[i]
+ * valid), cls_prob: . x R_cap x K, bbox_pred: . x R_cap x 4K, im_scale[i],
+ * im_hw[i] = original (height, width) as int32.  Outputs per image i (det_cap
+ * slots): dets_out[.][5] = (x1, y1, x2, y2, score) ordered by class then
+ * proposal index (np.vstack order), det_cls_out[.] class id,
+ * det_count_out[i]. */
+size_t vd_box_detections_workspace_size(int R_cap, int num_images, int num_classes);
+int vd_box_detections(const float *rois, const float *cls_prob, const float *bbox_pred,
+                      const int32_t *roi_count, int R_cap, int num_images, int num_classes,
+                      const float *im_scale, const int32_t *im_hw, float score_thresh,
+                      float nms_thresh, int dets_per_im, const float *bbox_reg_weights,
+                      int det_cap, float *dets_out, int32_t *det_cls_out,
+                      int32_t *det_count_out, void *workspace, size_t workspace_bytes,
+                      void *stream);
+
+/* Frame preparation, lib/utils/blob.py:37-114 at identity scale: u8 BGR frames
+ * (F x H x W x 3) -> fp32 blob minus PIXEL_MEANS, zero-padded to Hp x Wp
+ * (multiples of FPN.COARSEST_STRIDE).  lut[3*256] = float32(u - mean_c) for
+ * every byte value (numpy's float64 subtraction, then the float32 store).
+ * nhwc = 0 -> F x 3 x Hp x Wp, 1 -> F x Hp x Wp x 3. */
+int vd_image_to_blob(const uint8_t *frames, int F, int H, int W, const float *lut, int Hp,
+                     int Wp, int nhwc, float *blob, void *stream);
+
+/* B x C x H x W -> B x H x W x C (pyramid relayout for the NHWC RoIAlign). */
+int vd_nchw_to_nhwc(const float *in, int B, int C, int H, int W, float *out, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VOSDET_H_ */

@@ -1,0 +1,55 @@
+"""The C-ABI library loads and exports every entry point include/vosdet.h
+declares (no compute: this runs on the CPU host too)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "vosdet.h")
+
+
+def declared():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(vd_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_declares_entry_points():
+    names = declared()
+    for must in ["vd_roi_align_forward", "vd_roi_align_backward", "vd_roi_align_fpn_forward",
+                 "vd_nms", "vd_generate_proposals", "vd_collect_distribute",
+                 "vd_box_detections", "vd_roi_pool_forward", "vd_roi_crop_forward",
+                 "vd_roi_align_legacy_forward"]:
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from vosdetectron_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.fail("libvosdet.so not built (run __graft_entry__.build())")
+    L = _lib.lib()
+    for name in declared():
+        assert hasattr(L, name), name
+        assert name in _lib.SIGNATURES, "binding missing for %s" % name
+    assert L.vd_version() == 1
+    assert L.vd_status_string(2) == b"unsupported shape"
+
+
+def test_host_side_argument_errors_without_gpu():
+    """Validation happens before any launch, so it is testable on the host."""
+    from vosdetectron_amd import _lib
+    L = _lib.lib()
+    # rois with 4 columns -> VD_ERR_ARG (reference returns 0 and leaves zeros)
+    assert L.vd_roi_align_forward(7, 7, 0.25, 2, 1, 1, 1, 1, 1, 1, 3, 4, 1, None) == _lib.VD_ERR_ARG
+    assert L.vd_nms(None, 10, 5, 0.5, None, None, None, 0, None) == _lib.VD_ERR_ARG
+    assert L.vd_nms_workspace_size(1000) > 1000 * 16 * 8
+
+
+def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
+    from vosdetectron_amd import _lib
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "missing.so"))
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _lib.lib()

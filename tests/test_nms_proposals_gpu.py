@@ -1,0 +1,169 @@
+"""GPU parity of NMS, FPN level map, RPN proposals, collect/distribute and the
+box-head post-processing against the oracle and the reference-generated golden
+fixtures.  Index selection must be bit-exact."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rand_dets(rng, n, ties=False, span=800):
+    xy = rng.uniform(0, span, (n, 2))
+    wh = rng.uniform(1, 120, (n, 2))
+    s = rng.uniform(0, 1, n)
+    if ties:
+        s = np.round(s * 8) / 8  # heavy ties
+    d = np.hstack([xy, xy + wh, s[:, None]]).astype(np.float32)
+    return d
+
+
+@pytest.mark.parametrize("n,thr,ties", [(1, 0.5, False), (7, 0.5, True), (300, 0.7, False),
+                                        (1000, 0.7, True), (2500, 0.5, False), (64, 0.3, True),
+                                        (65, 0.3, False), (5000, 0.6, True)])
+def test_nms_bit_exact(n, thr, ties):
+    from vosdetectron_amd import ops
+    rng = np.random.default_rng(n + int(thr * 10))
+    d = rand_dets(rng, n, ties)
+    ref = orc.nms(d, thr)
+    out = ops.nms(torch.from_numpy(d).to(DEV), thr).cpu().numpy()
+    assert np.array_equal(out, ref)
+
+
+def test_nms_edge_cases():
+    from vosdetectron_amd import ops
+    same = np.array([[0, 0, 10, 10, 0.9]] * 5, np.float32)
+    assert ops.nms(torch.from_numpy(same).to(DEV), 0.5).cpu().tolist() == [4]
+    assert ops.nms(torch.zeros((0, 5), device=DEV), 0.5).numel() == 0
+    # threshold equality suppresses (>=)
+    d = np.array([[0, 0, 10, 10, 0.9], [0, 0, 10, 21, 0.8]], np.float32)
+    assert ops.nms(torch.from_numpy(d).to(DEV), 0.5).cpu().tolist() == [0]
+
+
+def test_fpn_levels_golden(golden):
+    from vosdetectron_amd import ops
+    g = golden("fpn_levels")
+    rois = np.hstack([np.zeros((len(g["boxes"]), 1), np.float32), g["boxes"]])
+    out = ops.map_rois_to_fpn_levels(torch.from_numpy(rois).to(DEV), 2, 5).cpu().numpy()
+    assert np.array_equal(out, g["lvls"].astype(np.int32))
+
+
+def _anchors(lvl):
+    return torch.from_numpy(orc.fpn_level_anchors(lvl)).to(DEV)
+
+
+def test_generate_proposals_golden(golden):
+    """Reference-executed GenerateProposalsOp per level (tests/golden/proposals.npz)."""
+    from vosdetectron_amd import ops
+    g = golden("proposals")
+    lv = list(range(2, 7))
+    probs = [torch.from_numpy(g["probs_fpn%d" % l]).to(DEV) for l in lv]
+    deltas = [torch.from_numpy(g["deltas_fpn%d" % l]).to(DEV) for l in lv]
+    rois, pr, cnt = ops.generate_proposals(probs, deltas, [_anchors(l) for l in lv],
+                                           [1. / 2 ** l for l in lv],
+                                           torch.from_numpy(g["im_info"]).to(DEV), 1000, 1000,
+                                           0.7, 0)
+    rois, pr, cnt = rois.cpu().numpy(), pr.cpu().numpy(), cnt.cpu().numpy()
+    for i, l in enumerate(lv):
+        ref_r, ref_p = g["rois_fpn%d" % l], g["roi_probs_fpn%d" % l]
+        k = cnt[0, i]
+        assert k == len(ref_r), (l, k, len(ref_r))
+        assert np.array_equal(rois[0, i, :k], ref_r), l
+        assert np.array_equal(pr[0, i, :k], ref_p[:, 0]), l
+    # collect + distribute against the reference's collect/distribute outputs
+    c = golden("collect_distribute")
+    cr, clv, ccnt = ops.collect_distribute(torch.from_numpy(rois).to(DEV),
+                                           torch.from_numpy(pr).to(DEV),
+                                           torch.from_numpy(cnt).to(DEV), 1000)
+    cr, clv = cr.cpu().numpy()[0], clv.cpu().numpy()[0]
+    assert int(ccnt.item()) == 1000
+    assert np.array_equal(cr, c["collected"])
+    for k in range(4):
+        sel = cr[clv == k]
+        assert np.array_equal(sel, c["rois_fpn%d" % (k + 2)])
+
+
+@pytest.mark.parametrize("seed,ties", [(0, False), (1, True), (2, True)])
+def test_generate_proposals_vs_oracle_batched(seed, ties):
+    """Two images, full-size P2..P6 of an 800x1344 blob, tied scores."""
+    from vosdetectron_amd import ops
+    rng = np.random.default_rng(seed)
+    N = 2
+    shapes = {2: (200, 336), 3: (100, 168), 4: (50, 84), 5: (25, 42), 6: (13, 21)}
+    im_info = np.array([[800, 1344, 1.0], [800, 1344, 1.0]], np.float32)
+    probs, deltas = [], []
+    for l, (H, W) in shapes.items():
+        p = rng.uniform(0, 1, (N, 3, H, W)).astype(np.float32)
+        if ties:
+            p = (np.round(p * 512) / 512).astype(np.float32)
+        probs.append(p)
+        deltas.append(rng.normal(0, 0.5, (N, 12, H, W)).astype(np.float32))
+    lv = list(shapes)
+    out = ops.generate_proposals([torch.from_numpy(p).to(DEV) for p in probs],
+                                 [torch.from_numpy(d).to(DEV) for d in deltas],
+                                 [_anchors(l) for l in lv], [1. / 2 ** l for l in lv],
+                                 torch.from_numpy(im_info).to(DEV), 1000, 1000, 0.7, 0)
+    rois, pr, cnt = [t.cpu().numpy() for t in out]
+    for i, l in enumerate(lv):
+        ref_r, ref_p = orc.generate_proposals(orc.fpn_level_anchors(l), 1. / 2 ** l, probs[i],
+                                              deltas[i], im_info)
+        for img in range(N):
+            sel = ref_r[:, 0] == img
+            k = cnt[img, i]
+            assert k == sel.sum(), (l, img)
+            assert np.array_equal(rois[img, i, :k], ref_r[sel]), (l, img)
+            assert np.array_equal(pr[img, i, :k], ref_p[sel, 0]), (l, img)
+    # per-image collect/distribute
+    cr, clv, ccnt = [t.cpu().numpy() for t in ops.collect_distribute(
+        *[torch.from_numpy(x).to(DEV) for x in (rois, pr, cnt)], 1000)]
+    for img in range(N):
+        rl = [rois[img, i, :cnt[img, i]] for i in range(5)]
+        pl = [pr[img, i, :cnt[img, i], None] for i in range(5)]
+        col = orc.collect(rl, pl, 1000)
+        assert np.array_equal(cr[img, :ccnt[img]], col)
+        lvls = orc.map_rois_to_fpn_levels(col[:, 1:5], 2, 5).astype(np.int32) - 2
+        assert np.array_equal(clv[img, :ccnt[img]], lvls)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_box_detections_vs_oracle(seed):
+    """Decode (weights 10,10,5,5) + clip to the original image + per-class NMS +
+    top-100 (core/test.py:157-184, 733-797) vs the oracle."""
+    from vosdetectron_amd import ops
+    rng = np.random.default_rng(seed)
+    N, R, K = 2, 1000, 81
+    im_h, im_w = 800, 1333
+    rois = np.zeros((N, R, 5), np.float32)
+    for i in range(N):
+        xy = rng.uniform(0, 1300, (R, 2))
+        wh = rng.uniform(4, 300, (R, 2))
+        rois[i, :, 0] = i
+        rois[i, :, 1:3] = xy
+        rois[i, :, 3:5] = np.minimum(xy + wh, [1343, 799])
+    logits = rng.normal(0, 2.5, (N, R, K)).astype(np.float32)
+    e = np.exp(logits - logits.max(-1, keepdims=True))
+    cls = (e / e.sum(-1, keepdims=True)).astype(np.float32)
+    if seed == 1:
+        cls = (np.round(cls * 256) / 256).astype(np.float32)  # ties in scores
+    pred = rng.normal(0, 1.0, (N, R, 4 * K)).astype(np.float32)
+    counts = np.array([R, R - 37], np.int32)
+    out = ops.box_detections(*[torch.from_numpy(x).to(DEV) for x in (rois, cls, pred, counts)],
+                             torch.tensor([1.0, 1.0], device=DEV),
+                             torch.tensor([[im_h, im_w]] * N, dtype=torch.int32, device=DEV),
+                             det_cap=8192)
+    dets, dcls, dcnt = [t.cpu().numpy() for t in out]
+    for i in range(N):
+        r = counts[i]
+        boxes = rois[i, :r, 1:5] / 1.0
+        pb = orc.bbox_transform(boxes, pred[i, :r], (10., 10., 5., 5.))
+        pb = orc.clip_tiled_boxes(pb, (im_h, im_w, 3))
+        sc, bx, cls_boxes = orc.box_results_with_nms_and_limit(cls[i, :r], pb)
+        n = dcnt[i]
+        assert n == len(sc)
+        assert np.array_equal(dets[i, :n, :4], bx)
+        assert np.array_equal(dets[i, :n, 4], sc)
+        ref_cls = np.concatenate([[j] * len(cls_boxes[j]) for j in range(1, K)]).astype(np.int32)
+        assert np.array_equal(dcls[i, :n], ref_cls)

@@ -1,0 +1,151 @@
+"""GPU parity of the RoI operators (HIP, through the C ABI) against the oracle.
+
+Bit-exact where the kernel keeps the reference's evaluation order (RoIAlign
+fwd NCHW / NHWC, RoIPool, RoICrop, legacy RoIAlign); the atomics-based backward
+is compared within fp32 tolerance (sum order differs, as it does between two
+runs of the reference's own atomicAdd kernel)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def make_rois(rng, n, img_w, img_h, batch=1, edge=True):
+    s = np.exp(rng.uniform(np.log(4), np.log(600), n))
+    a = np.exp(rng.uniform(np.log(0.5), np.log(2), n))
+    w, h = s / np.sqrt(a), s * np.sqrt(a)
+    cx, cy = rng.uniform(-20, img_w + 20, n), rng.uniform(-20, img_h + 20, n)
+    b = rng.integers(0, batch, n)
+    r = np.stack([b, cx - w / 2, cy - h / 2, cx + w / 2, cy + h / 2], 1).astype(np.float32)
+    if edge:
+        extra = np.array([
+            [0, -50, -50, -10, -10],        # fully outside (top-left)
+            [0, img_w + 5, img_h + 5, img_w + 40, img_h + 40],  # fully outside
+            [0, 10, 10, 10, 10],            # degenerate -> 1x1
+            [0, 30, 30, 20, 20],            # malformed x2<x1
+            [0, 0, 0, img_w - 1, img_h - 1],  # whole image
+            [0, img_w - 2, img_h - 2, img_w + 3, img_h + 3],  # straddles the far edge
+            [0, -0.75, -0.75, 2.2, 2.2],    # straddles the near edge
+        ], np.float32)
+        extra[:, 0] = np.minimum(extra[:, 0], batch - 1)
+        r = np.concatenate([r, extra])
+    return r
+
+
+@pytest.mark.parametrize("P,sr", [(7, 2), (14, 2), (7, 0), (5, 2)])
+def test_roi_align_nchw_bit_exact(P, sr):
+    from vosdetectron_amd import ops
+    rng = np.random.default_rng(P * 10 + sr)
+    B, C, H, W = 2, 24, 37, 51
+    f = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    rois = make_rois(rng, 60, W * 8, H * 8, batch=B)
+    scale = 1. / 8
+    ref = orc.roi_align(f, rois, P, P, scale, sr)
+    out = ops.roi_align_forward(torch.from_numpy(f).to(DEV), torch.from_numpy(rois).to(DEV), P, P,
+                                scale, sr).cpu().numpy()
+    assert np.array_equal(out, ref)
+
+
+def _pyramid(rng, B, C, sizes):
+    return [rng.standard_normal((B, C, h, w)).astype(np.float32) for (h, w) in sizes]
+
+
+@pytest.mark.parametrize("P,sr,C", [(7, 2, 256), (14, 2, 256), (7, 0, 256), (7, 2, 64),
+                                    (14, 2, 520), (6, 2, 128)])
+def test_roi_align_fpn_nhwc_bit_exact(P, sr, C):
+    """One launch over 4 levels vs the reference per-level loop + restore
+    (model_builder.py:252-303) evaluated by the oracle."""
+    from vosdetectron_amd import ops
+    rng = np.random.default_rng(1000 + P + sr + C)
+    B = 2
+    sizes = [(50, 84), (25, 42), (13, 21), (7, 11)]
+    scales = [1. / 4, 1. / 8, 1. / 16, 1. / 32]
+    feats = _pyramid(rng, B, C, sizes)
+    rois = make_rois(rng, 120, 336, 200, batch=B)
+    lv = orc.map_rois_to_fpn_levels(rois[:, 1:5], 2, 5).astype(np.int32) - 2
+    d = {"rois": rois}
+    order = np.empty((0,))
+    for k in range(4):
+        idx = np.where(lv == k)[0]
+        d["rois_fpn%d" % (k + 2)] = rois[idx]
+        order = np.concatenate([order, idx])
+    d["rois_idx_restore_int32"] = np.argsort(order, kind="stable").astype(np.int32)
+    ref = orc.roi_feature_transform(feats[::-1], d, "rois", P, scales[::-1], sr)
+    nhwc = [torch.from_numpy(x).to(DEV).permute(0, 2, 3, 1).contiguous() for x in feats]
+    out = ops.roi_align_fpn(nhwc, scales, torch.from_numpy(rois).to(DEV),
+                            torch.from_numpy(lv).to(DEV), P, sr).cpu().numpy()
+    assert np.array_equal(out, ref)
+    # scheduling permutation must not move outputs
+    perm = torch.from_numpy(rng.permutation(len(rois)).astype(np.int32)).to(DEV)
+    if P in (7, 14):
+        out2 = ops.roi_align_fpn(nhwc, scales, torch.from_numpy(rois).to(DEV),
+                                 torch.from_numpy(lv).to(DEV), P, sr, roi_order=perm)
+        assert np.array_equal(out2.cpu().numpy(), ref)
+
+
+def test_roi_align_function_api_and_backward():
+    from vosdetectron_amd.ops import RoIAlignFunction
+    rng = np.random.default_rng(7)
+    B, C, H, W = 1, 8, 20, 30
+    f = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    rois = make_rois(rng, 30, W * 4, H * 4, batch=B)
+    ft = torch.from_numpy(f).to(DEV).requires_grad_(True)
+    out = RoIAlignFunction(7, 7, 0.25, 2)(ft, torch.from_numpy(rois).to(DEV))
+    g = rng.standard_normal(out.shape).astype(np.float32)
+    out.backward(torch.from_numpy(g).to(DEV))
+    ref = orc.roi_align_backward(g, rois, f.shape, 0.25, 2)
+    np.testing.assert_allclose(ft.grad.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+    with pytest.raises(NotImplementedError):
+        RoIAlignFunction(7, 7, 0.25, 2)(torch.from_numpy(f), torch.from_numpy(rois))
+
+
+def test_roi_align_rejects_bad_rois():
+    from vosdetectron_amd import ops
+    from vosdetectron_amd._lib import VosdetError
+    f = torch.zeros((1, 4, 8, 8), device=DEV)
+    with pytest.raises(VosdetError):
+        ops.roi_align_forward(f, torch.zeros((3, 4), device=DEV), 7, 7, 1., 2)
+    out = ops.roi_align_forward(f, torch.zeros((0, 5), device=DEV), 7, 7, 1., 2)
+    assert out.shape == (0, 4, 7, 7)
+
+
+def test_legacy_pool_crop_bit_exact():
+    from vosdetectron_amd import ops
+    rng = np.random.default_rng(11)
+    B, C, H, W = 2, 16, 23, 31
+    f = rng.standard_normal((B, C, H, W)).astype(np.float32)
+    rois = make_rois(rng, 40, W * 16, H * 16, batch=B)
+    ft, rt = torch.from_numpy(f).to(DEV), torch.from_numpy(rois).to(DEV)
+    ref = orc.roi_align_legacy(f, rois, 7, 7, 1. / 16)
+    assert np.array_equal(ops.roi_align_legacy(ft, rt, 7, 7, 1. / 16).cpu().numpy(), ref)
+    ref_o, ref_a = orc.roi_pool(f, rois, 7, 7, 1. / 16)
+    fn = ops.RoIPoolFunction(7, 7, 1. / 16)
+    out = fn(ft, rt)
+    assert np.array_equal(out.cpu().numpy(), ref_o)
+    assert np.array_equal(fn.argmax.cpu().numpy(), ref_a)
+    # RoICrop: grids from the reference's affine_grid_gen shape, incl. outside taps
+    R, G = 8, 14
+    grid = rng.uniform(-1.3, 1.3, (R, G, G, 2)).astype(np.float32)
+    ref_c = orc.roi_crop(f, grid)
+    out_c = ops.RoICropFunction()(ft, torch.from_numpy(grid).to(DEV)).cpu().numpy()
+    assert np.array_equal(out_c, ref_c)
+
+
+def test_roi_pool_backward_matches_scatter():
+    from vosdetectron_amd import ops
+    rng = np.random.default_rng(5)
+    f = rng.standard_normal((1, 4, 12, 12)).astype(np.float32)
+    rois = make_rois(rng, 10, 48, 48, edge=False)
+    ft = torch.from_numpy(f).to(DEV).requires_grad_(True)
+    fn = ops.RoIPoolFunction(3, 3, 0.25)
+    out = fn(ft, torch.from_numpy(rois).to(DEV))
+    g = np.ones(out.shape, np.float32)
+    out.backward(torch.from_numpy(g).to(DEV))
+    _, arg = orc.roi_pool(f, rois, 3, 3, 0.25)
+    ref = np.zeros(f.size, np.float32)
+    np.add.at(ref, arg[arg >= 0].ravel(), 1.0)
+    assert np.array_equal(ft.grad.cpu().numpy().ravel(), ref)

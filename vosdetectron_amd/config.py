@@ -1,0 +1,135 @@
+"""Configuration: the subset of the reference's global ``cfg`` (lib/core/config.py)
+that the per-frame inference hot path reads, with the reference's defaults, and
+a YAML merge that accepts the reference's own config files unchanged
+(merge_cfg_from_file, config.py:1107-1113; unknown keys are ignored here
+because the training/dataset keys are out of scope).
+"""
+from __future__ import annotations
+
+import copy
+import math
+
+import yaml
+
+
+class AttrDict(dict):
+    """lib/utils/collections.py AttrDict equivalent."""
+
+    def __getattr__(self, name):
+        try:
+            return self[name]
+        except KeyError:
+            raise AttributeError(name)
+
+    def __setattr__(self, name, value):
+        self[name] = value
+
+
+def _d(**kw):
+    return AttrDict(kw)
+
+
+def default_cfg() -> AttrDict:
+    """Defaults from lib/core/config.py (line numbers cited per group)."""
+    return _d(
+        MODEL=_d(  # config.py:392-432
+            TYPE="generalized_rcnn", CONV_BODY="FPN.fpn_ResNet50_conv5_body", NUM_CLASSES=81,
+            CLS_AGNOSTIC_BBOX_REG=False, BBOX_REG_WEIGHTS=(10., 10., 5., 5.),
+            FASTER_RCNN=True, MASK_ON=True, KEYPOINTS_ON=False, RPN_ONLY=False),
+        RESNETS=_d(  # config.py:870-905
+            NUM_GROUPS=1, WIDTH_PER_GROUP=64, STRIDE_1X1=True,
+            TRANS_FUNC="bottleneck_transformation", STEM_FUNC="basic_bn_stem",
+            SHORTCUT_FUNC="basic_bn_shortcut", RES5_DILATION=1, USE_GN=False),
+        FPN=_d(  # config.py:680-726
+            FPN_ON=True, DIM=256, COARSEST_STRIDE=32, MULTILEVEL_ROIS=True, MULTILEVEL_RPN=True,
+            ROI_CANONICAL_SCALE=224, ROI_CANONICAL_LEVEL=4, ROI_MAX_LEVEL=5, ROI_MIN_LEVEL=2,
+            RPN_MAX_LEVEL=6, RPN_MIN_LEVEL=2, RPN_ASPECT_RATIOS=(0.5, 1, 2),
+            RPN_ANCHOR_START_SIZE=32, RPN_COLLECT_SCALE=1, EXTRA_CONV_LEVELS=False,
+            USE_GN=False),
+        FAST_RCNN=_d(  # config.py:620-645
+            ROI_BOX_HEAD="fast_rcnn_heads.roi_2mlp_head", MLP_HEAD_DIM=1024,
+            ROI_XFORM_METHOD="RoIPoolF", ROI_XFORM_SAMPLING_RATIO=0, ROI_XFORM_RESOLUTION=14),
+        MRCNN=_d(  # config.py:735-770
+            ROI_MASK_HEAD="mask_rcnn_heads.mask_rcnn_fcn_head_v1up4convs", RESOLUTION=14,
+            ROI_XFORM_METHOD="RoIAlign", ROI_XFORM_RESOLUTION=7, ROI_XFORM_SAMPLING_RATIO=0,
+            DIM_REDUCED=256, DILATION=2, UPSAMPLE_RATIO=1, USE_FC_OUTPUT=False,
+            CLS_SPECIFIC_MASK=True, CONV_INIT="GaussianFill"),
+        RPN=_d(CLS_ACTIVATION="sigmoid", SIZES=(64, 128, 256, 512), STRIDE=16,
+               ASPECT_RATIOS=(0.5, 1, 2)),  # config.py:655-675
+        TEST=_d(  # config.py:180-230, 945-950
+            SCALE=600, MAX_SIZE=1000, NMS=0.3, BBOX_REG=True, RPN_NMS_THRESH=0.7,
+            RPN_PRE_NMS_TOP_N=12000, RPN_POST_NMS_TOP_N=2000, RPN_MIN_SIZE=0,
+            DETECTIONS_PER_IM=100, SCORE_THRESH=0.05, NUM_DET_PER_CLASS_PRE=0,
+            NUM_DET_PER_CLASS_POST=0, NMS_CROSS_CLASS=0.),
+        PIXEL_MEANS=(102.9801, 115.9465, 122.7717),  # config.py:1015
+        BBOX_XFORM_CLIP=math.log(1000. / 16.),  # config.py:1009
+        CROP_RESIZE_WITH_MAX_POOL=True,  # config.py:1058
+    )
+
+
+def _merge(a, b):
+    for k, v in a.items():
+        if k not in b:
+            continue  # training / dataset keys: out of scope for the hot path
+        if isinstance(v, dict) and isinstance(b[k], dict):
+            _merge(v, b[k])
+        else:
+            if isinstance(b[k], tuple) and isinstance(v, (list, tuple)):
+                v = tuple(v)
+            b[k] = v
+
+
+def load_cfg(path: str | None = None, overrides: dict | None = None) -> AttrDict:
+    """Defaults, then a reference YAML (safe loader), then dotted overrides."""
+    cfg = default_cfg()
+    if path:
+        with open(path) as f:
+            _merge(yaml.safe_load(f) or {}, cfg)
+    for key, val in (overrides or {}).items():
+        d = cfg
+        parts = key.split(".")
+        for p in parts[:-1]:
+            d = d[p]
+        d[parts[-1]] = val
+    return cfg
+
+
+# The configurations BASELINE.json names, restated as overrides of the defaults
+# (values from configs/baselines/*.yaml of the reference).
+def e2e_mask_rcnn_R_50_FPN_1x() -> AttrDict:
+    return load_cfg(overrides={
+        "MODEL.CONV_BODY": "FPN.fpn_ResNet50_conv5_body", "MODEL.FASTER_RCNN": True,
+        "MODEL.MASK_ON": True, "FAST_RCNN.ROI_BOX_HEAD": "fast_rcnn_heads.roi_2mlp_head",
+        "FAST_RCNN.ROI_XFORM_METHOD": "RoIAlign", "FAST_RCNN.ROI_XFORM_RESOLUTION": 7,
+        "FAST_RCNN.ROI_XFORM_SAMPLING_RATIO": 2,
+        "MRCNN.ROI_MASK_HEAD": "mask_rcnn_heads.mask_rcnn_fcn_head_v1up4convs",
+        "MRCNN.RESOLUTION": 28, "MRCNN.ROI_XFORM_METHOD": "RoIAlign",
+        "MRCNN.ROI_XFORM_RESOLUTION": 14, "MRCNN.ROI_XFORM_SAMPLING_RATIO": 2,
+        "MRCNN.DILATION": 1, "MRCNN.CONV_INIT": "MSRAFill", "TEST.SCALE": 800,
+        "TEST.MAX_SIZE": 1333, "TEST.NMS": 0.5, "TEST.RPN_PRE_NMS_TOP_N": 1000,
+        "TEST.RPN_POST_NMS_TOP_N": 1000})
+
+
+def e2e_mask_rcnn_R_101_FPN_2x() -> AttrDict:
+    cfg = e2e_mask_rcnn_R_50_FPN_1x()
+    cfg.MODEL.CONV_BODY = "FPN.fpn_ResNet101_conv5_body"
+    return cfg
+
+
+def e2e_mask_rcnn_X_101_32x8d_FPN_1x() -> AttrDict:
+    cfg = e2e_mask_rcnn_R_50_FPN_1x()
+    cfg.MODEL.CONV_BODY = "FPN.fpn_ResNet101_conv5_body"
+    cfg.RESNETS.NUM_GROUPS = 32
+    cfg.RESNETS.WIDTH_PER_GROUP = 8
+    return cfg
+
+
+CONFIGS = {
+    "e2e_mask_rcnn_R-50-FPN_1x": e2e_mask_rcnn_R_50_FPN_1x,
+    "e2e_mask_rcnn_R-101-FPN_2x": e2e_mask_rcnn_R_101_FPN_2x,
+    "e2e_mask_rcnn_X-101-32x8d-FPN_1x": e2e_mask_rcnn_X_101_32x8d_FPN_1x,
+}
+
+
+def get(name: str) -> AttrDict:
+    return copy.deepcopy(CONFIGS[name]())

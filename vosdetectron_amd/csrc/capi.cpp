@@ -1,0 +1,196 @@
+// extern "C" surface of libvosdet.so (declared in include/vosdet.h).
+// Argument validation happens here; the kernels assume validated shapes.
+#include <hip/hip_runtime.h>
+
+#include "vosdet_internal.hpp"
+
+using namespace vd;
+
+#define VD_STREAM(s) reinterpret_cast<hipStream_t>(s)
+
+extern "C" {
+
+int vd_version(void) { return 1; }
+
+const char *vd_status_string(int status) {
+    switch (status) {
+        case VD_OK: return "ok";
+        case VD_ERR_ARG: return "invalid argument";
+        case VD_ERR_SHAPE: return "unsupported shape";
+        case VD_ERR_LAUNCH: return "kernel launch failed";
+        case VD_ERR_WORKSPACE: return "workspace too small";
+        default: return "unknown status";
+    }
+}
+
+static bool bad_feat(const void *p, int B, int C, int H, int W) {
+    return !p || B < 1 || C < 1 || H < 1 || W < 1;
+}
+
+int vd_roi_align_forward(int ah, int aw, float spatial_scale, int sampling_ratio,
+                         const float *features, int B, int C, int H, int W, const float *rois,
+                         int num_rois, int roi_cols, float *output, void *stream) {
+    if (roi_cols != 5) return VD_ERR_ARG;
+    if (num_rois == 0) return VD_OK;
+    if (bad_feat(features, B, C, H, W) || !rois || !output || ah < 1 || aw < 1 || num_rois < 0)
+        return VD_ERR_ARG;
+    return launch_roi_align_fwd_nchw(features, B, C, H, W, rois, num_rois, ah, aw, spatial_scale,
+                                     sampling_ratio, output, VD_STREAM(stream));
+}
+
+int vd_roi_align_backward(int ah, int aw, float spatial_scale, int sampling_ratio,
+                          const float *top_grad, int B, int C, int H, int W, const float *rois,
+                          int num_rois, int roi_cols, float *bottom_grad, void *stream) {
+    if (roi_cols != 5) return VD_ERR_ARG;
+    if (num_rois == 0) return VD_OK;
+    if (bad_feat(bottom_grad, B, C, H, W) || !rois || !top_grad || ah < 1 || aw < 1)
+        return VD_ERR_ARG;
+    return launch_roi_align_bwd_nchw(top_grad, B, C, H, W, rois, num_rois, ah, aw, spatial_scale,
+                                     sampling_ratio, bottom_grad, VD_STREAM(stream));
+}
+
+int vd_roi_align_fpn_forward(const VdFeatLevel *levels, int num_levels, int B, int C, int layout,
+                             const float *rois, const int32_t *roi_level,
+                             const int32_t *roi_order, int num_rois, int ah, int aw,
+                             int sampling_ratio, float *output, void *stream) {
+    if (num_rois == 0) return VD_OK;
+    if (!levels || num_levels < 1 || num_levels > VD_MAX_LEVELS || !rois || !output || B < 1 ||
+        C < 1 || ah < 1 || aw < 1 || num_rois < 0)
+        return VD_ERR_ARG;
+    if (num_levels > 1 && !roi_level) return VD_ERR_ARG;
+    FpnLevels fa = {};
+    for (int l = 0; l < num_levels; ++l) {
+        if (bad_feat(levels[l].data, B, C, levels[l].H, levels[l].W)) return VD_ERR_ARG;
+        fa.feat[l] = levels[l].data;
+        fa.H[l] = levels[l].H;
+        fa.W[l] = levels[l].W;
+        fa.scale[l] = levels[l].spatial_scale;
+    }
+    if (layout == VD_LAYOUT_NHWC)
+        return launch_roi_align_fpn_nhwc(fa, C, rois, roi_level, roi_order, num_rois, ah, aw,
+                                         sampling_ratio, output, VD_STREAM(stream));
+    if (layout != VD_LAYOUT_NCHW) return VD_ERR_ARG;
+    if (num_levels != 1) return VD_ERR_SHAPE;  // multi-level NCHW: use per-level calls
+    return launch_roi_align_fwd_nchw(fa.feat[0], B, C, fa.H[0], fa.W[0], rois, num_rois, ah, aw,
+                                     fa.scale[0], sampling_ratio, output, VD_STREAM(stream));
+}
+
+int vd_roi_align_legacy_forward(int ah, int aw, float spatial_scale, const float *features,
+                                int B, int C, int H, int W, const float *rois, int num_rois,
+                                float *output, void *stream) {
+    if (num_rois == 0) return VD_OK;
+    if (bad_feat(features, B, C, H, W) || !rois || !output || num_rois < 0) return VD_ERR_ARG;
+    if (H < 2 || W < 2) return VD_ERR_SHAPE;  // the kernel reads the 2x2 block at <= (H-2, W-2)
+    return launch_roi_align_legacy_fwd(features, B, C, H, W, rois, num_rois, ah, aw,
+                                       spatial_scale, output, VD_STREAM(stream));
+}
+
+int vd_roi_pool_forward(int ph, int pw, float spatial_scale, const float *features, int B, int C,
+                        int H, int W, const float *rois, int num_rois, float *output,
+                        int32_t *argmax, void *stream) {
+    if (num_rois == 0) return VD_OK;
+    if (bad_feat(features, B, C, H, W) || !rois || !output || ph < 1 || pw < 1 || num_rois < 0)
+        return VD_ERR_ARG;
+    return launch_roi_pool_fwd(features, B, C, H, W, rois, num_rois, ph, pw, spatial_scale,
+                               output, argmax, VD_STREAM(stream));
+}
+
+int vd_roi_pool_backward(const float *top_grad, const int32_t *argmax, int64_t num_outputs,
+                         float *bottom_grad, void *stream) {
+    if (num_outputs == 0) return VD_OK;
+    if (!top_grad || !argmax || !bottom_grad || num_outputs < 0) return VD_ERR_ARG;
+    return launch_roi_pool_bwd(top_grad, argmax, num_outputs, bottom_grad, VD_STREAM(stream));
+}
+
+int vd_roi_crop_forward(const float *input, int B, int C, int H, int W, const float *grid_yx,
+                        int num_rois, int GH, int GW, float *output, void *stream) {
+    if (num_rois == 0) return VD_OK;
+    if (bad_feat(input, B, C, H, W) || !grid_yx || !output || GH < 1 || GW < 1) return VD_ERR_ARG;
+    return launch_roi_crop_fwd(input, B, C, H, W, grid_yx, num_rois, GH, GW, output,
+                               VD_STREAM(stream));
+}
+
+size_t vd_nms_workspace_size(int n) { return nms_workspace_bytes(n); }
+
+int vd_nms(const float *dets, int n, int det_stride, float thresh, int64_t *keep_out,
+           int32_t *num_out, void *workspace, size_t workspace_bytes, void *stream) {
+    if (!num_out || (n > 0 && (!dets || !keep_out))) return VD_ERR_ARG;
+    return launch_nms(dets, n, det_stride, thresh, keep_out, num_out, workspace, workspace_bytes,
+                      VD_STREAM(stream));
+}
+
+int vd_map_rois_to_fpn_levels(const float *rois, int roi_stride, int col0, int R, int k_min,
+                              int k_max, float canonical_scale, float canonical_level,
+                              int32_t *lvl_out, void *stream) {
+    if (R == 0) return VD_OK;
+    if (!rois || !lvl_out || R < 0 || roi_stride < col0 + 4 || col0 < 0 || k_min > k_max)
+        return VD_ERR_ARG;
+    return launch_map_levels(rois, roi_stride, col0, R, k_min, k_max, canonical_scale,
+                             canonical_level, lvl_out, VD_STREAM(stream));
+}
+
+size_t vd_generate_proposals_workspace_size(const VdRpnLevel *levels, int num_levels,
+                                            int num_images, int pre_nms_topN) {
+    return rpn_workspace_bytes(levels, num_levels, num_images, pre_nms_topN);
+}
+
+int vd_generate_proposals(const VdRpnLevel *levels, int num_levels, int num_images,
+                          const float *im_info, int pre_nms_topN, int post_nms_topN,
+                          float nms_thresh, float min_size, float *rois_out, float *probs_out,
+                          int32_t *counts_out, void *workspace, size_t workspace_bytes,
+                          void *stream) {
+    if (!levels || !im_info || !rois_out || !probs_out || !counts_out) return VD_ERR_ARG;
+    for (int l = 0; l < num_levels && l < VD_MAX_LEVELS; ++l)
+        if (!levels[l].cls_prob || !levels[l].bbox_pred || !levels[l].anchors ||
+            levels[l].A < 1 || levels[l].H < 1 || levels[l].W < 1 ||
+            !(levels[l].spatial_scale > 0.f))
+            return VD_ERR_ARG;
+    return launch_rpn_proposals(levels, num_levels, num_images, im_info, pre_nms_topN,
+                                post_nms_topN, nms_thresh, min_size, rois_out, probs_out,
+                                counts_out, workspace, workspace_bytes, VD_STREAM(stream));
+}
+
+int vd_collect_distribute(const float *level_rois, const float *level_probs,
+                          const int32_t *level_counts, int num_levels, int level_cap,
+                          int num_images, int post_nms_topN, int k_min, int k_max,
+                          float *rois_out, int32_t *lvl_out, int32_t *count_out, void *stream) {
+    if (!level_rois || !level_probs || !level_counts || !rois_out || !lvl_out || !count_out ||
+        level_cap < 1 || k_min > k_max)
+        return VD_ERR_ARG;
+    return launch_collect_distribute(level_rois, level_probs, level_counts, num_levels,
+                                     level_cap, num_images, post_nms_topN, k_min, k_max,
+                                     rois_out, lvl_out, count_out, VD_STREAM(stream));
+}
+
+size_t vd_box_detections_workspace_size(int R_cap, int num_images, int num_classes) {
+    return box_detections_workspace_bytes(R_cap, num_images, num_classes);
+}
+
+int vd_box_detections(const float *rois, const float *cls_prob, const float *bbox_pred,
+                      const int32_t *roi_count, int R_cap, int num_images, int num_classes,
+                      const float *im_scale, const int32_t *im_hw, float score_thresh,
+                      float nms_thresh, int dets_per_im, const float *bbox_reg_weights,
+                      int det_cap, float *dets_out, int32_t *det_cls_out,
+                      int32_t *det_count_out, void *workspace, size_t workspace_bytes,
+                      void *stream) {
+    if (!rois || !cls_prob || !bbox_pred || !roi_count || !im_scale || !im_hw ||
+        !bbox_reg_weights || !dets_out || !det_cls_out || !det_count_out)
+        return VD_ERR_ARG;
+    return launch_box_detections(rois, cls_prob, bbox_pred, roi_count, R_cap, num_images,
+                                 num_classes, im_scale, im_hw, score_thresh, nms_thresh,
+                                 dets_per_im, bbox_reg_weights, det_cap, dets_out, det_cls_out,
+                                 det_count_out, workspace, workspace_bytes, VD_STREAM(stream));
+}
+
+int vd_image_to_blob(const uint8_t *frames, int F, int H, int W, const float *lut, int Hp,
+                     int Wp, int nhwc, float *blob, void *stream) {
+    if (!frames || !lut || !blob || H < 1 || W < 1) return VD_ERR_ARG;
+    return launch_image_to_blob(frames, F, H, W, lut, Hp, Wp, nhwc, blob, VD_STREAM(stream));
+}
+
+int vd_nchw_to_nhwc(const float *in, int B, int C, int H, int W, float *out, void *stream) {
+    if (!in || !out) return VD_ERR_ARG;
+    return launch_nchw_to_nhwc(in, B, C, H, W, out, VD_STREAM(stream));
+}
+
+}  // extern "C"

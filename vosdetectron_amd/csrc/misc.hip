@@ -1,0 +1,255 @@
+// The remaining RoI operators of the reference's lib/model (API completeness,
+// selectable through FAST_RCNN.ROI_XFORM_METHOD) and the frame/pyramid layout
+// kernels of the product path.
+//
+//   jwyang RoIAlign   lib/model/roi_align/src/roi_align_kernel.cu:15-70
+//   RoIPool fwd/bwd   lib/model/roi_pooling/src/roi_pooling_kernel.cu:24-93,128-203
+//   RoICrop fwd       lib/model/roi_crop/src/roi_crop_cuda_kernel.cu:11-109,201-255
+//   image -> blob     lib/utils/blob.py:37-114 (identity scale)
+#include <float.h>
+
+#include "common.hpp"
+#include "vosdet_internal.hpp"
+
+namespace vd {
+
+static int blocks_for(int64_t n, int bs) {
+    int64_t g = (n + bs - 1) / bs;
+    if (g > 65536) g = 65536;
+    return (int)(g < 1 ? 1 : g);
+}
+
+// ---------------------------------------------------------------- legacy
+__global__ __launch_bounds__(256) void roi_align_legacy_kernel(
+    int64_t nthreads, const float *__restrict__ feat, float scale, int H, int W, int C, int PH,
+    int PW, const float *__restrict__ rois, float *__restrict__ out) {
+    for (int64_t index = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; index < nthreads;
+         index += (int64_t)blockDim.x * gridDim.x) {
+        const int pw = (int)(index % PW);
+        const int ph = (int)((index / PW) % PH);
+        const int c = (int)((index / PW / PH) % C);
+        const int64_t n = index / PW / PH / C;
+        const float *r = rois + n * 5;
+        const int b = (int)r[0];  // reference multiplies a float batch index (:30,:46)
+        const float sw = r[1] * scale, sh = r[2] * scale, ew = r[3] * scale, eh = r[4] * scale;
+        const float rw = fmaxf((float)((double)(ew - sw) + 1.), 0.f);
+        const float rh = fmaxf((float)((double)(eh - sh) + 1.), 0.f);
+        const float bh = (float)(rh / (PH - 1.));
+        const float bw = (float)(rw / (PW - 1.));
+        const float h = (float)ph * bh + sh;
+        const float w = (float)pw * bw + sw;
+        const int hstart = (int)fminf(floorf(h), (float)(H - 2));
+        const int wstart = (int)fminf(floorf(w), (float)(W - 2));
+        if (h < 0 || h >= H || w < 0 || w >= W) {
+            out[index] = 0.f;
+            continue;
+        }
+        const float hr = h - (float)hstart, wr = w - (float)wstart;
+        const int64_t ul = (int64_t)b * C * H * W + ((int64_t)c * H + hstart) * W + wstart;
+        const int64_t ur = ul + 1, dl = ul + W, dr = dl + 1;
+        out[index] = (float)(feat[ul] * (1. - hr) * (1. - wr) + feat[ur] * (1. - hr) * wr +
+                             feat[dl] * hr * (1. - wr) + feat[dr] * hr * wr);
+    }
+}
+
+int launch_roi_align_legacy_fwd(const float *feat, int B, int C, int H, int W, const float *rois,
+                                int R, int PH, int PW, float scale, float *out, hipStream_t s) {
+    (void)B;
+    const int64_t n = (int64_t)R * C * PH * PW;
+    if (n == 0) return VD_OK;
+    if (PH < 2 || PW < 2) return VD_ERR_ARG;
+    hipLaunchKernelGGL(roi_align_legacy_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, n, feat,
+                       scale, H, W, C, PH, PW, rois, out);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+// ---------------------------------------------------------------- RoIPool
+__global__ __launch_bounds__(256) void roi_pool_fwd_kernel(
+    int64_t nthreads, const float *__restrict__ feat, float scale, int H, int W, int C, int PH,
+    int PW, const float *__restrict__ rois, float *__restrict__ out, int32_t *__restrict__ argmax) {
+    for (int64_t index = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; index < nthreads;
+         index += (int64_t)blockDim.x * gridDim.x) {
+        const int pw = (int)(index % PW);
+        const int ph = (int)((index / PW) % PH);
+        const int c = (int)((index / PW / PH) % C);
+        const int64_t n = index / PW / PH / C;
+        const float *r = rois + n * 5;
+        const int b = (int)r[0];
+        const int rsw = (int)roundf(r[1] * scale), rsh = (int)roundf(r[2] * scale);
+        const int rew = (int)roundf(r[3] * scale), reh = (int)roundf(r[4] * scale);
+        const int rw = (int)fmaxf((float)(rew - rsw + 1), 1.f);
+        const int rh = (int)fmaxf((float)(reh - rsh + 1), 1.f);
+        const float bh = (float)rh / (float)PH, bw = (float)rw / (float)PW;
+        int hs = (int)floorf((float)ph * bh), ws = (int)floorf((float)pw * bw);
+        int he = (int)ceilf((float)(ph + 1) * bh), we = (int)ceilf((float)(pw + 1) * bw);
+        hs = (int)fminf(fmaxf((float)(hs + rsh), 0.f), (float)H);
+        he = (int)fminf(fmaxf((float)(he + rsh), 0.f), (float)H);
+        ws = (int)fminf(fmaxf((float)(ws + rsw), 0.f), (float)W);
+        we = (int)fminf(fmaxf((float)(we + rsw), 0.f), (float)W);
+        const bool empty = (he <= hs) || (we <= ws);
+        float maxval = empty ? 0.f : -FLT_MAX;
+        int maxidx = -1;
+        const int64_t off = ((int64_t)b * C + c) * (int64_t)H * W;
+        for (int h = hs; h < he; ++h)
+            for (int w = ws; w < we; ++w) {
+                const float v = feat[off + (int64_t)h * W + w];
+                if (v > maxval) {
+                    maxval = v;
+                    maxidx = (int)(off + (int64_t)h * W + w);
+                }
+            }
+        out[index] = maxval;
+        if (argmax) argmax[index] = maxidx;
+    }
+}
+
+__global__ __launch_bounds__(256) void roi_pool_bwd_kernel(int64_t n,
+                                                           const float *__restrict__ top_diff,
+                                                           const int32_t *__restrict__ argmax,
+                                                           float *__restrict__ bottom_diff) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)blockDim.x * gridDim.x) {
+        const int a = argmax[i];
+        if (a >= 0) atomicAdd(bottom_diff + a, top_diff[i]);
+    }
+}
+
+int launch_roi_pool_fwd(const float *feat, int B, int C, int H, int W, const float *rois, int R,
+                        int PH, int PW, float scale, float *out, int32_t *argmax, hipStream_t s) {
+    (void)B;
+    const int64_t n = (int64_t)R * C * PH * PW;
+    if (n == 0) return VD_OK;
+    hipLaunchKernelGGL(roi_pool_fwd_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, n, feat,
+                       scale, H, W, C, PH, PW, rois, out, argmax);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+int launch_roi_pool_bwd(const float *top_diff, const int32_t *argmax, int64_t n,
+                        float *bottom_diff, hipStream_t s) {
+    if (n == 0) return VD_OK;
+    hipLaunchKernelGGL(roi_pool_bwd_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, n,
+                       top_diff, argmax, bottom_diff);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+// ---------------------------------------------------------------- RoICrop
+__device__ __forceinline__ void top_left(float x, int width, int &point, float &weight) {
+    const float xcoord = (x + 1) * (width - 1) / 2;
+    point = (int)floorf(xcoord);
+    weight = 1 - (xcoord - point);
+}
+__device__ __forceinline__ bool between(int v, int lo, int hi) { return v >= lo && v <= hi; }
+
+__global__ __launch_bounds__(256) void roi_crop_fwd_kernel(
+    int64_t nthreads, const float *__restrict__ in, int C, int H, int W,
+    const float *__restrict__ grid, int GH, int GW, int roi_per_image, float *__restrict__ out) {
+    for (int64_t index = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; index < nthreads;
+         index += (int64_t)blockDim.x * gridDim.x) {
+        const int xo = (int)(index % GW);
+        const int yo = (int)((index / GW) % GH);
+        const int c = (int)((index / GW / GH) % C);
+        const int64_t b = index / GW / GH / C;
+        const int64_t bi = b / roi_per_image;
+        const float *g = grid + ((b * GH + yo) * GW + xo) * 2;
+        const float yf = g[0], xf = g[1];
+        int yTL, xTL;
+        float yW, xW;
+        top_left(xf, W, xTL, xW);
+        top_left(yf, H, yTL, yW);
+        const bool tl = between(xTL, 0, W - 1) && between(yTL, 0, H - 1);
+        const bool tr = between(xTL + 1, 0, W - 1) && between(yTL, 0, H - 1);
+        const bool bl = between(xTL, 0, W - 1) && between(yTL + 1, 0, H - 1);
+        const bool br = between(xTL + 1, 0, W - 1) && between(yTL + 1, 0, H - 1);
+        if (!tl && !tr && !bl && !br) continue;
+        const float *plane = in + (bi * C + c) * (int64_t)H * W;
+        const float vTL = tl ? plane[(int64_t)yTL * W + xTL] : 0.f;
+        const float vTR = tr ? plane[(int64_t)yTL * W + xTL + 1] : 0.f;
+        const float vBL = bl ? plane[(int64_t)(yTL + 1) * W + xTL] : 0.f;
+        const float vBR = br ? plane[(int64_t)(yTL + 1) * W + xTL + 1] : 0.f;
+        out[index] = xW * yW * vTL + (1 - xW) * yW * vTR + xW * (1 - yW) * vBL +
+                     (1 - xW) * (1 - yW) * vBR;
+    }
+}
+
+int launch_roi_crop_fwd(const float *in, int B, int C, int H, int W, const float *grid, int R,
+                        int GH, int GW, float *out, hipStream_t s) {
+    const int64_t n = (int64_t)R * C * GH * GW;
+    if (n == 0) return VD_OK;
+    if (B < 1 || R < B) return VD_ERR_ARG;  // roiPerImage = ob / ib (launcher :217)
+    hipLaunchKernelGGL(roi_crop_fwd_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, n, in, C,
+                       H, W, grid, GH, GW, R / B, out);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+// ---------------------------------------------------------------- frames
+// One thread per 4 padded pixels of one row; u8 BGR triplets -> LUT floats.
+__global__ __launch_bounds__(256) void image_to_blob_kernel(const uint8_t *__restrict__ frames,
+                                                            int H, int W,
+                                                            const float *__restrict__ lut, int Hp,
+                                                            int Wp, int nhwc,
+                                                            float *__restrict__ blob) {
+    __shared__ float slut[768];
+    for (int i = threadIdx.x; i < 768; i += blockDim.x) slut[i] = lut[i];
+    __syncthreads();
+    const int f = blockIdx.z, y = blockIdx.y;
+    const uint8_t *src = frames + ((int64_t)f * H + y) * W * 3;
+    for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < Wp; x += gridDim.x * blockDim.x) {
+        float b = 0.f, g = 0.f, r = 0.f;
+        if (y < H && x < W) {
+            b = slut[src[x * 3 + 0]];
+            g = slut[256 + src[x * 3 + 1]];
+            r = slut[512 + src[x * 3 + 2]];
+        }
+        if (nhwc) {
+            float *d = blob + (((int64_t)f * Hp + y) * Wp + x) * 3;
+            d[0] = b;
+            d[1] = g;
+            d[2] = r;
+        } else {
+            const int64_t plane = (int64_t)Hp * Wp;
+            float *d = blob + (int64_t)f * 3 * plane + (int64_t)y * Wp + x;
+            d[0] = b;
+            d[plane] = g;
+            d[2 * plane] = r;
+        }
+    }
+}
+
+int launch_image_to_blob(const uint8_t *frames, int F, int H, int W, const float *lut, int Hp,
+                         int Wp, int nhwc, float *blob, hipStream_t s) {
+    if (F < 1 || Hp < H || Wp < W) return VD_ERR_ARG;
+    dim3 grid((Wp + 255) / 256, Hp, F);
+    hipLaunchKernelGGL(image_to_blob_kernel, grid, dim3(256), 0, s, frames, H, W, lut, Hp, Wp,
+                       nhwc, blob);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+// B x C x HW -> B x HW x C through a 64x64 LDS tile (+1 pad against bank conflicts).
+__global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float *__restrict__ in, int C,
+                                                           int HW, float *__restrict__ out) {
+    __shared__ float tile[64][65];
+    const int b = blockIdx.z;
+    const int c0 = blockIdx.y * 64, p0 = blockIdx.x * 64;
+    const float *src = in + (int64_t)b * C * HW;
+    float *dst = out + (int64_t)b * C * HW;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+    for (int k = ty; k < 64; k += 4) {
+        const int c = c0 + k, p = p0 + tx;
+        tile[k][tx] = (c < C && p < HW) ? src[(int64_t)c * HW + p] : 0.f;
+    }
+    __syncthreads();
+    for (int k = ty; k < 64; k += 4) {
+        const int p = p0 + k, c = c0 + tx;
+        if (p < HW && c < C) dst[(int64_t)p * C + c] = tile[tx][k];
+    }
+}
+
+int launch_nchw_to_nhwc(const float *in, int B, int C, int H, int W, float *out, hipStream_t s) {
+    const int HW = H * W;
+    if (B < 1 || C < 1 || HW < 1) return VD_ERR_ARG;
+    dim3 grid((HW + 63) / 64, (C + 63) / 64, B);
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel, grid, dim3(256), 0, s, in, C, HW, out);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+}  // namespace vd

@@ -1,0 +1,395 @@
+// RPN proposal generation + FPN collect/distribute, device resident.
+//
+// Reference (per image, per FPN level, host numpy in the reference):
+//   GenerateProposalsOp.forward / proposals_for_one_image
+//     lib/modeling/generate_proposals.py:20-168
+//   bbox_transform lib/utils/boxes.py:156-205, clip_tiled_boxes :138-153,
+//   _filter_boxes generate_proposals.py:171-182, nms -> cython_nms.pyx:37-87
+//   collect / distribute lib/modeling/collect_and_distribute_fpn_rpn_proposals.py:91-138
+//   map_rois_to_fpn_levels lib/utils/fpn.py:11-28
+//
+// One workgroup (1024 threads) per (level, image) does the whole chain in LDS:
+//   select  -- top pre_nms_topN of the H*W*A scores by the unique 64-bit key
+//              (score, ~index): a strided sample fixes a threshold whose
+//              candidate set is exact-superset-checked by a count pass (binary
+//              search over the sample on miss), candidates are compacted and
+//              bitonic-sorted.  Equals numpy's argpartition+argsort top-k with
+//              ties broken by lower index (the stable reading).
+//   decode  -- anchors + shifts (float64, as numpy) -> float32 boxes; the
+//              delta decode reproduces numpy 2's float64 promotion of dw/dh by
+//              the float64 BBOX_XFORM_CLIP; clip; min-size/centre filter.
+//   nms     -- processing order (score desc, position desc), ballot bitmask,
+//              single-wave resolve; survivors ascending, first post_nms_topN.
+#include "nms_block.hpp"
+#include "vosdet_internal.hpp"
+
+namespace vd {
+
+static constexpr int kSelCap = 8192;      // candidate keys held in LDS
+static constexpr int kPreMax = 2048;      // pre_nms_topN per level
+static constexpr int kSampleMax = 2048;
+static constexpr double kBboxXformClip = 4.135166556742356;  // np.log(1000. / 16.)
+
+struct RpnArgs {
+    VdRpnLevel lv[VD_MAX_LEVELS];
+};
+
+__host__ __device__ inline size_t a256(size_t b) { return (b + 255) & ~(size_t)255; }
+static inline size_t rpn_mask_bytes(int pre) {
+    return a256(sizeof(uint64_t) * (size_t)pre * (size_t)((pre + 63) / 64));
+}
+
+size_t rpn_workspace_bytes(const VdRpnLevel *levels, int num_levels, int num_images,
+                           int pre_nms_topN) {
+    (void)levels;
+    int pre = pre_nms_topN > 0 ? pre_nms_topN : kPreMax;
+    if (pre > kPreMax) pre = kPreMax;
+    return rpn_mask_bytes(pre) * (size_t)num_levels * (size_t)num_images + 256;
+}
+
+// numpy-2 bbox_transform of one box with weights (wx, wy, ww, wh): returns
+// x1, y1, x2, y2 as the float32 store of numpy's (partly float64) arithmetic.
+__device__ __forceinline__ void decode_box(float bx1, float by1, float bx2, float by2, float d0,
+                                           float d1, float d2, float d3, float wx, float wy,
+                                           float ww, float wh, float &x1, float &y1, float &x2,
+                                           float &y2) {
+    const float widths = bx2 - bx1 + 1.0f;
+    const float heights = by2 - by1 + 1.0f;
+    const float ctr_x = bx1 + 0.5f * widths;
+    const float ctr_y = by1 + 0.5f * heights;
+    const float dx = d0 / wx, dy = d1 / wy;
+    const double dw = fmin((double)(d2 / ww), kBboxXformClip);
+    const double dh = fmin((double)(d3 / wh), kBboxXformClip);
+    const float pcx = dx * widths + ctr_x;
+    const float pcy = dy * heights + ctr_y;
+    const double pw = fmax(exp(dw) * (double)widths, 1.0);
+    const double ph = fmax(exp(dh) * (double)heights, 1.0);
+    x1 = (float)((double)pcx - 0.5 * pw);
+    y1 = (float)((double)pcy - 0.5 * ph);
+    x2 = (float)((double)pcx + 0.5 * pw - 1.0);
+    y2 = (float)((double)pcy + 0.5 * ph - 1.0);
+}
+
+__device__ __forceinline__ float clip_coord(float v, float hi) {  // max(min(v, hi), 0)
+    return fmaxf(fminf(v, hi), 0.f);
+}
+
+// utils/fpn.py:11-28 in numpy's float32 arithmetic
+__device__ __forceinline__ int fpn_level(float x1, float y1, float x2, float y2, int k_min,
+                                         int k_max, float s0, float lvl0) {
+    const float w = x2 - x1 + 1.0f, h = y2 - y1 + 1.0f;
+    float area = w * h;
+    if (area < 0.f) area = 0.f;
+    const float s = sqrtf(area);
+    const float t = s / s0 + 1e-6f;
+    const float l2 = (float)log2((double)t);  // correctly rounded float32 log2
+    float lv = floorf(lvl0 + l2);
+    lv = fminf(fmaxf(lv, (float)k_min), (float)k_max);
+    return (int)lv;
+}
+
+struct RpnLds {
+    uint64_t keys[kSelCap];          // 64 KiB: candidates, later NMS order keys
+    float px1[kPreMax], py1[kPreMax], px2[kPreMax], py2[kPreMax], psc[kPreMax];
+    float ox1[kPreMax], oy1[kPreMax], ox2[kPreMax], oy2[kPreMax], oar[kPreMax];
+    uint8_t keep_rank[kPreMax];
+    uint8_t keep_pos[kPreMax];
+    int scratch[32];
+};
+
+__global__ __launch_bounds__(1024) void rpn_proposals_kernel(
+    RpnArgs args, int num_levels, const float *__restrict__ im_info, int pre_nms_topN,
+    int post_nms_topN, float nms_thresh, float min_size, float *__restrict__ rois_out,
+    float *__restrict__ probs_out, int32_t *__restrict__ counts_out, char *__restrict__ ws,
+    size_t mask_bytes) {
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    RpnLds &L = *reinterpret_cast<RpnLds *>(lds_raw);
+    const int l = blockIdx.x, img = blockIdx.y;
+    const VdRpnLevel lv = args.lv[l];
+    const int A = lv.A, H = lv.H, W = lv.W, K = H * W;
+    const int n_all = K * A;
+    const float *probs = lv.cls_prob + (int64_t)img * A * K;
+    const float *deltas = lv.bbox_pred + (int64_t)img * 4 * A * K;
+    const int slot = img * num_levels + l;
+    uint64_t *mask = reinterpret_cast<uint64_t *>(ws + (size_t)slot * mask_bytes);
+
+    // element e = (h*W + w)*A + a lives at probs[a*K + h*W + w]
+    auto key_of = [&](int e) -> uint64_t {
+        const int a = e % A, hw = e / A;
+        const float s = probs[(int64_t)a * K + hw];
+        return ((uint64_t)float_key(s) << 32) | (uint32_t)(0xffffffffu - (uint32_t)e);
+    };
+    // memory-order walk for coalesced count passes: m = a*K + hw  ->  e
+    auto key_mem = [&](int m) -> uint64_t {
+        const int a = m / K, hw = m - a * K;
+        const int e = hw * A + a;
+        return ((uint64_t)float_key(probs[m]) << 32) | (uint32_t)(0xffffffffu - (uint32_t)e);
+    };
+
+    const bool take_all = pre_nms_topN <= 0 || pre_nms_topN >= n_all;
+    const int pre = take_all ? n_all : pre_nms_topN;
+    int ncand;
+    if (take_all) {
+        for (int e = threadIdx.x; e < n_all; e += blockDim.x) L.keys[e] = key_of(e);
+        ncand = n_all;
+        __syncthreads();
+    } else {
+        // ---- sample + threshold search
+        const int S = min(kSampleMax, n_all);
+        for (int j = threadIdx.x; j < kSampleMax; j += blockDim.x)
+            L.keys[j] = j < S ? key_of((int)(((int64_t)j * n_all) / S)) : 0ull;
+        __syncthreads();
+        bitonic_sort_desc(L.keys, kSampleMax);
+        int lo = 0, hi = S - 1;  // rank window in the sorted sample
+        int rank = (int)(((int64_t)2 * pre * S + n_all - 1) / n_all);
+        if (rank > S - 1) rank = S - 1;
+        uint64_t thr = 0;
+        ncand = -1;
+        for (int it = 0; it < 24; ++it) {
+            thr = L.keys[rank];
+            __syncthreads();
+            int c = 0;
+            for (int m = threadIdx.x; m < n_all; m += blockDim.x) c += key_mem(m) >= thr;
+            c = block_sum(c, L.scratch);
+            if (c >= pre && c <= kSelCap) { ncand = c; break; }
+            if (c < pre) lo = rank + 1; else hi = rank - 1;
+            if (lo > hi) break;
+            rank = (lo + hi) >> 1;
+        }
+        if (ncand < 0) {  // cannot bracket: signal and bail out (host reports)
+            if (threadIdx.x == 0) counts_out[slot] = -1;
+            return;
+        }
+        block_compact(
+            n_all, [&](int m) { return key_mem(m) >= thr; },
+            [&](int pos, int m) { L.keys[pos] = key_mem(m); }, L.scratch);
+    }
+    {
+        const int np2 = next_pow2(ncand);
+        for (int i = ncand + threadIdx.x; i < np2; i += blockDim.x) L.keys[i] = 0ull;
+        __syncthreads();
+        bitonic_sort_desc(L.keys, np2);
+    }
+
+    // ---- decode + clip + filter (positions in score order)
+    const float im_h = im_info[img * 3 + 0], im_w = im_info[img * 3 + 1];
+    const float ms = min_size * im_info[img * 3 + 2];
+    const double stride = 1.0 / (double)lv.spatial_scale;
+    for (int t = threadIdx.x; t < pre; t += blockDim.x) {
+        const uint64_t k = L.keys[t];
+        const int e = (int)(0xffffffffu - (uint32_t)k);
+        const int a = e % A, hw = e / A, h = hw / W, w = hw - h * W;
+        const double sx = (double)w * stride, sy = (double)h * stride;
+        const double *an = lv.anchors + a * 4;
+        const float bx1 = (float)(an[0] + sx), by1 = (float)(an[1] + sy);
+        const float bx2 = (float)(an[2] + sx), by2 = (float)(an[3] + sy);
+        const float *d = deltas + (int64_t)(4 * a) * K + hw;
+        float x1, y1, x2, y2;
+        decode_box(bx1, by1, bx2, by2, d[0], d[K], d[2 * K], d[3 * K], 1.f, 1.f, 1.f, 1.f, x1, y1,
+                   x2, y2);
+        x1 = clip_coord(x1, im_w - 1.f);
+        y1 = clip_coord(y1, im_h - 1.f);
+        x2 = clip_coord(x2, im_w - 1.f);
+        y2 = clip_coord(y2, im_h - 1.f);
+        L.ox1[t] = x1;
+        L.oy1[t] = y1;
+        L.ox2[t] = x2;
+        L.oy2[t] = y2;
+        L.oar[t] = key_float((uint32_t)(k >> 32));
+    }
+    __syncthreads();
+    const int m = block_compact(
+        pre,
+        [&](int t) {
+            const float ws_ = L.ox2[t] - L.ox1[t] + 1.f, hs = L.oy2[t] - L.oy1[t] + 1.f;
+            const float xc = L.ox1[t] + ws_ / 2.f, yc = L.oy1[t] + hs / 2.f;
+            return (ws_ >= ms) && (hs >= ms) && (xc < im_w) && (yc < im_h);
+        },
+        [&](int p, int t) {
+            L.px1[p] = L.ox1[t];
+            L.py1[p] = L.oy1[t];
+            L.px2[p] = L.ox2[t];
+            L.py2[p] = L.oy2[t];
+            L.psc[p] = L.oar[t];
+        },
+        L.scratch);
+
+    const int cap = post_nms_topN > 0 ? post_nms_topN : pre;
+    float *ro = rois_out + (size_t)slot * cap * 5;
+    float *po = probs_out + (size_t)slot * cap;
+    if (nms_thresh <= 0.f) {
+        const int n_out = min(m, cap);
+        for (int p = threadIdx.x; p < n_out; p += blockDim.x) {
+            ro[p * 5 + 0] = (float)img;
+            ro[p * 5 + 1] = L.px1[p];
+            ro[p * 5 + 2] = L.py1[p];
+            ro[p * 5 + 3] = L.px2[p];
+            ro[p * 5 + 4] = L.py2[p];
+            po[p] = L.psc[p];
+        }
+        if (threadIdx.x == 0) counts_out[slot] = n_out;
+        return;
+    }
+
+    // ---- NMS: processing order = scores.argsort()[::-1] on the sorted array
+    {
+        const int np2 = next_pow2(m);
+        for (int p = threadIdx.x; p < np2; p += blockDim.x)
+            L.keys[p] = p < m ? ((uint64_t)float_key(L.psc[p]) << 32) | (uint32_t)p : 0ull;
+        __syncthreads();
+        if (m > 1) bitonic_sort_desc(L.keys, np2);
+    }
+    for (int r = threadIdx.x; r < m; r += blockDim.x) {
+        const int p = (int)(uint32_t)L.keys[r];
+        const float a = L.px1[p], b = L.py1[p], c = L.px2[p], e = L.py2[p];
+        L.ox1[r] = a;
+        L.oy1[r] = b;
+        L.ox2[r] = c;
+        L.oy2[r] = e;
+        L.oar[r] = (c - a + 1) * (e - b + 1);
+    }
+    __syncthreads();
+    nms_build_mask_rows(L.ox1, L.oy1, L.ox2, L.oy2, L.oar, m, nms_thresh, mask, wave_id(),
+                        num_waves());
+    __threadfence_block();
+    __syncthreads();
+    if (wave_id() == 0) nms_resolve_wave(mask, m, L.keep_rank);
+    __syncthreads();
+    for (int r = threadIdx.x; r < m; r += blockDim.x)
+        L.keep_pos[(int)(uint32_t)L.keys[r]] = L.keep_rank[r];
+    __syncthreads();
+    const int kept = block_compact(
+        m, [&](int p) { return L.keep_pos[p] != 0; },
+        [&](int pos, int p) {
+            if (pos < cap) {
+                ro[pos * 5 + 0] = (float)img;
+                ro[pos * 5 + 1] = L.px1[p];
+                ro[pos * 5 + 2] = L.py1[p];
+                ro[pos * 5 + 3] = L.px2[p];
+                ro[pos * 5 + 4] = L.py2[p];
+                po[pos] = L.psc[p];
+            }
+        },
+        L.scratch);
+    if (threadIdx.x == 0) counts_out[slot] = min(kept, cap);
+}
+
+int launch_rpn_proposals(const VdRpnLevel *levels, int num_levels, int num_images,
+                         const float *im_info, int pre_nms_topN, int post_nms_topN,
+                         float nms_thresh, float min_size, float *rois_out, float *probs_out,
+                         int32_t *counts_out, void *workspace, size_t ws_bytes, hipStream_t s) {
+    if (num_levels < 1 || num_levels > VD_MAX_LEVELS || num_images < 1) return VD_ERR_ARG;
+    RpnArgs args;
+    int max_pre = 0;
+    for (int l = 0; l < num_levels; ++l) {
+        args.lv[l] = levels[l];
+        const int n_all = levels[l].A * levels[l].H * levels[l].W;
+        const bool take_all = pre_nms_topN <= 0 || pre_nms_topN >= n_all;
+        const int pre = take_all ? n_all : pre_nms_topN;
+        if (take_all && n_all > kSelCap) return VD_ERR_SHAPE;
+        if (pre > kPreMax) return VD_ERR_SHAPE;
+        if (post_nms_topN <= 0 && pre > kPreMax) return VD_ERR_SHAPE;
+        max_pre = pre > max_pre ? pre : max_pre;
+    }
+    if (post_nms_topN <= 0) return VD_ERR_ARG;  // output capacity is post_nms_topN
+    const size_t mb = rpn_mask_bytes(kPreMax < max_pre ? kPreMax : (max_pre < 64 ? 64 : max_pre));
+    if (!workspace || ws_bytes < mb * (size_t)num_levels * (size_t)num_images)
+        return VD_ERR_WORKSPACE;
+    hipLaunchKernelGGL(rpn_proposals_kernel, dim3(num_levels, num_images), dim3(1024),
+                       sizeof(RpnLds), s, args, num_levels, im_info, pre_nms_topN, post_nms_topN,
+                       nms_thresh, min_size, rois_out, probs_out, counts_out, (char *)workspace,
+                       mb);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+// --------------------------------------------------------------------------
+// collect + distribute (per image)
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void collect_distribute_kernel(
+    const float *__restrict__ level_rois, const float *__restrict__ level_probs,
+    const int32_t *__restrict__ level_counts, int num_levels, int level_cap, int post_nms_topN,
+    int k_min, int k_max, float *__restrict__ rois_out, int32_t *__restrict__ lvl_out,
+    int32_t *__restrict__ count_out) {
+    __shared__ uint64_t keys[kSelCap];
+    __shared__ int offs[VD_MAX_LEVELS + 1];
+    const int img = blockIdx.x;
+    if (threadIdx.x == 0) {
+        int o = 0;
+        for (int l = 0; l < num_levels; ++l) {
+            offs[l] = o;
+            const int c = level_counts[img * num_levels + l];
+            o += c > 0 ? c : 0;
+        }
+        offs[num_levels] = o;
+    }
+    __syncthreads();
+    const int n = offs[num_levels];
+    const int np2 = next_pow2(n < 1 ? 1 : n);
+    for (int q = threadIdx.x; q < np2; q += blockDim.x) {
+        uint64_t k = 0;
+        if (q < n) {
+            int l = 0;
+            while (q >= offs[l + 1]) ++l;
+            const int t = q - offs[l];
+            const float p = level_probs[((size_t)img * num_levels + l) * level_cap + t];
+            k = ((uint64_t)float_key(p) << 32) | (uint32_t)(0xffffffffu - (uint32_t)q);
+        }
+        keys[q] = k;
+    }
+    __syncthreads();
+    bitonic_sort_desc(keys, np2);
+    const int R = min(n, post_nms_topN);
+    for (int r = threadIdx.x; r < R; r += blockDim.x) {
+        const int q = (int)(0xffffffffu - (uint32_t)keys[r]);
+        int l = 0;
+        while (q >= offs[l + 1]) ++l;
+        const int t = q - offs[l];
+        const float *src = level_rois + (((size_t)img * num_levels + l) * level_cap + t) * 5;
+        float *dst = rois_out + ((size_t)img * post_nms_topN + r) * 5;
+        const float b = src[0], x1 = src[1], y1 = src[2], x2 = src[3], y2 = src[4];
+        dst[0] = b;
+        dst[1] = x1;
+        dst[2] = y1;
+        dst[3] = x2;
+        dst[4] = y2;
+        lvl_out[(size_t)img * post_nms_topN + r] =
+            fpn_level(x1, y1, x2, y2, k_min, k_max, 224.f, 4.f) - k_min;
+    }
+    if (threadIdx.x == 0) count_out[img] = R;
+}
+
+int launch_collect_distribute(const float *level_rois, const float *level_probs,
+                              const int32_t *level_counts, int num_levels, int level_cap,
+                              int num_images, int post_nms_topN, int k_min, int k_max,
+                              float *rois_out, int32_t *lvl_out, int32_t *count_out,
+                              hipStream_t s) {
+    if (num_levels < 1 || num_levels > VD_MAX_LEVELS || num_images < 1 || post_nms_topN < 1)
+        return VD_ERR_ARG;
+    if ((int64_t)num_levels * level_cap > kSelCap) return VD_ERR_SHAPE;
+    hipLaunchKernelGGL(collect_distribute_kernel, dim3(num_images), dim3(1024), 0, s, level_rois,
+                       level_probs, level_counts, num_levels, level_cap, post_nms_topN, k_min,
+                       k_max, rois_out, lvl_out, count_out);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+// --------------------------------------------------------------------------
+// stand-alone level map
+// --------------------------------------------------------------------------
+__global__ void map_levels_kernel(const float *__restrict__ rois, int stride, int col0, int R,
+                                  int k_min, int k_max, float s0, float lvl0,
+                                  int32_t *__restrict__ out) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= R) return;
+    const float *b = rois + (int64_t)r * stride + col0;
+    out[r] = fpn_level(b[0], b[1], b[2], b[3], k_min, k_max, s0, lvl0);
+}
+
+int launch_map_levels(const float *rois, int roi_stride, int col0, int R, int k_min, int k_max,
+                      float s0, float lvl0, int32_t *lvl_out, hipStream_t s) {
+    if (R <= 0) return VD_OK;
+    hipLaunchKernelGGL(map_levels_kernel, dim3((R + 255) / 256), dim3(256), 0, s, rois,
+                       roi_stride, col0, R, k_min, k_max, s0, lvl0, lvl_out);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+}  // namespace vd

@@ -1,0 +1,71 @@
+// Internal launcher declarations shared between the kernel translation units
+// and the C-ABI (capi.cpp).  Not part of the public interface (include/vosdet.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/vosdet.h"
+
+namespace vd {
+
+struct FpnLevels {
+    const float *feat[VD_MAX_LEVELS];
+    int H[VD_MAX_LEVELS];
+    int W[VD_MAX_LEVELS];
+    float scale[VD_MAX_LEVELS];
+};
+
+int launch_roi_align_fwd_nchw(const float *feat, int B, int C, int H, int W, const float *rois,
+                              int R, int PH, int PW, float scale, int sr, float *out,
+                              hipStream_t s);
+int launch_roi_align_bwd_nchw(const float *top_diff, int B, int C, int H, int W,
+                              const float *rois, int R, int PH, int PW, float scale, int sr,
+                              float *bottom_diff, hipStream_t s);
+int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, const int *lvl,
+                              const int *order, int R, int PH, int PW, int sr, float *out,
+                              hipStream_t s);
+
+int launch_roi_align_legacy_fwd(const float *feat, int B, int C, int H, int W, const float *rois,
+                                int R, int PH, int PW, float scale, float *out, hipStream_t s);
+int launch_roi_pool_fwd(const float *feat, int B, int C, int H, int W, const float *rois, int R,
+                        int PH, int PW, float scale, float *out, int32_t *argmax, hipStream_t s);
+int launch_roi_pool_bwd(const float *top_diff, const int32_t *argmax, int64_t n_out,
+                        float *bottom_diff, hipStream_t s);
+int launch_roi_crop_fwd(const float *in, int B, int C, int H, int W, const float *grid, int R,
+                        int GH, int GW, float *out, hipStream_t s);
+
+int launch_nms(const float *dets, int n, int stride, float thresh, int64_t *keep, int32_t *nkeep,
+               void *workspace, size_t ws_bytes, hipStream_t s);
+size_t nms_workspace_bytes(int n);
+
+int launch_map_levels(const float *rois, int roi_stride, int col0, int R, int k_min, int k_max,
+                      float s0, float lvl0, int32_t *lvl_out, hipStream_t s);
+
+int launch_rpn_proposals(const VdRpnLevel *levels, int num_levels, int num_images,
+                         const float *im_info, int pre_nms_topN, int post_nms_topN,
+                         float nms_thresh, float min_size, float *rois_out, float *probs_out,
+                         int32_t *counts_out, void *workspace, size_t ws_bytes, hipStream_t s);
+size_t rpn_workspace_bytes(const VdRpnLevel *levels, int num_levels, int num_images,
+                           int pre_nms_topN);
+
+int launch_collect_distribute(const float *level_rois, const float *level_probs,
+                              const int32_t *level_counts, int num_levels, int level_cap,
+                              int num_images, int post_nms_topN, int k_min, int k_max,
+                              float *rois_out, int32_t *lvl_out, int32_t *count_out,
+                              hipStream_t s);
+
+int launch_box_detections(const float *rois, const float *cls_prob, const float *bbox_pred,
+                          const int32_t *roi_count, int R_cap, int num_images, int num_classes,
+                          const float *im_scale, const int32_t *im_hw, float score_thresh,
+                          float nms_thresh, int dets_per_im, const float *bbox_weights,
+                          int det_cap, float *dets_out, int32_t *det_cls_out,
+                          int32_t *det_count_out, void *workspace, size_t ws_bytes,
+                          hipStream_t s);
+size_t box_detections_workspace_bytes(int R_cap, int num_images, int num_classes);
+
+int launch_image_to_blob(const uint8_t *frames, int F, int H, int W, const float *lut,
+                         int Hp, int Wp, int nhwc, float *blob, hipStream_t s);
+int launch_nchw_to_nhwc(const float *in, int B, int C, int H, int W, float *out, hipStream_t s);
+
+}  // namespace vd

@@ -1,0 +1,390 @@
+"""Torch-facing wrappers over the C ABI (libvosdet.so).
+
+Every function takes device tensors, launches on torch's current HIP stream and
+returns device tensors; shapes and dtypes are checked here, and any kernel
+status other than VD_OK raises.  PyTorch is used for allocation and streams
+only -- all arithmetic happens in the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _need(t: torch.Tensor, name: str, dtype=torch.float32) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError("%s must be a torch.Tensor" % name)
+    if not t.is_cuda:
+        raise ValueError("%s must be a device (HIP) tensor; there is no CPU path" % name)
+    if t.dtype != dtype:
+        raise TypeError("%s must be %s, got %s" % (name, dtype, t.dtype))
+    return t.contiguous()
+
+
+def _ws(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+# --------------------------------------------------------------------------- #
+# RoIAlign (Caffe2)                                                            #
+# --------------------------------------------------------------------------- #
+def roi_align_forward(features, rois, aligned_height, aligned_width, spatial_scale,
+                      sampling_ratio):
+    """RoIAlignFunction.forward (roi_xfrom/roi_align/functions/roi_align.py:16-32) on
+    NCHW features; returns R x C x ah x aw."""
+    f = _need(features, "features")
+    r = _need(rois, "rois")
+    if f.dim() != 4 or r.dim() != 2:
+        raise ValueError("features must be 4-D NCHW and rois 2-D")
+    B, C, H, W = f.shape
+    R = r.shape[0]
+    out = torch.empty((R, C, aligned_height, aligned_width), dtype=torch.float32, device=f.device)
+    if R == 0:
+        return out
+    check(lib().vd_roi_align_forward(int(aligned_height), int(aligned_width),
+                                     float(spatial_scale), int(sampling_ratio), f.data_ptr(),
+                                     B, C, H, W, r.data_ptr(), R, r.shape[1], out.data_ptr(),
+                                     _stream()), "vd_roi_align_forward")
+    return out
+
+
+def roi_align_backward(top_grad, rois, feat_shape, spatial_scale, sampling_ratio):
+    g = _need(top_grad, "top_grad")
+    r = _need(rois, "rois")
+    B, C, H, W = feat_shape
+    R, _, ah, aw = g.shape
+    out = torch.zeros((B, C, H, W), dtype=torch.float32, device=g.device)
+    if R == 0:
+        return out
+    check(lib().vd_roi_align_backward(ah, aw, float(spatial_scale), int(sampling_ratio),
+                                      g.data_ptr(), B, C, H, W, r.data_ptr(), R, r.shape[1],
+                                      out.data_ptr(), _stream()), "vd_roi_align_backward")
+    return out
+
+
+class _RoIAlignAutograd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, features, rois, ah, aw, scale, sr):
+        ctx.save_for_backward(rois)
+        ctx.meta = (tuple(features.shape), scale, sr)
+        return roi_align_forward(features, rois, ah, aw, scale, sr)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        (rois,) = ctx.saved_tensors
+        shape, scale, sr = ctx.meta
+        g = roi_align_backward(grad_out, rois, shape, scale, sr)
+        return g, None, None, None, None, None
+
+
+class RoIAlignFunction:
+    """Drop-in for the reference's old-style ``RoIAlignFunction(aligned_height,
+    aligned_width, spatial_scale, sampling_ratio)(features, rois)``
+    (lib/modeling/roi_xfrom/roi_align/functions/roi_align.py:7-48).  The
+    reference raises NotImplementedError for CPU tensors (:29-30); so does this
+    one (there is no CPU path)."""
+
+    def __init__(self, aligned_height, aligned_width, spatial_scale, sampling_ratio):
+        self.aligned_width = int(aligned_width)
+        self.aligned_height = int(aligned_height)
+        self.spatial_scale = float(spatial_scale)
+        self.sampling_ratio = int(sampling_ratio)
+
+    def __call__(self, features, rois):
+        if not features.is_cuda:
+            raise NotImplementedError("RoIAlign has no CPU implementation")
+        return _RoIAlignAutograd.apply(features, rois, self.aligned_height, self.aligned_width,
+                                       self.spatial_scale, self.sampling_ratio)
+
+    forward = __call__
+
+
+class RoIAlign(torch.nn.Module):
+    """modules/roi_align.py:6-17 counterpart."""
+
+    def __init__(self, aligned_height, aligned_width, spatial_scale, sampling_ratio):
+        super().__init__()
+        self.fn = RoIAlignFunction(aligned_height, aligned_width, spatial_scale, sampling_ratio)
+
+    def forward(self, features, rois):
+        return self.fn(features, rois)
+
+
+def roi_align_fpn(levels: Sequence[torch.Tensor], spatial_scales: Sequence[float],
+                  rois: torch.Tensor, roi_level: Optional[torch.Tensor], resolution: int,
+                  sampling_ratio: int, layout: str = "nhwc",
+                  roi_order: Optional[torch.Tensor] = None,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One-launch multi-level RoIAlign (replaces the per-level loop + cat + restore
+    of model_builder.py:252-303).  levels: finest first, each B x H x W x C
+    (layout 'nhwc') or B x C x H x W ('nchw', single level only).  roi_level[r]
+    is the index into ``levels``.  Output row r belongs to rois[r]."""
+    if len(levels) < 1 or len(levels) > _lib.VD_MAX_LEVELS:
+        raise ValueError("1..%d levels" % _lib.VD_MAX_LEVELS)
+    r = _need(rois, "rois")
+    nhwc = layout == "nhwc"
+    descs = (_lib.VdFeatLevel * len(levels))()
+    keep = []
+    for i, (t, sc) in enumerate(zip(levels, spatial_scales)):
+        t = _need(t, "levels[%d]" % i)
+        keep.append(t)
+        if nhwc:
+            B, H, W, C = t.shape
+        else:
+            B, C, H, W = t.shape
+        descs[i] = _lib.VdFeatLevel(t.data_ptr(), H, W, float(sc))
+    R = r.shape[0]
+    if out is None:
+        out = torch.empty((R, C, resolution, resolution), dtype=torch.float32, device=r.device)
+    if R == 0:
+        return out
+    lv = _need(roi_level, "roi_level", torch.int32) if roi_level is not None else None
+    od = _need(roi_order, "roi_order", torch.int32) if roi_order is not None else None
+    check(lib().vd_roi_align_fpn_forward(
+        descs, len(levels), B, C, _lib.VD_LAYOUT_NHWC if nhwc else _lib.VD_LAYOUT_NCHW,
+        r.data_ptr(), lv.data_ptr() if lv is not None else None,
+        od.data_ptr() if od is not None else None, R, resolution, resolution,
+        int(sampling_ratio), out.data_ptr(), _stream()), "vd_roi_align_fpn_forward")
+    return out
+
+
+# --------------------------------------------------------------------------- #
+# lib/model ops: legacy RoIAlign, RoIPool, RoICrop                             #
+# --------------------------------------------------------------------------- #
+def roi_align_legacy(features, rois, aligned_height, aligned_width, spatial_scale):
+    """jwyang RoIAlignFunction (lib/model/roi_align/functions/roi_align.py)."""
+    f = _need(features, "features")
+    r = _need(rois, "rois")
+    B, C, H, W = f.shape
+    R = r.shape[0]
+    out = torch.zeros((R, C, aligned_height, aligned_width), dtype=torch.float32, device=f.device)
+    if R:
+        check(lib().vd_roi_align_legacy_forward(aligned_height, aligned_width,
+                                                float(spatial_scale), f.data_ptr(), B, C, H, W,
+                                                r.data_ptr(), R, out.data_ptr(), _stream()),
+              "vd_roi_align_legacy_forward")
+    return out
+
+
+class _RoIPoolAutograd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, features, rois, ph, pw, scale):
+        f = _need(features, "features")
+        r = _need(rois, "rois")
+        B, C, H, W = f.shape
+        R = r.shape[0]
+        out = torch.zeros((R, C, ph, pw), dtype=torch.float32, device=f.device)
+        arg = torch.full((R, C, ph, pw), -1, dtype=torch.int32, device=f.device)
+        if R:
+            check(lib().vd_roi_pool_forward(ph, pw, float(scale), f.data_ptr(), B, C, H, W,
+                                            r.data_ptr(), R, out.data_ptr(), arg.data_ptr(),
+                                            _stream()), "vd_roi_pool_forward")
+        ctx.save_for_backward(arg)
+        ctx.shape = (B, C, H, W)
+        return out, arg
+
+    @staticmethod
+    def backward(ctx, grad_out, _grad_arg):
+        (arg,) = ctx.saved_tensors
+        g = _need(grad_out, "grad_out")
+        bottom = torch.zeros(ctx.shape, dtype=torch.float32, device=g.device)
+        check(lib().vd_roi_pool_backward(g.data_ptr(), arg.data_ptr(), g.numel(),
+                                         bottom.data_ptr(), _stream()), "vd_roi_pool_backward")
+        return bottom, None, None, None, None
+
+
+class RoIPoolFunction:
+    """``RoIPoolFunction(pooled_height, pooled_width, spatial_scale)(features, rois)``
+    (lib/model/roi_pooling/functions/roi_pool.py:6-38), CUDA-kernel semantics."""
+
+    def __init__(self, pooled_height, pooled_width, spatial_scale):
+        self.pooled_height = int(pooled_height)
+        self.pooled_width = int(pooled_width)
+        self.spatial_scale = float(spatial_scale)
+        self.argmax = None
+
+    def __call__(self, features, rois):
+        out, self.argmax = _RoIPoolAutograd.apply(features, rois, self.pooled_height,
+                                                  self.pooled_width, self.spatial_scale)
+        return out
+
+
+class RoICropFunction:
+    """``RoICropFunction()(input_BCHW, grid_yx)`` (lib/model/roi_crop/functions/roi_crop.py:7-15)."""
+
+    def __call__(self, input1, input2):
+        f = _need(input1, "input")
+        g = _need(input2, "grid")
+        B, C, H, W = f.shape
+        R, GH, GW, two = g.shape
+        if two != 2:
+            raise ValueError("grid must be R x GH x GW x 2 (y, x)")
+        out = torch.zeros((R, C, GH, GW), dtype=torch.float32, device=f.device)
+        if R:
+            check(lib().vd_roi_crop_forward(f.data_ptr(), B, C, H, W, g.data_ptr(), R, GH, GW,
+                                            out.data_ptr(), _stream()), "vd_roi_crop_forward")
+        return out
+
+
+# --------------------------------------------------------------------------- #
+# NMS / levels                                                                 #
+# --------------------------------------------------------------------------- #
+def nms(dets: torch.Tensor, thresh: float) -> torch.Tensor:
+    """cython_nms.nms semantics on device: dets N x (>=5) fp32 -> kept indices
+    (int64, ascending)."""
+    d = _need(dets, "dets")
+    n = d.shape[0]
+    keep = torch.empty((max(n, 1),), dtype=torch.int64, device=d.device)
+    num = torch.zeros((1,), dtype=torch.int32, device=d.device)
+    wsb = lib().vd_nms_workspace_size(n)
+    ws = _ws(wsb, d.device)
+    check(lib().vd_nms(d.data_ptr() if n else None, n, d.shape[1] if d.dim() == 2 else 5,
+                       float(np.float32(thresh)), keep.data_ptr(), num.data_ptr(),
+                       ws.data_ptr(), ws.numel(), _stream()), "vd_nms")
+    return keep[: int(num.item())]
+
+
+def map_rois_to_fpn_levels(rois: torch.Tensor, k_min: int, k_max: int, col0: int = 1,
+                           canonical_scale: float = 224., canonical_level: float = 4.):
+    """utils/fpn.py:11-28 on device; returns int32 levels (k_min..k_max)."""
+    r = _need(rois, "rois")
+    R = r.shape[0]
+    out = torch.empty((R,), dtype=torch.int32, device=r.device)
+    if R:
+        check(lib().vd_map_rois_to_fpn_levels(r.data_ptr(), r.shape[1], col0, R, k_min, k_max,
+                                              float(canonical_scale), float(canonical_level),
+                                              out.data_ptr(), _stream()),
+              "vd_map_rois_to_fpn_levels")
+    return out
+
+
+def nchw_to_nhwc(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    t = _need(x, "x")
+    B, C, H, W = t.shape
+    if out is None:
+        out = torch.empty((B, H, W, C), dtype=torch.float32, device=t.device)
+    check(lib().vd_nchw_to_nhwc(t.data_ptr(), B, C, H, W, out.data_ptr(), _stream()),
+          "vd_nchw_to_nhwc")
+    return out
+
+
+def pixel_lut(pixel_means=(102.9801, 115.9465, 122.7717)) -> np.ndarray:
+    """float32(u - mean_c) for u in 0..255 exactly as numpy computes
+    ``im.astype(float32); im -= PIXEL_MEANS`` (float64 subtraction, float32 store,
+    lib/utils/blob.py:126-127)."""
+    u = np.arange(256, dtype=np.float32).astype(np.float64)
+    return np.stack([(u - m).astype(np.float32) for m in pixel_means]).reshape(-1)
+
+
+def image_to_blob(frames: torch.Tensor, lut: torch.Tensor, Hp: int, Wp: int, nhwc: bool = False,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    fr = _need(frames, "frames", torch.uint8)
+    F, H, W, three = fr.shape
+    lt = _need(lut, "lut")
+    if out is None:
+        shape = (F, Hp, Wp, 3) if nhwc else (F, 3, Hp, Wp)
+        out = torch.empty(shape, dtype=torch.float32, device=fr.device)
+    check(lib().vd_image_to_blob(fr.data_ptr(), F, H, W, lt.data_ptr(), Hp, Wp, int(nhwc),
+                                 out.data_ptr(), _stream()), "vd_image_to_blob")
+    return out
+
+
+# --------------------------------------------------------------------------- #
+# Proposals, collect/distribute, detections                                    #
+# --------------------------------------------------------------------------- #
+def generate_proposals(cls_probs: Sequence[torch.Tensor], bbox_preds: Sequence[torch.Tensor],
+                       anchors: Sequence[torch.Tensor], spatial_scales: Sequence[float],
+                       im_info: torch.Tensor, pre_nms_topN: int, post_nms_topN: int,
+                       nms_thresh: float, min_size: float, out=None):
+    """GenerateProposalsOp over all levels / images.  Returns (rois [N,L,post,5],
+    probs [N,L,post], counts int32 [N,L])."""
+    L = len(cls_probs)
+    descs = (_lib.VdRpnLevel * L)()
+    keep = []
+    N = cls_probs[0].shape[0]
+    for i in range(L):
+        p = _need(cls_probs[i], "cls_prob")
+        d = _need(bbox_preds[i], "bbox_pred")
+        a = _need(anchors[i], "anchors", torch.float64)
+        keep += [p, d, a]
+        _, A, H, W = p.shape
+        descs[i] = _lib.VdRpnLevel(p.data_ptr(), d.data_ptr(), a.data_ptr(), A, H, W,
+                                   float(spatial_scales[i]))
+    info = _need(im_info, "im_info")
+    dev = info.device
+    if out is None:
+        rois = torch.zeros((N, L, post_nms_topN, 5), dtype=torch.float32, device=dev)
+        probs = torch.zeros((N, L, post_nms_topN), dtype=torch.float32, device=dev)
+        counts = torch.zeros((N, L), dtype=torch.int32, device=dev)
+    else:
+        rois, probs, counts = out
+    wsb = lib().vd_generate_proposals_workspace_size(descs, L, N, pre_nms_topN)
+    ws = _ws(wsb, dev)
+    check(lib().vd_generate_proposals(descs, L, N, info.data_ptr(), int(pre_nms_topN),
+                                      int(post_nms_topN), float(np.float32(nms_thresh)),
+                                      float(min_size), rois.data_ptr(), probs.data_ptr(),
+                                      counts.data_ptr(), ws.data_ptr(), ws.numel(), _stream()),
+          "vd_generate_proposals")
+    return rois, probs, counts
+
+
+def collect_distribute(level_rois, level_probs, level_counts, post_nms_topN: int, k_min: int = 2,
+                       k_max: int = 5, out=None):
+    """collect + distribute per image: returns (rois [N,post,5], lvl idx int32
+    [N,post] (level - k_min), counts int32 [N])."""
+    lr = _need(level_rois, "level_rois")
+    lp = _need(level_probs, "level_probs")
+    lc = _need(level_counts, "level_counts", torch.int32)
+    N, L, cap, _ = lr.shape
+    if out is None:
+        rois = torch.zeros((N, post_nms_topN, 5), dtype=torch.float32, device=lr.device)
+        lvl = torch.zeros((N, post_nms_topN), dtype=torch.int32, device=lr.device)
+        cnt = torch.zeros((N,), dtype=torch.int32, device=lr.device)
+    else:
+        rois, lvl, cnt = out
+    check(lib().vd_collect_distribute(lr.data_ptr(), lp.data_ptr(), lc.data_ptr(), L, cap, N,
+                                      int(post_nms_topN), k_min, k_max, rois.data_ptr(),
+                                      lvl.data_ptr(), cnt.data_ptr(), _stream()),
+          "vd_collect_distribute")
+    return rois, lvl, cnt
+
+
+def box_detections(rois, cls_prob, bbox_pred, roi_count, im_scale, im_hw, score_thresh=0.05,
+                   nms_thresh=0.5, dets_per_im=100, bbox_reg_weights=(10., 10., 5., 5.),
+                   det_cap=256, out=None):
+    """Decode + clip + per-class NMS + detections limit.  rois [N,R,5],
+    cls_prob [N,R,K], bbox_pred [N,R,4K] -> (dets [N,cap,5], cls int32 [N,cap],
+    counts int32 [N])."""
+    r = _need(rois, "rois")
+    p = _need(cls_prob, "cls_prob")
+    d = _need(bbox_pred, "bbox_pred")
+    c = _need(roi_count, "roi_count", torch.int32)
+    s = _need(im_scale, "im_scale")
+    hw = _need(im_hw, "im_hw", torch.int32)
+    N, R, K = p.shape
+    if out is None:
+        dets = torch.zeros((N, det_cap, 5), dtype=torch.float32, device=r.device)
+        cls = torch.zeros((N, det_cap), dtype=torch.int32, device=r.device)
+        cnt = torch.zeros((N,), dtype=torch.int32, device=r.device)
+    else:
+        dets, cls, cnt = out
+    wsb = lib().vd_box_detections_workspace_size(R, N, K)
+    ws = _ws(wsb, r.device)
+    w = (ctypes.c_float * 4)(*[float(np.float32(x)) for x in bbox_reg_weights])
+    check(lib().vd_box_detections(r.data_ptr(), p.data_ptr(), d.data_ptr(), c.data_ptr(), R, N, K,
+                                  s.data_ptr(), hw.data_ptr(), float(np.float32(score_thresh)),
+                                  float(np.float32(nms_thresh)), int(dets_per_im),
+                                  ctypes.cast(w, ctypes.c_void_p), det_cap, dets.data_ptr(),
+                                  cls.data_ptr(), cnt.data_ptr(), ws.data_ptr(), ws.numel(),
+                                  _stream()), "vd_box_detections")
+    return dets, cls, cnt
