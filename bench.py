@@ -1,0 +1,246 @@
+#!/usr/bin/env python3
+"""Benchmark: frames/s of e2e_mask_rcnn_R-50-FPN_1x inference on synthetic
+800x1333 frames (BASELINE.json configs[1]), plus the RoIAlign HBM roofline and
+the reference CPU path timed on the host.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch F]
+
+One process per GPU (torchrun for N>1, RCCL).  A step = every rank runs the full
+per-frame hot path on its own F frames (already resident in HBM as u8), then one
+all_gather of the fixed-size padded detections + masks collects every rank's
+results (weak scaling: per-GPU work is fixed).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def synthetic_frames(n, seed0, h=800, w=1333):
+    return np.stack([np.random.RandomState(seed0 + i).randint(0, 256, (h, w, 3), np.uint8)
+                     for i in range(n)])
+
+
+def synthetic_rois(seed, R=1000, img_w=1333, img_h=800, batch_idx=0):
+    """SURVEY.md §8(d) synthetic proposals."""
+    rng = np.random.default_rng(seed)
+    s = np.exp(rng.uniform(np.log(16), np.log(512), R))
+    a = np.exp(rng.uniform(np.log(0.5), np.log(2), R))
+    w, h = s / np.sqrt(a), s * np.sqrt(a)
+    cx, cy = rng.uniform(0, img_w, R), rng.uniform(0, img_h, R)
+    x1 = np.clip(cx - w / 2, 0, img_w - 1)
+    y1 = np.clip(cy - h / 2, 0, img_h - 1)
+    x2 = np.clip(cx + w / 2, 0, img_w - 1)
+    y2 = np.clip(cy + h / 2, 0, img_h - 1)
+    return np.stack([np.full(R, batch_idx), x1, y1, x2, y2], 1).astype(np.float32)
+
+
+def fpn_levels_np(rois):
+    w = rois[:, 3] - rois[:, 1] + 1
+    h = rois[:, 4] - rois[:, 2] + 1
+    s = np.sqrt(np.maximum(w * h, 0))
+    return np.clip(np.floor(4 + np.log2(s / 224 + 1e-6)), 2, 5).astype(np.int32)
+
+
+def roi_align_algorithmic_bytes(rois, lvls, sizes, C, P):
+    """4*C*|union of per-RoI footprints| per level + outputs + rois."""
+    touched = 0
+    for li, (H, W) in enumerate(sizes):
+        m = np.zeros((H, W), bool)
+        sel = rois[lvls == li]
+        sc = 1.0 / 2 ** (li + 2)
+        for r in sel:
+            x1, y1, x2, y2 = r[1] * sc, r[2] * sc, r[3] * sc, r[4] * sc
+            ya, xa = int(math.floor(y1)), int(math.floor(x1))
+            yb = int(math.floor(max(y2, y1 + 1))) + 1
+            xb = int(math.floor(max(x2, x1 + 1))) + 1
+            m[max(ya, 0):min(yb + 1, H), max(xa, 0):min(xb + 1, W)] = True
+        touched += int(m.sum())
+    return 4 * C * touched + 4 * len(rois) * C * P * P + 20 * len(rois)
+
+
+def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=50):
+    """RoIAlign (FPN NHWC, one launch over 4 levels x `frames` images) timed with HIP
+    events on the launch stream; >= 8 distinct frames so the working set (>700 MB)
+    exceeds the 256 MB Infinity Cache."""
+    from vosdetectron_amd import ops
+    sizes = [(200, 336), (100, 168), (50, 84), (25, 42)]
+    scales = [1. / 4, 1. / 8, 1. / 16, 1. / 32]
+    g = torch.Generator(device=dev).manual_seed(1)
+    pyr = [torch.randn((frames, h, w, C), generator=g, device=dev) for h, w in sizes]
+    rois, lvls, nbytes = [], [], 0
+    for f in range(frames):
+        r = synthetic_rois(f, R, batch_idx=f)
+        lv = fpn_levels_np(r) - 2
+        nbytes += roi_align_algorithmic_bytes(r, lv, sizes, C, P)
+        rois.append(r)
+        lvls.append(lv)
+    rois_t = torch.from_numpy(np.concatenate(rois)).to(dev)
+    lv_t = torch.from_numpy(np.concatenate(lvls)).to(dev)
+    out = torch.empty((frames * R, C, P, P), device=dev)
+    s = torch.cuda.current_stream()
+    for _ in range(3):
+        ops.roi_align_fpn(pyr, scales, rois_t, lv_t, P, sr, out=out)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        ops.roi_align_fpn(pyr, scales, rois_t, lv_t, P, sr, out=out)
+    e1.record(s)
+    e1.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / iters
+    achieved = nbytes / t / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "roi_align_fpn_nhwc_kernel<7>",
+            "launch": "%d frames x %d RoIs, C=%d, P=%d, sr=%d" % (frames, R, C, P, sr),
+            "algorithmic_bytes_per_launch": int(nbytes), "avg_launch_us": round(t * 1e6, 2)}
+
+
+def cpu_baseline(cfg_name, sd, n_frames=2, threads=None):
+    """The reference's CPU path (oracle/pipeline.py) on a bounded sample."""
+    from oracle.pipeline import RefCPUPipeline
+    threads = threads or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    blocks = {"e2e_mask_rcnn_R-50-FPN_1x": (3, 4, 6, 3),
+              "e2e_mask_rcnn_R-101-FPN_2x": (3, 4, 23, 3)}[cfg_name]
+    ref = RefCPUPipeline(sd, block_counts=blocks)
+    fr = synthetic_frames(n_frames + 1, 1000)
+    ref(fr[0])  # warm-up
+    t0 = time.perf_counter()
+    for i in range(n_frames):
+        ref(fr[i + 1])
+    dt = time.perf_counter() - t0
+    return {"value": round(n_frames / dt, 4), "unit": "frames/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d synthetic 800x1333 frames, full im_detect_all path (torch-CPU convs, "
+                      "oracle C RoIAlign/NMS, numpy proposals), %.1f s, cpu=%s" % (
+                          n_frames, dt, platform.processor() or platform.machine())}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4, help="frames per GPU per step")
+    ap.add_argument("--config", default="e2e_mask_rcnn_R-50-FPN_1x")
+    ap.add_argument("--layout", default="nchw", choices=["nchw", "nhwc"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=2)
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.backends.cudnn.benchmark = True
+
+    from vosdetectron_amd import config as vcfg
+    from vosdetectron_amd.engine import FramePipeline
+    from vosdetectron_amd.weights import build_model
+
+    cfg = vcfg.get(args.config)
+    model, sd = build_model(cfg, seed=0, device=dev, channels_last=args.layout == "nhwc")
+    pipe = FramePipeline(model, cfg, batch=args.batch, channels_last=args.layout == "nhwc",
+                         device=dev)
+    F = args.batch
+    frames = torch.from_numpy(synthetic_frames(F, 1 + rank * F)).to(dev)
+
+    cap, MR = pipe.det_cap, cfg.MRCNN.RESOLUTION
+    gathered = None
+    if world > 1:
+        import torch.distributed as dist
+        pad_dets = torch.zeros((F, cap, 5), device=dev)
+        pad_cls = torch.zeros((F, cap), dtype=torch.int32, device=dev)
+        pad_masks = torch.zeros((F, cap, MR, MR), device=dev)
+        g_dets = torch.zeros((world * F, cap, 5), device=dev)
+        g_cls = torch.zeros((world * F, cap), dtype=torch.int32, device=dev)
+        g_cnt = torch.zeros((world * F,), dtype=torch.int32, device=dev)
+        g_masks = torch.zeros((world * F, cap, MR, MR), device=dev)
+
+    def step():
+        out = pipe.run(frames)
+        if world > 1:
+            counts = out["counts_host"]
+            pad_masks.zero_()
+            o = 0
+            for f, c in enumerate(counts):
+                pad_masks[f, :c] = out["masks"][o:o + c]
+                o += c
+            dist.all_gather_into_tensor(g_dets, out["dets"].contiguous())
+            dist.all_gather_into_tensor(g_cls, out["classes"].contiguous())
+            dist.all_gather_into_tensor(g_cnt, out["counts"].contiguous())
+            dist.all_gather_into_tensor(g_masks, pad_masks)
+        return out
+
+    for _ in range(args.warmup):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    dets_per_frame = float(np.mean(out["counts_host"]))
+
+    roof = None
+    if not args.no_roofline and rank == 0:
+        roof = measure_roialign_roofline(dev)
+    cpu = None
+    if not args.no_cpu_baseline and rank == 0 and world == 1:
+        cpu = cpu_baseline(args.config, sd, args.cpu_frames)
+
+    if rank == 0:
+        fps = world * F * args.steps / dt
+        line = {
+            "metric": "frames/sec @1333x800 e2e_mask_rcnn_R-50-FPN, 1/2/4/8 MI355X; "
+                      "RoIAlign HBM GB/s",
+            "value": round(fps, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (u8 800x1333 frames, RandomState seeds; deterministic "
+                    "N(0,1/fan_in) weights)",
+            "config": {"workload": "%s inference, %d synthetic 800x1333 frames per GPU per step, "
+                                   "full im_detect_all path (proposals, box head, class NMS, "
+                                   "mask head)" % (args.config, F),
+                       "frames_per_gpu_step": F, "global_batch": world * F,
+                       "parallelism": "frame-sharded dp%d + RCCL all_gather" % world,
+                       "layout": args.layout, "dets_per_frame": dets_per_frame},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

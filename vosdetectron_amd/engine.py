@@ -1,0 +1,150 @@
+"""Device-resident per-frame inference engine (the hot path).
+
+Replaces the host-driven chain of lib/core/test.py im_detect_all (:50-111):
+im_detect_bbox (:128-190) -> box_results_with_nms_and_limit (:733-797) ->
+im_detect_mask (:366-402), for a batch of F frames already resident in HBM:
+
+  u8 frames --vd_image_to_blob--> blob --PyTorch ResNet-FPN--> P2..P6
+  --PyTorch RPN convs--> vd_generate_proposals (all levels, all frames)
+  --> vd_collect_distribute --> vd_roi_align_fpn (one launch, NHWC pyramid)
+  --> PyTorch fc6/fc7/cls/bbox --> vd_box_detections (decode, clip, class NMS,
+  top-100) --> [one D2H of the detection counts] --> mask rois + level map
+  --> vd_roi_align_fpn 14x14 --> PyTorch mask head --> class-selected 28x28.
+
+The reference crosses host<->device 5+5 times in proposals alone and twice per
+roi_feature_transform; here the only host read is the per-frame detection
+count that sizes the mask-head batch.  Outputs match the reference's
+`cls_boxes` rows (class-major, proposal order) and the class-selected masks
+that segm_results consumes (segm_results' paste/RLE is out of scope).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import ops
+
+
+class FramePipeline:
+    def __init__(self, model, cfg, frame_hw=(800, 1333), batch=1, channels_last=False,
+                 det_cap=256, device="cuda"):
+        self.model = model
+        self.cfg = cfg
+        self.F = batch
+        self.H, self.W = frame_hw
+        self.device = torch.device(device)
+        self.channels_last = channels_last
+        self.det_cap = det_cap
+        # blob geometry (lib/utils/blob.py:37-161); identity scale only
+        smin, smax = min(frame_hw), max(frame_hw)
+        scale = float(cfg.TEST.SCALE) / float(smin)
+        if np.round(scale * smax) > cfg.TEST.MAX_SIZE:
+            scale = float(cfg.TEST.MAX_SIZE) / float(smax)
+        if scale != 1.0:
+            raise NotImplementedError(
+                "frames must be at the configured test scale (cv2.resize is outside the "
+                "hot path); got im_scale %.4f" % scale)
+        self.im_scale = scale
+        st = cfg.FPN.COARSEST_STRIDE
+        self.Hp = int(math.ceil(self.H / st) * st)
+        self.Wp = int(math.ceil(self.W / st) * st)
+        self.lut = torch.from_numpy(ops.pixel_lut(cfg.PIXEL_MEANS)).to(self.device)
+        F = batch
+        self.im_info = torch.tensor([[self.Hp, self.Wp, scale]] * F, dtype=torch.float32,
+                                    device=self.device)
+        self.im_scale_t = torch.full((F,), scale, dtype=torch.float32, device=self.device)
+        self.im_hw = torch.tensor([[self.H, self.W]] * F, dtype=torch.int32, device=self.device)
+        k_min, k_max = cfg.FPN.RPN_MIN_LEVEL, cfg.FPN.RPN_MAX_LEVEL
+        self.rpn_levels = list(range(k_min, k_max + 1))
+        self.anchors = [getattr(model, "anchors_fpn%d" % l).to(self.device)
+                        for l in self.rpn_levels]
+        self.rpn_scales = [1. / 2 ** l for l in self.rpn_levels]
+        self.roi_levels = list(range(cfg.FPN.ROI_MIN_LEVEL, cfg.FPN.ROI_MAX_LEVEL + 1))
+        self.roi_scales = [1. / 2 ** l for l in self.roi_levels]
+        self.timers = None
+
+    # ------------------------------------------------------------------ #
+    def backbone(self, frames):
+        nhwc = self.channels_last
+        blob = ops.image_to_blob(frames, self.lut, self.Hp, self.Wp, nhwc=nhwc)
+        if nhwc:
+            blob = blob.permute(0, 3, 1, 2)  # NCHW view, channels_last memory
+        return self.model.Conv_Body(blob)  # [P6, P5, P4, P3, P2]
+
+    def nhwc_pyramid(self, feats):
+        """P2..P5 as B x H x W x C (a free view when the body ran channels_last)."""
+        out = []
+        for lvl in self.roi_levels:
+            t = feats[len(feats) - 1 - (lvl - self.rpn_levels[0])]
+            if t.is_contiguous(memory_format=torch.channels_last):
+                out.append(t.permute(0, 2, 3, 1))
+            else:
+                out.append(ops.nchw_to_nhwc(t))
+        return out
+
+    @torch.no_grad()
+    def run(self, frames: torch.Tensor):
+        """frames: F x H x W x 3 uint8 BGR on the device.  Returns a dict of device
+        tensors: dets [F,cap,5] (x1,y1,x2,y2,score), classes [F,cap], counts [F]
+        (host list too), masks [M,28,28] for the M = sum(counts) detections in
+        (frame, class, proposal) order."""
+        cfg = self.cfg
+        F = frames.shape[0]
+        feats = self.backbone(frames)
+        # RPN heads on P2..P6 (finest first for the proposal kernel)
+        probs, deltas = [], []
+        for lvl in self.rpn_levels:
+            t = feats[len(feats) - 1 - (lvl - self.rpn_levels[0])]
+            p, d = self.model.RPN.level_outputs(t)
+            probs.append(p.contiguous())
+            deltas.append(d.contiguous())
+        tst = cfg.TEST
+        lrois, lprobs, lcnt = ops.generate_proposals(
+            probs, deltas, self.anchors, self.rpn_scales, self.im_info[:F],
+            tst.RPN_PRE_NMS_TOP_N, tst.RPN_POST_NMS_TOP_N, tst.RPN_NMS_THRESH, tst.RPN_MIN_SIZE)
+        post = int(tst.RPN_POST_NMS_TOP_N * cfg.FPN.RPN_COLLECT_SCALE + 0.5)
+        rois, rlvl, rcnt = ops.collect_distribute(lrois, lprobs, lcnt, post,
+                                                  cfg.FPN.ROI_MIN_LEVEL, cfg.FPN.ROI_MAX_LEVEL)
+        pyr = self.nhwc_pyramid(feats)
+        fr = cfg.FAST_RCNN
+        box_feat = ops.roi_align_fpn(pyr, self.roi_scales, rois.view(-1, 5), rlvl.view(-1),
+                                     fr.ROI_XFORM_RESOLUTION, fr.ROI_XFORM_SAMPLING_RATIO)
+        x = self.model.Box_Head.mlp(box_feat)
+        cls_prob, bbox_pred = self.model.Box_Outs(x)
+        K = cls_prob.shape[1]
+        dets, dcls, dcnt = ops.box_detections(
+            rois, cls_prob.view(F, post, K), bbox_pred.view(F, post, 4 * K), rcnt,
+            self.im_scale_t[:F], self.im_hw[:F], tst.SCORE_THRESH, tst.NMS,
+            tst.DETECTIONS_PER_IM, cfg.MODEL.BBOX_REG_WEIGHTS, self.det_cap)
+        counts = dcnt.cpu().tolist()  # the one host read: sizes the mask batch
+        if max(counts) > self.det_cap:
+            raise RuntimeError("detections exceed det_cap=%d: %s" % (self.det_cap, counts))
+        out = {"dets": dets, "classes": dcls, "counts": dcnt, "counts_host": counts,
+               "rois": rois, "roi_counts": rcnt, "cls_prob": cls_prob, "bbox_pred": bbox_pred}
+        M = sum(counts)
+        R = cfg.MRCNN.RESOLUTION
+        if M == 0:
+            out["masks"] = torch.zeros((0, R, R), device=self.device)
+            return out
+        sel = torch.cat([torch.arange(c, device=self.device) + f * self.det_cap
+                         for f, c in enumerate(counts)])
+        flat = dets.view(-1, 5).index_select(0, sel)
+        bidx = torch.cat([torch.full((c,), f, dtype=torch.float32, device=self.device)
+                          for f, c in enumerate(counts)])
+        # _get_rois_blob (test.py:877-906): float64 product, float32 store
+        boxes = (flat[:, :4].double() * self.im_scale).float()
+        mrois = torch.cat([bidx[:, None], boxes], 1).contiguous()
+        mlvl = ops.map_rois_to_fpn_levels(mrois, cfg.FPN.ROI_MIN_LEVEL, cfg.FPN.ROI_MAX_LEVEL)
+        mlvl = (mlvl - cfg.FPN.ROI_MIN_LEVEL).contiguous()
+        mc = cfg.MRCNN
+        mfeat = ops.roi_align_fpn(pyr, self.roi_scales, mrois, mlvl, mc.ROI_XFORM_RESOLUTION,
+                                  mc.ROI_XFORM_SAMPLING_RATIO)
+        mh = self.model.Mask_Head.head(mfeat)
+        mcls = dcls.view(-1).index_select(0, sel)
+        out["masks"] = self.model.Mask_Outs.selected(mh, mcls)
+        out["mask_rois"] = mrois
+        out["mask_feat"] = mfeat
+        out["mask_head"] = mh
+        return out
