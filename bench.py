@@ -72,11 +72,33 @@ def roi_align_algorithmic_bytes(rois, lvls, sizes, C, P):
     return 4 * C * touched + 4 * len(rois) * C * P * P + 20 * len(rois)
 
 
-def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=50):
+def xcd_order(rois, lvls, n_xcd=8):
+    """Scheduling permutation for the RoIAlign launch: RoIs sorted by (frame, level,
+    y-band, x) and dealt so that XCD k (blocks b with b % 8 == k) walks the k-th
+    contiguous slice of that order -- spatial neighbours share an L2."""
+    band = np.floor((rois[:, 2] + rois[:, 4]) * 0.5 / 2.0 ** (lvls + 2) / 8).astype(np.int64)
+    cx = (rois[:, 1] + rois[:, 3]) * 0.5
+    srt = np.lexsort((cx, band, lvls, rois[:, 0]))
+    n = len(srt)
+    per = -(-n // n_xcd)
+    order = np.empty(n, np.int32)
+    b = np.arange(n)
+    slot = (b % n_xcd) * per + b // n_xcd
+    # blocks whose slot runs past n (last partial slice) take the leftovers in order
+    ok = slot < n
+    order[ok] = srt[slot[ok]]
+    rest = np.setdiff1d(np.arange(n), order[ok], assume_unique=False)
+    order[~ok] = srt[np.isin(srt, rest)]
+    return order
+
+
+def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=None,
+                              use_order=True):
     """RoIAlign (FPN NHWC, one launch over 4 levels x `frames` images) timed with HIP
     events on the launch stream; >= 8 distinct frames so the working set (>700 MB)
     exceeds the 256 MB Infinity Cache."""
     from vosdetectron_amd import ops
+    iters = iters or int(os.environ.get("RA_ITERS", "50"))
     sizes = [(200, 336), (100, 168), (50, 84), (25, 42)]
     scales = [1. / 4, 1. / 8, 1. / 16, 1. / 32]
     g = torch.Generator(device=dev).manual_seed(1)
@@ -88,23 +110,26 @@ def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=50)
         nbytes += roi_align_algorithmic_bytes(r, lv, sizes, C, P)
         rois.append(r)
         lvls.append(lv)
-    rois_t = torch.from_numpy(np.concatenate(rois)).to(dev)
-    lv_t = torch.from_numpy(np.concatenate(lvls)).to(dev)
+    rois_np, lv_np = np.concatenate(rois), np.concatenate(lvls)
+    rois_t = torch.from_numpy(rois_np).to(dev)
+    lv_t = torch.from_numpy(lv_np).to(dev)
+    order = ops.xcd_roi_order(rois_t, lv_t) if use_order else None
     out = torch.empty((frames * R, C, P, P), device=dev)
     s = torch.cuda.current_stream()
     for _ in range(3):
-        ops.roi_align_fpn(pyr, scales, rois_t, lv_t, P, sr, out=out)
+        ops.roi_align_fpn(pyr, scales, rois_t, lv_t, P, sr, out=out, roi_order=order)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(iters):
-        ops.roi_align_fpn(pyr, scales, rois_t, lv_t, P, sr, out=out)
+        ops.roi_align_fpn(pyr, scales, rois_t, lv_t, P, sr, out=out, roi_order=order)
     e1.record(s)
     e1.synchronize()
     t = e0.elapsed_time(e1) / 1e3 / iters
     achieved = nbytes / t / 1e9
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": "roi_align_fpn_nhwc_kernel<7>",
+            "kernel": "vd::roi_align_fpn_nhwc_kernel<7,2,2> (XCD-ordered)" if use_order
+                      else "vd::roi_align_fpn_nhwc_kernel<7,2,2>",
             "launch": "%d frames x %d RoIs, C=%d, P=%d, sr=%d" % (frames, R, C, P, sr),
             "algorithmic_bytes_per_launch": int(nbytes), "avg_launch_us": round(t * 1e6, 2)}
 

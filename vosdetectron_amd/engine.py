@@ -109,8 +109,10 @@ class FramePipeline:
                                                   cfg.FPN.ROI_MIN_LEVEL, cfg.FPN.ROI_MAX_LEVEL)
         pyr = self.nhwc_pyramid(feats)
         fr = cfg.FAST_RCNN
-        box_feat = ops.roi_align_fpn(pyr, self.roi_scales, rois.view(-1, 5), rlvl.view(-1),
-                                     fr.ROI_XFORM_RESOLUTION, fr.ROI_XFORM_SAMPLING_RATIO)
+        flat_rois, flat_lvl = rois.view(-1, 5), rlvl.view(-1)
+        box_feat = ops.roi_align_fpn(pyr, self.roi_scales, flat_rois, flat_lvl,
+                                     fr.ROI_XFORM_RESOLUTION, fr.ROI_XFORM_SAMPLING_RATIO,
+                                     roi_order=ops.xcd_roi_order(flat_rois, flat_lvl))
         x = self.model.Box_Head.mlp(box_feat)
         cls_prob, bbox_pred = self.model.Box_Outs(x)
         K = cls_prob.shape[1]

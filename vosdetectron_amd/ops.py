@@ -158,6 +158,38 @@ def roi_align_fpn(levels: Sequence[torch.Tensor], spatial_scales: Sequence[float
     return out
 
 
+_ORDER_CACHE = {}
+
+
+def xcd_roi_order(rois: torch.Tensor, roi_level: torch.Tensor, n_xcd: int = 8,
+                  band: int = 8) -> torch.Tensor:
+    """Scheduling permutation for roi_align_fpn (never changes results): RoIs
+    sorted by (image, level, y-band of 8 level pixels, x) and dealt so that the
+    blocks of one XCD (b % 8 equal) walk one contiguous slice of that order --
+    spatial neighbours, whose footprints overlap, run on the same L2."""
+    r = rois
+    lv = roi_level.to(torch.int64)
+    scale = torch.pow(2.0, -(lv + 2).to(torch.float32))
+    cy = (r[:, 2] + r[:, 4]) * 0.5 * scale
+    cx = (r[:, 1] + r[:, 3]) * 0.5 * scale
+    key = (((r[:, 0].to(torch.int64) * 8 + lv) * 4096 + (cy / band).to(torch.int64)) * 65536
+           + cx.clamp(0, 65535).to(torch.int64))
+    srt = torch.argsort(key)
+    n = r.shape[0]
+    perm = _ORDER_CACHE.get((n, n_xcd, r.device))
+    if perm is None:
+        per = -(-n // n_xcd)
+        b = np.arange(n)
+        slot = (b % n_xcd) * per + b // n_xcd
+        ok = slot < n
+        p = np.empty(n, np.int64)
+        p[ok] = slot[ok]
+        p[~ok] = np.setdiff1d(np.arange(n), slot[ok])
+        perm = torch.from_numpy(p).to(r.device)
+        _ORDER_CACHE[(n, n_xcd, r.device)] = perm
+    return srt[perm].to(torch.int32).contiguous()
+
+
 # --------------------------------------------------------------------------- #
 # lib/model ops: legacy RoIAlign, RoIPool, RoICrop                             #
 # --------------------------------------------------------------------------- #
