@@ -67,9 +67,11 @@ int vd_roi_align_backward(int aligned_height, int aligned_width, float spatial_s
  * levels[roi_level[r]] (roi_level == NULL -> level 0) and written to output
  * row r, i.e. already in the order the reference restores with
  * `_idx_restore_int32`.  layout: VD_LAYOUT_NHWC (B x H x W x C, the product
- * layout; C % 4 == 0) or VD_LAYOUT_NCHW.  roi_order (optional, NHWC with a
- * pooled size of 7, 14 or 28): a permutation that only changes the order in
- * which RoIs are scheduled (locality), never the output placement. */
+ * layout; C % 4 == 0) or VD_LAYOUT_NCHW.  roi_order (optional): a permutation
+ * that only changes the order in which RoIs are scheduled (L2 locality), never
+ * the output placement.  output_layout: VD_LAYOUT_NCHW -> num_rois x C x ah x aw
+ * (the reference's layout), VD_LAYOUT_NHWC -> num_rois x ah x aw x C (NHWC
+ * input, ah == aw in {7, 14}; what channels_last heads consume). */
 typedef struct {
     const float *data;
     int H;
@@ -80,7 +82,8 @@ typedef struct {
 int vd_roi_align_fpn_forward(const VdFeatLevel *levels, int num_levels, int B, int C, int layout,
                              const float *rois, const int32_t *roi_level,
                              const int32_t *roi_order, int num_rois, int aligned_height,
-                             int aligned_width, int sampling_ratio, float *output, void *stream);
+                             int aligned_width, int sampling_ratio, int output_layout,
+                             float *output, void *stream);
 
 /* jwyang RoIAlign (legacy, lib/model/roi_align).  Replaces
  * roi_align_forward_cuda(int aligned_height, int aligned_width, float

@@ -17,15 +17,16 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 
 
-@pytest.fixture(scope="module")
-def setup():
+@pytest.fixture(scope="module", params=["nchw", "nhwc"])
+def setup(request):
     from vosdetectron_amd import config as vcfg
     from vosdetectron_amd.engine import FramePipeline
     from vosdetectron_amd.weights import build_model
     cfg = vcfg.get("e2e_mask_rcnn_R-50-FPN_1x")
-    model, sd = build_model(cfg, device=DEV)
+    cl = request.param == "nhwc"
+    model, sd = build_model(cfg, device=DEV, channels_last=cl)
     frame = np.random.RandomState(1000).randint(0, 256, (800, 1333, 3), np.uint8)
-    pipe = FramePipeline(model, cfg, batch=1, device=DEV)
+    pipe = FramePipeline(model, cfg, batch=1, device=DEV, channels_last=cl)
     out = pipe.run(torch.from_numpy(frame[None]).to(DEV))
     return cfg, model, sd, pipe, frame, out
 

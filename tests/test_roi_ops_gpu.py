@@ -79,6 +79,11 @@ def test_roi_align_fpn_nhwc_bit_exact(P, sr, C):
     out = ops.roi_align_fpn(nhwc, scales, torch.from_numpy(rois).to(DEV),
                             torch.from_numpy(lv).to(DEV), P, sr).cpu().numpy()
     assert np.array_equal(out, ref)
+    # NHWC output layout (product path) holds the same numbers
+    if P in (7, 14):
+        o2 = ops.roi_align_fpn(nhwc, scales, torch.from_numpy(rois).to(DEV),
+                               torch.from_numpy(lv).to(DEV), P, sr, out_layout="nhwc")
+        assert np.array_equal(o2.permute(0, 3, 1, 2).cpu().numpy(), ref)
     # scheduling permutation must not move outputs
     perm = torch.from_numpy(rng.permutation(len(rois)).astype(np.int32)).to(DEV)
     if P in (7, 14):

@@ -52,7 +52,8 @@ int vd_roi_align_backward(int ah, int aw, float spatial_scale, int sampling_rati
 int vd_roi_align_fpn_forward(const VdFeatLevel *levels, int num_levels, int B, int C, int layout,
                              const float *rois, const int32_t *roi_level,
                              const int32_t *roi_order, int num_rois, int ah, int aw,
-                             int sampling_ratio, float *output, void *stream) {
+                             int sampling_ratio, int output_layout, float *output,
+                             void *stream) {
     if (num_rois == 0) return VD_OK;
     if (!levels || num_levels < 1 || num_levels > VD_MAX_LEVELS || !rois || !output || B < 1 ||
         C < 1 || ah < 1 || aw < 1 || num_rois < 0)
@@ -66,10 +67,12 @@ int vd_roi_align_fpn_forward(const VdFeatLevel *levels, int num_levels, int B, i
         fa.W[l] = levels[l].W;
         fa.scale[l] = levels[l].spatial_scale;
     }
+    if (output_layout != VD_LAYOUT_NCHW && output_layout != VD_LAYOUT_NHWC) return VD_ERR_ARG;
     if (layout == VD_LAYOUT_NHWC)
         return launch_roi_align_fpn_nhwc(fa, C, rois, roi_level, roi_order, num_rois, ah, aw,
-                                         sampling_ratio, output, VD_STREAM(stream));
-    if (layout != VD_LAYOUT_NCHW) return VD_ERR_ARG;
+                                         sampling_ratio, output_layout == VD_LAYOUT_NHWC, output,
+                                         VD_STREAM(stream));
+    if (layout != VD_LAYOUT_NCHW || output_layout != VD_LAYOUT_NCHW) return VD_ERR_ARG;
     if (num_levels != 1) return VD_ERR_SHAPE;  // multi-level NCHW: use per-level calls
     return launch_roi_align_fwd_nchw(fa.feat[0], B, C, fa.H[0], fa.W[0], rois, num_rois, ah, aw,
                                      fa.scale[0], sampling_ratio, output, VD_STREAM(stream));

@@ -285,7 +285,7 @@ __device__ __forceinline__ void nhwc_row_sr(const RoiGeom &g, int C, int ph, int
 template <int P, int SR, int D>
 __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_kernel(
     FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
-    const int *__restrict__ roi_order, int R, int sr, int rows_per_block,
+    const int *__restrict__ roi_order, int R, int sr, int rows_per_block, int out_nhwc,
     float *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float tile[];
     const int r = roi_order ? roi_order[blockIdx.x] : (int)blockIdx.x;
@@ -308,7 +308,15 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_kernel(
             nhwc_row_sr<P, (SR > 0 ? SR : 1), D>(g, C, row0 + prow, active ? c0 : 0, acc);
         else
             nhwc_row<P>(g, C, row0 + prow, active ? c0 : 0, active, acc);
-        if (active) {
+        if (active && out_nhwc) {  // [R][P][P][C]: one coalesced 1 KiB store per bin
+            float *o = out + (((int64_t)r * P + row0 + prow) * P) * C + c0;
+#pragma unroll
+            for (int pw = 0; pw < P; ++pw) {
+                const float4 a = acc[pw];
+                *reinterpret_cast<float4 *>(o + (int64_t)pw * C) =
+                    make_float4(a.x / g.count, a.y / g.count, a.z / g.count, a.w / g.count);
+            }
+        } else if (active) {
 #pragma unroll
             for (int pw = 0; pw < P; ++pw) {
                 float *t = tile + (int64_t)c0 * seg + prow * P + pw;
@@ -319,6 +327,7 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_kernel(
             }
         }
     }
+    if (out_nhwc) return;
     __syncthreads();
     float *o = out + (int64_t)r * C * P * P + row0 * P;
     if (rows == P) {  // whole RoI: one contiguous C*P*P block
@@ -668,27 +677,37 @@ static constexpr int kTileBudget = 64 * 1024;  // LDS bytes per workgroup (2-3 W
 
 template <int P, int SR, int D = 3>
 static int launch_rows(const FpnLevels &fa, int C, const float *rois, const int *lvl,
-                       const int *order, int R, int sr, float *out, hipStream_t s) {
+                       const int *order, int R, int sr, float *out, hipStream_t s,
+                       int out_nhwc = 0) {
     const int row_bytes = C * P * 4;
     int rows = kTileBudget / row_bytes;
     if (rows < 1) rows = 1;
-    if (rows > P) rows = P;
-    if ((int64_t)rows * row_bytes > 160 * 1024) return VD_ERR_SHAPE;
+    if (rows > P || out_nhwc) rows = P;
+    if (!out_nhwc && (int64_t)rows * row_bytes > 160 * 1024) return VD_ERR_SHAPE;
     const int chunks = (C + 255) / 256;
     int waves = rows * chunks;
     if (waves > 8) waves = 8;  // __launch_bounds__(512): <= 256 VGPRs, acc[P] stays in registers
-    const size_t lds = (size_t)rows * row_bytes;
+    const size_t lds = out_nhwc ? 0 : (size_t)rows * row_bytes;
     dim3 grid(R, (P + rows - 1) / rows);
-    hipLaunchKernelGGL((roi_align_fpn_nhwc_kernel<P, SR, D>), grid, dim3(64 * waves), lds, s, fa, C, rois,
-                       lvl, order, R, sr, rows, out);
+    hipLaunchKernelGGL((roi_align_fpn_nhwc_kernel<P, SR, D>), grid, dim3(64 * waves), lds, s, fa,
+                       C, rois, lvl, order, R, sr, rows, out_nhwc, out);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
 int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, const int *lvl,
-                              const int *order, int R, int PH, int PW, int sr, float *out,
-                              hipStream_t s) {
+                              const int *order, int R, int PH, int PW, int sr, int out_nhwc,
+                              float *out, hipStream_t s) {
     if (R == 0) return VD_OK;
     if (C % 4 != 0) return VD_ERR_SHAPE;
+    if (out_nhwc) {  // product path: [R][P][P][C] written straight from registers
+        if (PH == PW && PH == 7)
+            return sr == 2 ? launch_rows<7, 2, 2>(fa, C, rois, lvl, order, R, sr, out, s, 1)
+                           : launch_rows<7, 0>(fa, C, rois, lvl, order, R, sr, out, s, 1);
+        if (PH == PW && PH == 14)
+            return sr == 2 ? launch_rows<14, 2, 2>(fa, C, rois, lvl, order, R, sr, out, s, 1)
+                           : launch_rows<14, 0>(fa, C, rois, lvl, order, R, sr, out, s, 1);
+        return VD_ERR_SHAPE;
+    }
     static const int variant = [] {
         const char *e = getenv("VOSDET_ROIALIGN_VARIANT");
         return e ? atoi(e) : 3;  // 3: row kernel, SR=2 unrolled, 1 sample ahead (best measured)

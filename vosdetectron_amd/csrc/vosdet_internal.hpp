@@ -23,8 +23,8 @@ int launch_roi_align_bwd_nchw(const float *top_diff, int B, int C, int H, int W,
                               const float *rois, int R, int PH, int PW, float scale, int sr,
                               float *bottom_diff, hipStream_t s);
 int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, const int *lvl,
-                              const int *order, int R, int PH, int PW, int sr, float *out,
-                              hipStream_t s);
+                              const int *order, int R, int PH, int PW, int sr, int out_nhwc,
+                              float *out, hipStream_t s);
 
 int launch_roi_align_legacy_fwd(const float *feat, int B, int C, int H, int W, const float *rois,
                                 int R, int PH, int PW, float scale, float *out, hipStream_t s);

@@ -110,10 +110,12 @@ class FramePipeline:
         pyr = self.nhwc_pyramid(feats)
         fr = cfg.FAST_RCNN
         flat_rois, flat_lvl = rois.view(-1, 5), rlvl.view(-1)
+        fast = self.channels_last and hasattr(self.model.Box_Head, "fc1_nhwc_weight")
         box_feat = ops.roi_align_fpn(pyr, self.roi_scales, flat_rois, flat_lvl,
                                      fr.ROI_XFORM_RESOLUTION, fr.ROI_XFORM_SAMPLING_RATIO,
-                                     roi_order=ops.xcd_roi_order(flat_rois, flat_lvl))
-        x = self.model.Box_Head.mlp(box_feat)
+                                     roi_order=ops.xcd_roi_order(flat_rois, flat_lvl),
+                                     out_layout="nhwc" if fast else "nchw")
+        x = self.model.Box_Head.mlp_nhwc(box_feat) if fast else self.model.Box_Head.mlp(box_feat)
         cls_prob, bbox_pred = self.model.Box_Outs(x)
         K = cls_prob.shape[1]
         dets, dcls, dcnt = ops.box_detections(
@@ -130,6 +132,10 @@ class FramePipeline:
         if M == 0:
             out["masks"] = torch.zeros((0, R, R), device=self.device)
             return out
+        # pad the mask batch to a multiple of 64 rows: a handful of stable shapes
+        # for the convolution algorithm search (padding rows are zero RoIs whose
+        # outputs are dropped)
+        Mp = -(-M // 64) * 64
         sel = torch.cat([torch.arange(c, device=self.device) + f * self.det_cap
                          for f, c in enumerate(counts)])
         flat = dets.view(-1, 5).index_select(0, sel)
@@ -141,12 +147,23 @@ class FramePipeline:
         mlvl = ops.map_rois_to_fpn_levels(mrois, cfg.FPN.ROI_MIN_LEVEL, cfg.FPN.ROI_MAX_LEVEL)
         mlvl = (mlvl - cfg.FPN.ROI_MIN_LEVEL).contiguous()
         mc = cfg.MRCNN
+        mcls = dcls.view(-1).index_select(0, sel)
+        out["mask_rois"] = mrois
+        if fast and hasattr(self.model.Mask_Head, "up_w"):
+            if Mp > M:
+                mrois = torch.cat([mrois, mrois.new_zeros((Mp - M, 5))])
+                mlvl = torch.cat([mlvl, mlvl.new_zeros((Mp - M,))])
+                mcls = torch.cat([mcls, mcls.new_ones((Mp - M,))])
+            mfeat = ops.roi_align_fpn(pyr, self.roi_scales, mrois, mlvl,
+                                      mc.ROI_XFORM_RESOLUTION, mc.ROI_XFORM_SAMPLING_RATIO,
+                                      out_layout="nhwc")
+            up = self.model.Mask_Head.head_nhwc(mfeat)
+            out["masks"] = self.model.Mask_Outs.selected_from_up(up, mcls)[:M]
+            out["mask_feat"] = mfeat[:M].permute(0, 3, 1, 2)
+            return out
         mfeat = ops.roi_align_fpn(pyr, self.roi_scales, mrois, mlvl, mc.ROI_XFORM_RESOLUTION,
                                   mc.ROI_XFORM_SAMPLING_RATIO)
         mh = self.model.Mask_Head.head(mfeat)
-        mcls = dcls.view(-1).index_select(0, sel)
         out["masks"] = self.model.Mask_Outs.selected(mh, mcls)
-        out["mask_rois"] = mrois
         out["mask_feat"] = mfeat
-        out["mask_head"] = mh
         return out

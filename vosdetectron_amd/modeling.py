@@ -209,6 +209,21 @@ class Roi2MLPHead(nn.Module):
         x = F.relu(self.fc1(x.view(x.size(0), -1)), inplace=True)
         return F.relu(self.fc2(x), inplace=True)
 
+    def mlp_nhwc(self, x):
+        """fc6/fc7 on R x P x P x C RoI features: fc6's weight columns are permuted
+        once (prepare) from the reference's (c, ph, pw) flattening to (ph, pw, c)."""
+        x = F.relu(F.linear(x.reshape(x.size(0), -1), self.fc1_nhwc_weight, self.fc1.bias),
+                   inplace=True)
+        return F.relu(self.fc2(x), inplace=True)
+
+    @torch.no_grad()
+    def prepare(self):
+        res = self.cfg.FAST_RCNN.ROI_XFORM_RESOLUTION
+        w = self.fc1.weight
+        C = w.shape[1] // (res * res)
+        self.fc1_nhwc_weight = (w.view(w.shape[0], C, res, res).permute(0, 2, 3, 1)
+                                .reshape(w.shape[0], -1).contiguous())
+
     def forward(self, x, rpn_ret):
         c = self.cfg.FAST_RCNN
         x = self.roi_xform(x, rpn_ret, blob_rois="rois", method=c.ROI_XFORM_METHOD,
@@ -250,6 +265,24 @@ class MaskHeadV1upXconvs(nn.Module):
     def head(self, x):
         return F.relu(self.upconv(self.conv_fcn(x)), inplace=True)
 
+    @torch.no_grad()
+    def prepare(self):
+        """ConvTranspose2d(k=2, s=2) has no overlapping taps, so it is one GEMM
+        [M*H*W, Cin] x [Cin, 2*2*Cout] followed by a depth-to-space shuffle."""
+        w = self.upconv.weight  # Cin x Cout x 2 x 2
+        self.up_w = w.permute(0, 2, 3, 1).reshape(w.shape[0], -1).contiguous()  # Cin x (i,j,co)
+        self.up_b = self.upconv.bias.repeat(4).contiguous()
+
+    def head_nhwc(self, x_nhwc):
+        """x_nhwc: M x P x P x C RoI features.  Returns M x P x P x 2 x 2 x C
+        (relu'd upconv output; (h, w, i, j) -> pixel (2h+i, 2w+j))."""
+        M, P, _, C = x_nhwc.shape
+        x = x_nhwc.permute(0, 3, 1, 2)  # NCHW view with channels_last strides
+        x = self.conv_fcn(x)
+        x = x.permute(0, 2, 3, 1).reshape(M * P * P, -1)
+        y = torch.addmm(self.up_b, x, self.up_w)
+        return F.relu_(y).view(M, P, P, 2, 2, -1)
+
     def forward(self, x, rpn_ret):
         c = self.cfg.MRCNN
         x = self.roi_xform(x, rpn_ret, blob_rois="mask_rois", method=c.ROI_XFORM_METHOD,
@@ -276,6 +309,15 @@ class MaskRCNNOutputs(nn.Module):
         w = self.classify.weight[cls_idx.long(), :, 0, 0]  # M x D
         b = self.classify.bias[cls_idx.long()]
         y = torch.einsum("mdhw,md->mhw", x, w) + b.view(-1, 1, 1)
+        return torch.sigmoid(y)
+
+    def selected_from_up(self, up, cls_idx):
+        """up: M x P x P x 2 x 2 x D (MaskHead.head_nhwc) -> M x 2P x 2P masks."""
+        M, P = up.shape[0], up.shape[1]
+        w = self.classify.weight[cls_idx.long(), :, 0, 0]  # M x D
+        b = self.classify.bias[cls_idx.long()]
+        y = torch.bmm(up.view(M, P * P * 4, -1), w.unsqueeze(2)).view(M, P, P, 2, 2)
+        y = y.permute(0, 1, 3, 2, 4).reshape(M, 2 * P, 2 * P) + b.view(-1, 1, 1)
         return torch.sigmoid(y)
 
 
@@ -362,6 +404,8 @@ class Generalized_RCNN(nn.Module):
                     blk.fd = _fold(blk.downsample[0], blk.downsample[1])
                 blk.fused = True
         self.RPN.fuse()
+        self.Box_Head.prepare()
+        self.Mask_Head.prepare()
         return self
 
 

@@ -124,11 +124,12 @@ def roi_align_fpn(levels: Sequence[torch.Tensor], spatial_scales: Sequence[float
                   rois: torch.Tensor, roi_level: Optional[torch.Tensor], resolution: int,
                   sampling_ratio: int, layout: str = "nhwc",
                   roi_order: Optional[torch.Tensor] = None,
-                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  out: Optional[torch.Tensor] = None, out_layout: str = "nchw") -> torch.Tensor:
     """One-launch multi-level RoIAlign (replaces the per-level loop + cat + restore
     of model_builder.py:252-303).  levels: finest first, each B x H x W x C
     (layout 'nhwc') or B x C x H x W ('nchw', single level only).  roi_level[r]
-    is the index into ``levels``.  Output row r belongs to rois[r]."""
+    is the index into ``levels``.  Output row r belongs to rois[r]; out_layout
+    'nchw' -> R x C x P x P (the reference's), 'nhwc' -> R x P x P x C."""
     if len(levels) < 1 or len(levels) > _lib.VD_MAX_LEVELS:
         raise ValueError("1..%d levels" % _lib.VD_MAX_LEVELS)
     r = _need(rois, "rois")
@@ -144,8 +145,10 @@ def roi_align_fpn(levels: Sequence[torch.Tensor], spatial_scales: Sequence[float
             B, C, H, W = t.shape
         descs[i] = _lib.VdFeatLevel(t.data_ptr(), H, W, float(sc))
     R = r.shape[0]
+    onhwc = out_layout == "nhwc"
     if out is None:
-        out = torch.empty((R, C, resolution, resolution), dtype=torch.float32, device=r.device)
+        shape = (R, resolution, resolution, C) if onhwc else (R, C, resolution, resolution)
+        out = torch.empty(shape, dtype=torch.float32, device=r.device)
     if R == 0:
         return out
     lv = _need(roi_level, "roi_level", torch.int32) if roi_level is not None else None
@@ -154,7 +157,8 @@ def roi_align_fpn(levels: Sequence[torch.Tensor], spatial_scales: Sequence[float
         descs, len(levels), B, C, _lib.VD_LAYOUT_NHWC if nhwc else _lib.VD_LAYOUT_NCHW,
         r.data_ptr(), lv.data_ptr() if lv is not None else None,
         od.data_ptr() if od is not None else None, R, resolution, resolution,
-        int(sampling_ratio), out.data_ptr(), _stream()), "vd_roi_align_fpn_forward")
+        int(sampling_ratio), _lib.VD_LAYOUT_NHWC if onhwc else _lib.VD_LAYOUT_NCHW,
+        out.data_ptr(), _stream()), "vd_roi_align_fpn_forward")
     return out
 
 

@@ -123,4 +123,5 @@ def build_model(cfg, seed: int = 0, device="cuda", fold=True, channels_last=Fals
     if channels_last:
         m.Conv_Body.to(memory_format=torch.channels_last)
         m.RPN.to(memory_format=torch.channels_last)
+        m.Mask_Head.conv_fcn.to(memory_format=torch.channels_last)
     return m, sd
