@@ -204,6 +204,17 @@ int vd_box_detections(const float *rois, const float *cls_prob, const float *bbo
 int vd_image_to_blob(const uint8_t *frames, int F, int H, int W, const float *lut, int Hp,
                      int Wp, int nhwc, float *blob, void *stream);
 
+/* Convolution epilogue, in place on x (N x C x H x W logical, physical NHWC when
+ * nhwc = 1):  x = act((x + bias[c]) + r),  r = 0 (residual_mode 0), residual
+ * (+ residual_bias[c]) of the same shape (mode 1), or residual nearest-2x
+ * upsampled from (H/2, W/2) (+ residual_bias[c]) (mode 2: the FPN top-down add,
+ * lib/modeling/FPN.py:293-299).  act = ReLU if relu.  One pass instead of the
+ * bias / residual / ReLU passes after a bias-free convolution (the frozen
+ * AffineChannel2d of ResNet.py:276-294 folded into conv weight + bias).
+ * bias / residual_bias may be NULL; N*C*H*W % 4 == 0. */
+int vd_bias_act(float *x, const float *bias, const float *residual, const float *residual_bias,
+                int N, int C, int H, int W, int nhwc, int residual_mode, int relu, void *stream);
+
 /* B x C x H x W -> B x H x W x C (pyramid relayout for the NHWC RoIAlign). */
 int vd_nchw_to_nhwc(const float *in, int B, int C, int H, int W, float *out, void *stream);
 

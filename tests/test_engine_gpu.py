@@ -27,7 +27,7 @@ def setup(request):
     model, sd = build_model(cfg, device=DEV, channels_last=cl)
     frame = np.random.RandomState(1000).randint(0, 256, (800, 1333, 3), np.uint8)
     pipe = FramePipeline(model, cfg, batch=1, device=DEV, channels_last=cl)
-    out = pipe.run(torch.from_numpy(frame[None]).to(DEV))
+    out = pipe.run(torch.from_numpy(frame[None]).to(DEV), keep_intermediates=True)
     return cfg, model, sd, pipe, frame, out
 
 
@@ -38,16 +38,16 @@ def test_stagewise_parity(setup):
     from vosdetectron_amd import ops
     blob = ops.image_to_blob(torch.from_numpy(frame[None]).to(DEV), pipe.lut, pipe.Hp, pipe.Wp)
     assert np.array_equal(blob.cpu().numpy(), blob_ref)
-    # rerun the body + RPN to get the exact tensors the engine consumed
-    with torch.no_grad():
-        feats = pipe.backbone(torch.from_numpy(frame[None]).to(DEV))
-        rl, pl = [], []
-        for i, lvl in enumerate(range(2, 7)):
-            p, d = model.RPN.level_outputs(feats[6 - lvl])
-            r, pr = orc.generate_proposals(orc.fpn_level_anchors(lvl), 1. / 2 ** lvl,
-                                           p.cpu().numpy(), d.cpu().numpy(), im_info)
-            rl.append(r)
-            pl.append(pr)
+    # the exact tensors the engine consumed (convolution algorithms may differ
+    # between two calls, so a rerun would not be bit-identical)
+    feats = out["feats"]
+    rl, pl = [], []
+    for i, lvl in enumerate(range(2, 7)):
+        p, d = out["rpn_probs"][i], out["rpn_deltas"][i]
+        r, pr = orc.generate_proposals(orc.fpn_level_anchors(lvl), 1. / 2 ** lvl,
+                                       p.cpu().numpy(), d.cpu().numpy(), im_info)
+        rl.append(r)
+        pl.append(pr)
     rois = orc.collect(rl, pl, 1000)
     n = int(out["roi_counts"][0].item())
     assert n == len(rois)
@@ -56,7 +56,7 @@ def test_stagewise_parity(setup):
     rpn_ret = orc.distribute(rois)
     blobs = [f.cpu().numpy() for f in feats[1:]]
     bf_ref = orc.roi_feature_transform(blobs, rpn_ret, "rois", 7, [1. / 32, 1. / 16, 1. / 8, 1. / 4], 2)
-    pyr = pipe.nhwc_pyramid(feats)
+    pyr = out["pyramid"]
     lv = orc.map_rois_to_fpn_levels(rois[:, 1:5], 2, 5).astype(np.int32) - 2
     bf = ops.roi_align_fpn(pyr, pipe.roi_scales, torch.from_numpy(rois).to(DEV),
                            torch.from_numpy(lv).to(DEV), 7, 2)

@@ -58,6 +58,7 @@ SIGNATURES = {
                                _P, _P, _S, _P]),
     "vd_image_to_blob": (_I, [_P, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
     "vd_nchw_to_nhwc": (_I, [_P, _I, _I, _I, _I, _P, _P]),
+    "vd_bias_act": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
 }
 
 

@@ -191,6 +191,15 @@ int vd_image_to_blob(const uint8_t *frames, int F, int H, int W, const float *lu
     return launch_image_to_blob(frames, F, H, W, lut, Hp, Wp, nhwc, blob, VD_STREAM(stream));
 }
 
+int vd_bias_act(float *x, const float *bias, const float *residual, const float *residual_bias,
+                int N, int C, int H, int W, int nhwc, int residual_mode, int relu, void *stream) {
+    if (!x || N < 1 || C < 1 || H < 1 || W < 1 || residual_mode < 0 || residual_mode > 2 ||
+        (residual_mode && !residual))
+        return VD_ERR_ARG;
+    return launch_bias_act(x, bias, residual, residual_bias, (int64_t)N * C * H * W, C, H, W,
+                           nhwc, residual_mode, relu, VD_STREAM(stream));
+}
+
 int vd_nchw_to_nhwc(const float *in, int B, int C, int H, int W, float *out, void *stream) {
     if (!in || !out) return VD_ERR_ARG;
     return launch_nchw_to_nhwc(in, B, C, H, W, out, VD_STREAM(stream));

@@ -252,4 +252,74 @@ int launch_nchw_to_nhwc(const float *in, int B, int C, int H, int W, float *out,
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
+// ---------------------------------------------------------------- conv epilogue
+// out = act((x + bias[c]) + res_term), in place on x, where res_term is
+//   mode 0: 0, mode 1: z (+ bias2[c]), mode 2: z nearest-2x-upsampled (+ bias2[c]).
+// One read of x (and z), one write: replaces the bias-add, residual-add and
+// ReLU passes PyTorch runs after each MIOpen convolution (each a full HBM
+// round trip of the activation).  Same association order as the unfused
+// module code ((conv + bias) + residual), so results are bit-identical to it.
+template <bool NHWC>
+__global__ __launch_bounds__(256) void bias_act_kernel(float *__restrict__ x,
+                                                       const float *__restrict__ bias,
+                                                       const float *__restrict__ z,
+                                                       const float *__restrict__ bias2,
+                                                       int64_t n4, int C, int H, int W,
+                                                       int mode, int relu) {
+    for (int64_t i4 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i4 < n4;
+         i4 += (int64_t)blockDim.x * gridDim.x) {
+        float4 v = reinterpret_cast<float4 *>(x)[i4];
+        float r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = i4 * 4 + k;
+            int c;
+            int64_t zi = i;
+            if (NHWC) {
+                c = (int)(i % C);
+                if (mode == 2) {  // i = ((n*H + h)*W + w)*C + c
+                    const int64_t pix = i / C;
+                    const int w = (int)(pix % W);
+                    const int64_t nh = pix / W;
+                    const int h = (int)(nh % H);
+                    const int64_t nn = nh / H;
+                    zi = ((nn * (H / 2) + h / 2) * (W / 2) + w / 2) * C + c;
+                }
+            } else {
+                const int64_t hw = (int64_t)H * W;
+                c = (int)((i / hw) % C);
+                if (mode == 2) {  // i = ((n*C + c)*H + h)*W + w
+                    const int w = (int)(i % W);
+                    const int h = (int)((i / W) % H);
+                    const int64_t nc = i / hw;
+                    zi = (nc * (H / 2) + h / 2) * (W / 2) + w / 2;
+                }
+            }
+            float y = r[k] + (bias ? bias[c] : 0.f);
+            if (mode) {
+                float t = z[zi];
+                if (bias2) t = t + bias2[c];
+                y = y + t;
+            }
+            if (relu) y = fmaxf(y, 0.f);
+            r[k] = y;
+        }
+        reinterpret_cast<float4 *>(x)[i4] = make_float4(r[0], r[1], r[2], r[3]);
+    }
+}
+
+int launch_bias_act(float *x, const float *bias, const float *z, const float *bias2, int64_t n,
+                    int C, int H, int W, int nhwc, int mode, int relu, hipStream_t s) {
+    if (n == 0) return VD_OK;
+    if (n % 4 != 0 || (mode == 2 && ((H & 1) || (W & 1)))) return VD_ERR_SHAPE;
+    const int64_t n4 = n / 4;
+    if (nhwc)
+        hipLaunchKernelGGL(bias_act_kernel<true>, dim3(blocks_for(n4, 256)), dim3(256), 0, s, x,
+                           bias, z, bias2, n4, C, H, W, mode, relu);
+    else
+        hipLaunchKernelGGL(bias_act_kernel<false>, dim3(blocks_for(n4, 256)), dim3(256), 0, s, x,
+                           bias, z, bias2, n4, C, H, W, mode, relu);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
 }  // namespace vd

@@ -85,7 +85,7 @@ class FramePipeline:
         return out
 
     @torch.no_grad()
-    def run(self, frames: torch.Tensor):
+    def run(self, frames: torch.Tensor, keep_intermediates: bool = False):
         """frames: F x H x W x 3 uint8 BGR on the device.  Returns a dict of device
         tensors: dets [F,cap,5] (x1,y1,x2,y2,score), classes [F,cap], counts [F]
         (host list too), masks [M,28,28] for the M = sum(counts) detections in
@@ -127,6 +127,8 @@ class FramePipeline:
             raise RuntimeError("detections exceed det_cap=%d: %s" % (self.det_cap, counts))
         out = {"dets": dets, "classes": dcls, "counts": dcnt, "counts_host": counts,
                "rois": rois, "roi_counts": rcnt, "cls_prob": cls_prob, "bbox_pred": bbox_pred}
+        if keep_intermediates:  # for stage-wise parity tests
+            out.update(feats=feats, rpn_probs=probs, rpn_deltas=deltas, pyramid=pyr)
         M = sum(counts)
         R = cfg.MRCNN.RESOLUTION
         if M == 0:

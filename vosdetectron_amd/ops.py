@@ -314,6 +314,32 @@ def nchw_to_nhwc(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.T
     return out
 
 
+def bias_act_(x: torch.Tensor, bias: Optional[torch.Tensor], residual=None, residual_bias=None,
+              relu: bool = True, upsample_residual: bool = False) -> torch.Tensor:
+    """In-place conv epilogue x = act((x + bias) + residual[+residual_bias]) (vd_bias_act).
+    x: N x C x H x W, contiguous or channels_last; residual in the same memory format."""
+    N, C, H, W = x.shape
+    if x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous():
+        nhwc = 1
+    elif x.is_contiguous():
+        nhwc = 0
+    else:
+        raise ValueError("x must be contiguous (NCHW or channels_last)")
+    if not x.is_cuda or x.dtype != torch.float32:
+        raise ValueError("x must be a float32 device tensor")
+    mode = 0
+    if residual is not None:
+        mode = 2 if upsample_residual else 1
+        want = torch.channels_last if nhwc else torch.contiguous_format
+        if not residual.is_contiguous(memory_format=want):
+            residual = residual.contiguous(memory_format=want)
+    check(lib().vd_bias_act(x.data_ptr(), bias.data_ptr() if bias is not None else None,
+                            residual.data_ptr() if residual is not None else None,
+                            residual_bias.data_ptr() if residual_bias is not None else None,
+                            N, C, H, W, nhwc, mode, int(relu), _stream()), "vd_bias_act")
+    return x
+
+
 def pixel_lut(pixel_means=(102.9801, 115.9465, 122.7717)) -> np.ndarray:
     """float32(u - mean_c) for u in 0..255 exactly as numpy computes
     ``im.astype(float32); im -= PIXEL_MEANS`` (float64 subtraction, float32 store,
