@@ -211,7 +211,7 @@ int vd_image_to_blob(const uint8_t *frames, int F, int H, int W, const float *lu
  * lib/modeling/FPN.py:293-299).  act = ReLU if relu.  One pass instead of the
  * bias / residual / ReLU passes after a bias-free convolution (the frozen
  * AffineChannel2d of ResNet.py:276-294 folded into conv weight + bias).
- * bias / residual_bias may be NULL; N*C*H*W % 4 == 0. */
+ * bias / residual_bias may be NULL; N*C*H*W < 2^31. */
 int vd_bias_act(float *x, const float *bias, const float *residual, const float *residual_bias,
                 int N, int C, int H, int W, int nhwc, int residual_mode, int relu, void *stream);
 

@@ -259,66 +259,91 @@ int launch_nchw_to_nhwc(const float *in, int B, int C, int H, int W, float *out,
 // ReLU passes PyTorch runs after each MIOpen convolution (each a full HBM
 // round trip of the activation).  Same association order as the unfused
 // module code ((conv + bias) + residual), so results are bit-identical to it.
-template <bool NHWC>
-__global__ __launch_bounds__(256) void bias_act_kernel(float *__restrict__ x,
-                                                       const float *__restrict__ bias,
-                                                       const float *__restrict__ z,
-                                                       const float *__restrict__ bias2,
-                                                       int64_t n4, int C, int H, int W,
-                                                       int mode, int relu) {
-    for (int64_t i4 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i4 < n4;
-         i4 += (int64_t)blockDim.x * gridDim.x) {
+// NHWC, C % 4 == 0: one float4 = 4 consecutive channels of one pixel.
+__global__ __launch_bounds__(256) void bias_act_nhwc4_kernel(
+    float *__restrict__ x, const float *__restrict__ bias, const float *__restrict__ z,
+    const float *__restrict__ bias2, uint32_t n4, uint32_t C4, uint32_t H, uint32_t W, int mode,
+    int relu) {
+    for (uint32_t i4 = blockIdx.x * blockDim.x + threadIdx.x; i4 < n4;
+         i4 += blockDim.x * gridDim.x) {
+        const uint32_t c4 = i4 % C4;
         float4 v = reinterpret_cast<float4 *>(x)[i4];
-        float r[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int64_t i = i4 * 4 + k;
-            int c;
-            int64_t zi = i;
-            if (NHWC) {
-                c = (int)(i % C);
-                if (mode == 2) {  // i = ((n*H + h)*W + w)*C + c
-                    const int64_t pix = i / C;
-                    const int w = (int)(pix % W);
-                    const int64_t nh = pix / W;
-                    const int h = (int)(nh % H);
-                    const int64_t nn = nh / H;
-                    zi = ((nn * (H / 2) + h / 2) * (W / 2) + w / 2) * C + c;
-                }
-            } else {
-                const int64_t hw = (int64_t)H * W;
-                c = (int)((i / hw) % C);
-                if (mode == 2) {  // i = ((n*C + c)*H + h)*W + w
-                    const int w = (int)(i % W);
-                    const int h = (int)((i / W) % H);
-                    const int64_t nc = i / hw;
-                    zi = (nc * (H / 2) + h / 2) * (W / 2) + w / 2;
-                }
-            }
-            float y = r[k] + (bias ? bias[c] : 0.f);
-            if (mode) {
-                float t = z[zi];
-                if (bias2) t = t + bias2[c];
-                y = y + t;
-            }
-            if (relu) y = fmaxf(y, 0.f);
-            r[k] = y;
+        if (bias) {
+            const float4 bb = reinterpret_cast<const float4 *>(bias)[c4];
+            v.x = v.x + bb.x; v.y = v.y + bb.y; v.z = v.z + bb.z; v.w = v.w + bb.w;
         }
-        reinterpret_cast<float4 *>(x)[i4] = make_float4(r[0], r[1], r[2], r[3]);
+        if (mode) {
+            uint32_t zi = i4;
+            if (mode == 2) {  // i4 = ((n*H + h)*W + w)*C4 + c4
+                const uint32_t pix = i4 / C4;
+                const uint32_t w = pix % W, nh = pix / W;
+                const uint32_t h = nh % H, nn = nh / H;
+                zi = ((nn * (H / 2) + h / 2) * (W / 2) + w / 2) * C4 + c4;
+            }
+            float4 t = reinterpret_cast<const float4 *>(z)[zi];
+            if (bias2) {
+                const float4 bb = reinterpret_cast<const float4 *>(bias2)[c4];
+                t.x = t.x + bb.x; t.y = t.y + bb.y; t.z = t.z + bb.z; t.w = t.w + bb.w;
+            }
+            v.x = v.x + t.x; v.y = v.y + t.y; v.z = v.z + t.z; v.w = v.w + t.w;
+        }
+        if (relu) {
+            v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f);
+            v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+        reinterpret_cast<float4 *>(x)[i4] = v;
+    }
+}
+
+// Any layout / C: one element per thread.
+__global__ __launch_bounds__(256) void bias_act_scalar_kernel(
+    float *__restrict__ x, const float *__restrict__ bias, const float *__restrict__ z,
+    const float *__restrict__ bias2, uint32_t n, uint32_t C, uint32_t H, uint32_t W, int nhwc,
+    int mode, int relu) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += blockDim.x * gridDim.x) {
+        uint32_t c, w, h, nn;
+        if (nhwc) {  // i = ((n*H + h)*W + w)*C + c
+            c = i % C;
+            const uint32_t pix = i / C;
+            w = pix % W;
+            h = (pix / W) % H;
+            nn = pix / W / H;
+        } else {  // i = ((n*C + c)*H + h)*W + w
+            w = i % W;
+            h = (i / W) % H;
+            c = (i / W / H) % C;
+            nn = i / W / H / C;
+        }
+        float y = x[i];
+        if (bias) y = y + bias[c];
+        if (mode) {
+            uint32_t zi = i;
+            if (mode == 2)
+                zi = nhwc ? ((nn * (H / 2) + h / 2) * (W / 2) + w / 2) * C + c
+                          : ((nn * C + c) * (H / 2) + h / 2) * (W / 2) + w / 2;
+            float t = z[zi];
+            if (bias2) t = t + bias2[c];
+            y = y + t;
+        }
+        if (relu) y = fmaxf(y, 0.f);
+        x[i] = y;
     }
 }
 
 int launch_bias_act(float *x, const float *bias, const float *z, const float *bias2, int64_t n,
                     int C, int H, int W, int nhwc, int mode, int relu, hipStream_t s) {
     if (n == 0) return VD_OK;
-    if (n % 4 != 0 || (mode == 2 && ((H & 1) || (W & 1)))) return VD_ERR_SHAPE;
-    const int64_t n4 = n / 4;
-    if (nhwc)
-        hipLaunchKernelGGL(bias_act_kernel<true>, dim3(blocks_for(n4, 256)), dim3(256), 0, s, x,
-                           bias, z, bias2, n4, C, H, W, mode, relu);
-    else
-        hipLaunchKernelGGL(bias_act_kernel<false>, dim3(blocks_for(n4, 256)), dim3(256), 0, s, x,
-                           bias, z, bias2, n4, C, H, W, mode, relu);
+    if (n >= (int64_t)1 << 31 || (mode == 2 && ((H & 1) || (W & 1)))) return VD_ERR_SHAPE;
+    if (nhwc && C % 4 == 0) {
+        const int64_t n4 = n / 4;
+        hipLaunchKernelGGL(bias_act_nhwc4_kernel, dim3(blocks_for(n4, 256)), dim3(256), 0, s, x,
+                           bias, z, bias2, (uint32_t)n4, (uint32_t)(C / 4), (uint32_t)H,
+                           (uint32_t)W, mode, relu);
+    } else {
+        hipLaunchKernelGGL(bias_act_scalar_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, x,
+                           bias, z, bias2, (uint32_t)n, (uint32_t)C, (uint32_t)H, (uint32_t)W,
+                           nhwc, mode, relu);
+    }
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 

@@ -41,6 +41,19 @@ class AffineChannel2d(nn.Module):
         return x * self.weight.view(1, -1, 1, 1) + self.bias.view(1, -1, 1, 1)
 
 
+def _conv_nb(conv: nn.Conv2d, x):
+    """The convolution of `conv` without its bias (added by the fused epilogue)."""
+    return F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+
+
+def _conv_epi(conv: nn.Conv2d, x, relu=True, res=None, res_bias=None, up=False):
+    """conv -> one vd_bias_act pass: act((conv(x) + b) + (res [+ res_bias])).  Same
+    association order as the module code it replaces (bias kernel after the MIOpen
+    conv, then the residual add, then ReLU), so the results are bit-identical."""
+    return ops.bias_act_(_conv_nb(conv, x), conv.bias, res, res_bias, relu=relu,
+                         upsample_residual=up)
+
+
 def _stage_counts(conv_body: str):
     return {"FPN.fpn_ResNet50_conv5_body": (3, 4, 6, 3),
             "FPN.fpn_ResNet101_conv5_body": (3, 4, 23, 3),
@@ -64,8 +77,15 @@ class Bottleneck(nn.Module):
             self.downsample = nn.Sequential(nn.Conv2d(inplanes, outplanes, 1, stride, bias=False),
                                             AffineChannel2d(outplanes))
         self.fused = False
+        self.epilogue = False
 
     def forward(self, x):
+        if self.fused and self.epilogue and x.is_cuda:
+            out = _conv_epi(self.f1, x)
+            out = _conv_epi(self.f2, out)
+            if self.downsample is not None:
+                return _conv_epi(self.f3, out, res=_conv_nb(self.fd, x), res_bias=self.fd.bias)
+            return _conv_epi(self.f3, out, res=x)
         if self.fused:
             out = F.relu(self.f1(x), inplace=True)
             out = F.relu(self.f2(out), inplace=True)
@@ -88,6 +108,19 @@ def _fold(conv: nn.Conv2d, aff: AffineChannel2d) -> nn.Conv2d:
     f.weight.requires_grad_(False)
     f.bias.requires_grad_(False)
     return f
+
+
+class _StemEpilogue(nn.Module):
+    """Folded stem: conv1 (+ bias + ReLU in one epilogue pass) + max-pool."""
+
+    def __init__(self, conv1, maxpool):
+        super().__init__()
+        self.conv1, self.maxpool = conv1, maxpool
+
+    def forward(self, x):
+        if x.is_cuda:
+            return self.maxpool(_conv_epi(self.conv1, x))
+        return self.maxpool(F.relu(self.conv1(x), inplace=True))
 
 
 class ResNetBody(nn.Module):
@@ -128,8 +161,11 @@ class TopdownLateral(nn.Module):
     def __init__(self, dim_top, dim_lateral):
         super().__init__()
         self.conv_lateral = nn.Conv2d(dim_lateral, dim_top, 1, 1, 0)
+        self.epilogue = False
 
     def forward(self, top, lateral):
+        if self.epilogue and lateral.is_cuda:
+            return _conv_epi(self.conv_lateral, lateral, relu=False, res=top, up=True)
         return self.conv_lateral(lateral) + F.interpolate(top, scale_factor=2, mode="nearest")
 
 
@@ -183,7 +219,10 @@ class FPNRPNOutputs(nn.Module):
 
     def level_outputs(self, x):
         """(sigmoid cls probs N x A x H x W, bbox deltas N x 4A x H x W)."""
-        h = F.relu(self.FPN_RPN_conv(x), inplace=True)
+        if self.fused is not None and x.is_cuda:
+            h = _conv_epi(self.FPN_RPN_conv, x)
+        else:
+            h = F.relu(self.FPN_RPN_conv(x), inplace=True)
         A = self.num_anchors
         if self.fused is not None:
             o = self.fused(h)
@@ -278,7 +317,9 @@ class MaskHeadV1upXconvs(nn.Module):
         (relu'd upconv output; (h, w, i, j) -> pixel (2h+i, 2w+j))."""
         M, P, _, C = x_nhwc.shape
         x = x_nhwc.permute(0, 3, 1, 2)  # NCHW view with channels_last strides
-        x = self.conv_fcn(x)
+        for m in self.conv_fcn:
+            if isinstance(m, nn.Conv2d):
+                x = _conv_epi(m, x)
         x = x.permute(0, 2, 3, 1).reshape(M * P * P, -1)
         y = torch.addmm(self.up_b, x, self.up_w)
         return F.relu_(y).view(M, P, P, 2, 2, -1)
@@ -389,12 +430,17 @@ class Generalized_RCNN(nn.Module):
 
     # -- inference-time fusion ---------------------------------------------- #
     @torch.no_grad()
-    def fold_affine(self):
+    def fold_affine(self, epilogue: bool = True):
+        """Fold the frozen AffineChannel2d into conv weight + bias; with `epilogue`
+        the bias/residual/ReLU after each conv run as one vd_bias_act pass."""
         body = self.Conv_Body.conv_body
         stem = body.res1
-        body.res1 = nn.Sequential(OrderedDict([
-            ("conv1", _fold(stem.conv1, stem.bn1)), ("relu", nn.ReLU(inplace=True)),
-            ("maxpool", stem.maxpool)]))
+        if epilogue:
+            body.res1 = _StemEpilogue(_fold(stem.conv1, stem.bn1), stem.maxpool)
+        else:
+            body.res1 = nn.Sequential(OrderedDict([
+                ("conv1", _fold(stem.conv1, stem.bn1)), ("relu", nn.ReLU(inplace=True)),
+                ("maxpool", stem.maxpool)]))
         for i in range(2, body.convX + 1):
             for blk in getattr(body, "res%d" % i):
                 blk.f1 = _fold(blk.conv1, blk.bn1)
@@ -403,6 +449,9 @@ class Generalized_RCNN(nn.Module):
                 if blk.downsample is not None:
                     blk.fd = _fold(blk.downsample[0], blk.downsample[1])
                 blk.fused = True
+                blk.epilogue = epilogue
+        for m in self.Conv_Body.topdown_lateral_modules:
+            m.epilogue = epilogue
         self.RPN.fuse()
         self.Box_Head.prepare()
         self.Mask_Head.prepare()

@@ -327,9 +327,16 @@ def bias_act_(x: torch.Tensor, bias: Optional[torch.Tensor], residual=None, resi
         raise ValueError("x must be contiguous (NCHW or channels_last)")
     if not x.is_cuda or x.dtype != torch.float32:
         raise ValueError("x must be a float32 device tensor")
+    for v in (bias, residual_bias):
+        if v is not None and (v.numel() != C or not v.is_contiguous() or v.dtype != torch.float32):
+            raise ValueError("bias vectors must be contiguous float32 of length C")
     mode = 0
     if residual is not None:
         mode = 2 if upsample_residual else 1
+        want_shape = (N, C, H // 2, W // 2) if upsample_residual else (N, C, H, W)
+        if tuple(residual.shape) != want_shape or residual.dtype != torch.float32:
+            raise ValueError("residual shape %s, expected %s" % (tuple(residual.shape),
+                                                                 want_shape))
         want = torch.channels_last if nhwc else torch.contiguous_format
         if not residual.is_contiguous(memory_format=want):
             residual = residual.contiguous(memory_format=want)
