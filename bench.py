@@ -92,8 +92,18 @@ def xcd_order(rois, lvls, n_xcd=8):
     return order
 
 
+ROIALIGN_KERNEL = {"3": "vd::roi_align_fpn_nhwc_kernel<7,2,2> (reference order)",
+                   "8": "vd::roi_align_fpn_nhwc_sep_kernel<2,false,false> (separable)"}
+
+
+# rocprofv3 --pmc passes of this exact launch (tools/prof_roialign.sh, separate
+# passes per counter group; FETCH_SIZE doubled per the MI355X guide): L2<->fabric
+# bytes per launch, committed under profiles/ and reported as "traffic".
+ROIALIGN_PMC = {"8": "separable_v8_xcd.json", "3": "rowkernel_v3_xcd.json"}
+
+
 def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=None,
-                              use_order=True):
+                              use_order=True, out_layout="nhwc"):
     """RoIAlign (FPN NHWC, one launch over 4 levels x `frames` images) timed with HIP
     events on the launch stream; >= 8 distinct frames so the working set (>700 MB)
     exceeds the 256 MB Infinity Cache."""
@@ -114,22 +124,35 @@ def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=Non
     rois_t = torch.from_numpy(rois_np).to(dev)
     lv_t = torch.from_numpy(lv_np).to(dev)
     order = ops.xcd_roi_order(rois_t, lv_t) if use_order else None
-    out = torch.empty((frames * R, C, P, P), device=dev)
+    shape = (frames * R, P, P, C) if out_layout == "nhwc" else (frames * R, C, P, P)
+    out = torch.empty(shape, device=dev)
     s = torch.cuda.current_stream()
     for _ in range(3):
-        ops.roi_align_fpn(pyr, scales, rois_t, lv_t, P, sr, out=out, roi_order=order)
+        ops.roi_align_fpn(pyr, scales, rois_t, lv_t, P, sr, out=out, roi_order=order,
+                          out_layout=out_layout)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(iters):
-        ops.roi_align_fpn(pyr, scales, rois_t, lv_t, P, sr, out=out, roi_order=order)
+        ops.roi_align_fpn(pyr, scales, rois_t, lv_t, P, sr, out=out, roi_order=order,
+                          out_layout=out_layout)
     e1.record(s)
     e1.synchronize()
     t = e0.elapsed_time(e1) / 1e3 / iters
     achieved = nbytes / t / 1e9
+    variant = os.environ.get("VOSDET_ROIALIGN_VARIANT", "8")
+    traffic, tsrc = None, None
+    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_roialign_pmc",
+                       ROIALIGN_PMC.get(variant, "-"))
+    if use_order and out_layout == "nhwc" and (frames, R, C, P, sr) == (8, 1000, 256, 7, 2) \
+            and os.path.exists(pmc):
+        traffic = int(json.load(open(pmc))["traffic_bytes"])
+        tsrc = os.path.relpath(pmc, os.path.dirname(os.path.abspath(__file__)))
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": "vd::roi_align_fpn_nhwc_kernel<7,2,2> (XCD-ordered)" if use_order
-                      else "vd::roi_align_fpn_nhwc_kernel<7,2,2>",
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": tsrc,
+            "kernel": ROIALIGN_KERNEL.get(os.environ.get("VOSDET_ROIALIGN_VARIANT", "8"),
+                                          "vd::roi_align_fpn_nhwc_kernel")
+                      + (" (XCD-ordered)" if use_order else "") + ", out " + out_layout,
             "launch": "%d frames x %d RoIs, C=%d, P=%d, sr=%d" % (frames, R, C, P, sr),
             "algorithmic_bytes_per_launch": int(nbytes), "avg_launch_us": round(t * 1e6, 2)}
 
@@ -160,9 +183,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4, help="frames per GPU per step")
+    ap.add_argument("--batch", type=int, default=8, help="frames per GPU per step")
     ap.add_argument("--config", default="e2e_mask_rcnn_R-50-FPN_1x")
-    ap.add_argument("--layout", default="nchw", choices=["nchw", "nhwc"])
+    ap.add_argument("--layout", default="nhwc", choices=["nchw", "nhwc"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--no-roofline", action="store_true")
@@ -190,31 +213,14 @@ def main():
     F = args.batch
     frames = torch.from_numpy(synthetic_frames(F, 1 + rank * F)).to(dev)
 
-    cap, MR = pipe.det_cap, cfg.MRCNN.RESOLUTION
-    gathered = None
-    if world > 1:
-        import torch.distributed as dist
-        pad_dets = torch.zeros((F, cap, 5), device=dev)
-        pad_cls = torch.zeros((F, cap), dtype=torch.int32, device=dev)
-        pad_masks = torch.zeros((F, cap, MR, MR), device=dev)
-        g_dets = torch.zeros((world * F, cap, 5), device=dev)
-        g_cls = torch.zeros((world * F, cap), dtype=torch.int32, device=dev)
-        g_cnt = torch.zeros((world * F,), dtype=torch.int32, device=dev)
-        g_masks = torch.zeros((world * F, cap, MR, MR), device=dev)
+    from vosdetectron_amd.runner import ResultGatherer
+    gatherer = ResultGatherer(F, pipe.det_cap, cfg.MRCNN.RESOLUTION, world, dev)
 
     def step():
         out = pipe.run(frames)
-        if world > 1:
-            counts = out["counts_host"]
-            pad_masks.zero_()
-            o = 0
-            for f, c in enumerate(counts):
-                pad_masks[f, :c] = out["masks"][o:o + c]
-                o += c
-            dist.all_gather_into_tensor(g_dets, out["dets"].contiguous())
-            dist.all_gather_into_tensor(g_cls, out["classes"].contiguous())
-            dist.all_gather_into_tensor(g_cnt, out["counts"].contiguous())
-            dist.all_gather_into_tensor(g_masks, pad_masks)
+        if world > 1:  # one all_gather per result tensor over RCCL (runner.py)
+            gatherer.gather(out["dets"], out["classes"], out["counts"], out["masks"],
+                            out["counts_host"])
         return out
 
     for _ in range(args.warmup):

@@ -1,10 +1,11 @@
 """End-to-end engine on the GPU vs the oracle pipeline.
 
-Stage-wise parity (bit-exact): each HIP stage is fed the GPU's own upstream
-tensors and compared with the oracle run on the same inputs -- proposals from
-the GPU's RPN outputs, the box RoIAlign from the GPU's pyramid and rois, the
-detections from the GPU's class scores / deltas, the mask RoIAlign from the GPU
-detections.  The dense PyTorch parts (convs: MIOpen vs oneDNN, folded vs
+Stage-wise parity: each HIP stage is fed the GPU's own upstream tensors and
+compared with the oracle run on the same inputs -- proposals from the GPU's RPN
+outputs and the detections from the GPU's class scores / deltas bit-exact; the
+box RoIAlign from the GPU's pyramid and rois and the mask RoIAlign from the GPU
+detections within north_star's 1e-4 (the product's separable kernel), and
+bit-exact through the reference-order kernel (variant 3).  The dense PyTorch parts (convs: MIOpen vs oneDNN, folded vs
 unfolded AffineChannel) are compared within fp32 tolerance, and the final
 detections are matched against the fully independent CPU pipeline."""
 import numpy as np
@@ -31,7 +32,7 @@ def setup(request):
     return cfg, model, sd, pipe, frame, out
 
 
-def test_stagewise_parity(setup):
+def test_stagewise_parity(setup, monkeypatch):
     cfg, model, sd, pipe, frame, out = setup
     # blob (image_to_blob) vs get_image_blob
     blob_ref, _, im_info = orc.get_image_blob(frame)
@@ -58,9 +59,13 @@ def test_stagewise_parity(setup):
     bf_ref = orc.roi_feature_transform(blobs, rpn_ret, "rois", 7, [1. / 32, 1. / 16, 1. / 8, 1. / 4], 2)
     pyr = out["pyramid"]
     lv = orc.map_rois_to_fpn_levels(rois[:, 1:5], 2, 5).astype(np.int32) - 2
-    bf = ops.roi_align_fpn(pyr, pipe.roi_scales, torch.from_numpy(rois).to(DEV),
-                           torch.from_numpy(lv).to(DEV), 7, 2)
-    assert np.array_equal(bf.cpu().numpy(), bf_ref)
+    args = (pyr, pipe.roi_scales, torch.from_numpy(rois).to(DEV), torch.from_numpy(lv).to(DEV),
+            7, 2)
+    np.testing.assert_allclose(ops.roi_align_fpn(*args).cpu().numpy(), bf_ref, rtol=1e-4,
+                               atol=1e-4)
+    monkeypatch.setenv("VOSDET_ROIALIGN_VARIANT", "3")
+    assert np.array_equal(ops.roi_align_fpn(*args).cpu().numpy(), bf_ref)
+    monkeypatch.delenv("VOSDET_ROIALIGN_VARIANT")
     # detections from the GPU's own head outputs
     sc = out["cls_prob"][:n].cpu().numpy()
     dl = out["bbox_pred"][:n].cpu().numpy()
@@ -75,7 +80,10 @@ def test_stagewise_parity(setup):
     mret = orc.distribute(out["mask_rois"].cpu().numpy(), prefix="mask_rois")
     mf_ref = orc.roi_feature_transform(blobs, mret, "mask_rois", 14,
                                        [1. / 32, 1. / 16, 1. / 8, 1. / 4], 2)
-    assert np.array_equal(out["mask_feat"].cpu().numpy(), mf_ref)
+    mf = out["mask_feat"].cpu().numpy()
+    if mf.ndim == 4 and mf.shape[-1] == mf_ref.shape[1] and mf.shape[1] != mf_ref.shape[1]:
+        mf = mf.transpose(0, 3, 1, 2)  # NHWC product layout
+    np.testing.assert_allclose(mf, mf_ref, rtol=1e-4, atol=1e-4)
 
 
 def test_model_outputs_vs_cpu_torch(setup):

@@ -56,10 +56,12 @@ def _pyramid(rng, B, C, sizes):
 
 @pytest.mark.parametrize("P,sr,C", [(7, 2, 256), (14, 2, 256), (7, 0, 256), (7, 2, 64),
                                     (14, 2, 520), (6, 2, 128)])
-def test_roi_align_fpn_nhwc_bit_exact(P, sr, C):
+def test_roi_align_fpn_nhwc_bit_exact(P, sr, C, monkeypatch):
     """One launch over 4 levels vs the reference per-level loop + restore
-    (model_builder.py:252-303) evaluated by the oracle."""
+    (model_builder.py:252-303) evaluated by the oracle.  Kernel variant 3 keeps
+    the reference's per-sample arithmetic order: bit-exact."""
     from vosdetectron_amd import ops
+    monkeypatch.setenv("VOSDET_ROIALIGN_VARIANT", "3")
     rng = np.random.default_rng(1000 + P + sr + C)
     B = 2
     sizes = [(50, 84), (25, 42), (13, 21), (7, 11)]
@@ -154,3 +156,39 @@ def test_roi_pool_backward_matches_scatter():
     ref = np.zeros(f.size, np.float32)
     np.add.at(ref, arg[arg >= 0].ravel(), 1.0)
     assert np.array_equal(ft.grad.cpu().numpy().ravel(), ref)
+
+
+@pytest.mark.parametrize("variant", [None, "8", "9", "13", "14"])
+@pytest.mark.parametrize("P,C", [(7, 256), (14, 256), (7, 64), (14, 520)])
+def test_roi_align_fpn_separable_within_tolerance(P, C, variant, monkeypatch):
+    """Separable NHWC kernel (variant 8): same sampling, summation re-associated
+    as sum_x w_x sum_y w_y F, so it holds the reference to 1e-4 (north_star's
+    RoIAlign tolerance), not bit-for-bit."""
+    from vosdetectron_amd import ops
+    rng = np.random.default_rng(2000 + P + C)
+    B = 2
+    sizes = [(50, 84), (25, 42), (13, 21), (7, 11)]
+    scales = [1. / 4, 1. / 8, 1. / 16, 1. / 32]
+    feats = _pyramid(rng, B, C, sizes)
+    rois = make_rois(rng, 150, 336, 200, batch=B)
+    rois[:4, 1:5] = [[-30, -20, 40, 30], [300, 180, 400, 260], [0, 0, 0.5, 0.5],
+                     [330, 190, 335.9, 199.9]]  # partly outside / degenerate / at the edge
+    lv = orc.map_rois_to_fpn_levels(rois[:, 1:5], 2, 5).astype(np.int32) - 2
+    d = {"rois": rois}
+    order = np.empty((0,))
+    for k in range(4):
+        idx = np.where(lv == k)[0]
+        d["rois_fpn%d" % (k + 2)] = rois[idx]
+        order = np.concatenate([order, idx])
+    d["rois_idx_restore_int32"] = np.argsort(order, kind="stable").astype(np.int32)
+    ref = orc.roi_feature_transform(feats[::-1], d, "rois", P, scales[::-1], 2)
+    nhwc = [torch.from_numpy(x).to(DEV).permute(0, 2, 3, 1).contiguous() for x in feats]
+    if variant is None:  # the product default
+        monkeypatch.delenv("VOSDET_ROIALIGN_VARIANT", raising=False)
+    else:
+        monkeypatch.setenv("VOSDET_ROIALIGN_VARIANT", variant)
+    args = (nhwc, scales, torch.from_numpy(rois).to(DEV), torch.from_numpy(lv).to(DEV), P, 2)
+    o1 = ops.roi_align_fpn(*args).cpu().numpy()
+    o2 = ops.roi_align_fpn(*args, out_layout="nhwc").permute(0, 3, 1, 2).cpu().numpy()
+    np.testing.assert_allclose(o1, ref, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(o2, ref, rtol=1e-4, atol=1e-4)

@@ -15,7 +15,9 @@ if __name__ == "__main__":
     P = int(sys.argv[1]) if len(sys.argv) > 1 else 7
     R = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
     order = os.environ.get("ORDER", "1") == "1"
-    r = measure_roialign_roofline(torch.device("cuda"), frames=8, R=R, P=P, use_order=order)
+    frames = int(os.environ.get("FRAMES", "8"))
+    r = measure_roialign_roofline(torch.device("cuda"), frames=frames, R=R, P=P, use_order=order,
+                                  out_layout=os.environ.get("OUT", "nhwc"))
     r["variant"] = os.environ.get("VOSDET_ROIALIGN_VARIANT", "default")
     r["xcd_order"] = order
     print(json.dumps(r), flush=True)

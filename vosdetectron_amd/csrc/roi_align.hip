@@ -8,17 +8,16 @@
 //    on arbitrary caller tensors): one lane per output element, the reference's
 //    decomposition, kept as the compatibility path.
 //  * NHWC multi-level FPN (the product path): one launch for every RoI of every
-//    FPN level.  A 64-lane wave owns 256 channels of one output row (ph): each
-//    lane loads float4 (16 B) of the 4 bilinear taps, so every tap is a fully
-//    coalesced 1 KiB wave load of one pyramid pixel.  The sample geometry is
-//    wave-uniform (scalar), so re-use of the previous sample's tap columns along
-//    x is a uniform branch, not divergence.  Results are transposed through LDS
-//    into the reference's [R][C][P][P] output and written as contiguous rows.
-//
-// Arithmetic order (sample positions, weights, w1*v1+w2*v2+w3*v3+w4*v4, the
-// iy-major accumulation and the final /count) is the reference's, and the file
-// is compiled without FMA contraction, so results are bit-identical to the C
-// restatement in oracle/roi_ops.c.
+//    FPN level on the NHWC pyramid (one 1 KiB coalesced wave load per pixel,
+//    lane = 4 channels).  The default kernel (roi_align_fpn_nhwc_sep_kernel,
+//    variant 8) factors the bilinear sampling into a row pass and a column pass
+//    so each pixel is fetched ~once per output row; it re-associates the sums,
+//    so it holds the reference to 1e-4 (north_star's RoIAlign tolerance).  The
+//    row kernel (variant 3, VOSDET_ROIALIGN_VARIANT=3) keeps the reference's
+//    per-sample order -- sample positions, weights, w1*v1+w2*v2+w3*v3+w4*v4,
+//    iy-major accumulation, final /count, no FMA contraction -- and is
+//    bit-identical to the C restatement in oracle/roi_ops.c, as are the NCHW
+//    kernels.
 #include <stdlib.h>
 
 #include "common.hpp"
@@ -280,6 +279,318 @@ __device__ __forceinline__ void nhwc_row_sr(const RoiGeom &g, int C, int ph, int
             if (vxs[j]) acc[j / SR] = t;  // out-of-range sample contributes exactly 0
         }
     }
+}
+
+// --------------------------------------------------------------------------
+// Separable NHWC forward.  Bilinear sampling on a tensor-product grid factors:
+//   sum_{iy,ix} [hy hx F(yl,xl) + hy lx F(yl,xh) + ly hx F(yh,xl) + ly lx F(yh,xh)]
+//     = sum_ix [hx V(xl) + lx V(xh)],   V(x) = sum_iy [hy F(yl,x) + ly F(yh,x)],
+// with out-of-range samples dropping out of either sum.  Per output row the
+// 2*SR y taps are merged into distinct pixel rows (usually 2-3), and V(x) is
+// computed once per distinct column while the x samples sweep left to right
+// (their columns are non-decreasing), so a 1 KiB pixel is fetched ~once per row
+// instead of once per tap: ~4x fewer vector-memory instructions than
+// nhwc_row_sr, which is what bounds the gather (texture-addresser issue).  Each
+// bin is finished and stored before the next starts, so no per-row accumulator
+// array is live (low VGPRs, high occupancy).  Rounding differs from the
+// reference's per-sample order by a few ulp (north_star's RoIAlign tolerance is
+// 1e-4 fp32); the bit-exact kernels above stay selectable.
+// --------------------------------------------------------------------------
+template <int SR>
+struct RowTaps {
+    int row[2 * SR];
+    float w[2 * SR];
+    bool alive[2 * SR];
+};
+
+template <int SR>
+__device__ __forceinline__ RowTaps<SR> row_taps(const RoiGeom &g, int ph) {
+    RowTaps<SR> t;
+    const int H = g.H;
+#pragma unroll
+    for (int iy = 0; iy < SR; ++iy) {
+        float y = g.sh + ph * g.bh + (iy + .5f) * g.bh / SR;
+        const bool ok = !(y < -1.0f || y > (float)H);
+        if (y <= 0) y = 0;
+        int yl = (int)y, yh;
+        if (yl >= H - 1) { yh = yl = H - 1; y = (float)yl; } else yh = yl + 1;
+        const float ly = y - yl;
+        t.row[2 * iy] = yl;
+        t.w[2 * iy] = 1.f - ly;
+        t.alive[2 * iy] = ok;
+        t.row[2 * iy + 1] = yh;
+        t.w[2 * iy + 1] = ly;
+        t.alive[2 * iy + 1] = ok;
+    }
+#pragma unroll
+    for (int k = 1; k < 2 * SR; ++k)
+#pragma unroll
+        for (int k2 = 0; k2 < k; ++k2)
+            if (t.alive[k] && t.alive[k2] && t.row[k2] == t.row[k]) {
+                t.w[k2] += t.w[k];
+                t.alive[k] = false;
+            }
+    return t;
+}
+
+__device__ __forceinline__ float4 fma4(float w, const float4 &a, const float4 &c) {
+    return make_float4(fmaf(w, a.x, c.x), fmaf(w, a.y, c.y), fmaf(w, a.z, c.z), fmaf(w, a.w, c.w));
+}
+
+template <int SR>
+struct TapCol {
+    float4 f[2 * SR];
+};
+
+template <int SR>
+__device__ __forceinline__ TapCol<SR> load_column(const RowTaps<SR> &t, const float *base,
+                                                  int64_t rowstride, int64_t xoff) {
+    TapCol<SR> c;
+#pragma unroll
+    for (int k = 0; k < 2 * SR; ++k)
+        if (t.alive[k]) c.f[k] = ld4(base + t.row[k] * rowstride + xoff);
+    return c;
+}
+
+template <int SR, bool FMA>
+__device__ __forceinline__ float4 combine_column(const RowTaps<SR> &t, const TapCol<SR> &c) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < 2 * SR; ++k)
+        if (t.alive[k]) {
+            if (FMA) {
+                v = fma4(t.w[k], c.f[k], v);
+            } else {
+                v.x += t.w[k] * c.f[k].x;
+                v.y += t.w[k] * c.f[k].y;
+                v.z += t.w[k] * c.f[k].z;
+                v.w += t.w[k] * c.f[k].w;
+            }
+        }
+    return v;
+}
+
+// PF: while the bins consume column x, the taps of column x+1 (the next one the
+// left-to-right sweep needs unless it skips) are already in flight.
+template <int SR, bool FMA, bool PF>
+__global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
+    FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
+    const int *__restrict__ roi_order, int P, int out_nhwc, float *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float tile[];  // [C][P][P] (NCHW out)
+    const int r = roi_order ? roi_order[blockIdx.x] : (int)blockIdx.x;
+    int li = roi_level ? roi_level[r] : 0;
+    li = __builtin_amdgcn_readfirstlane(li);
+    const RoiGeom g = roi_geom(fa, C, rois + (int64_t)r * 5, li, P, P, SR);
+    const int chunks = (C + 255) / 256;
+    const int lane = lane_id();
+    const int W = g.W;
+    const int64_t rowstride = (int64_t)W * C;
+    const float inv = 1.f / g.count;  // count = SR*SR, a power of two for SR=2: exact
+    for (int u = wave_id(); u < P * chunks; u += num_waves()) {
+        const int ph = u / chunks;
+        const int ck = u - ph * chunks;
+        const int c0 = ck * 256 + lane * 4;
+        const bool active = c0 < C;
+        const float *base = g.feat + (active ? c0 : 0);
+        const RowTaps<SR> taps = row_taps<SR>(g, ph);
+        int cl = -1, ch = -1, pfc = -1;
+        float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+        TapCol<SR> pf;
+        auto column = [&](int x) -> float4 {
+            if (PF) {
+                TapCol<SR> cur;
+                if (x == pfc) cur = pf;
+                else cur = load_column<SR>(taps, base, rowstride, (int64_t)x * C);
+                pfc = min(x + 1, W - 1);
+                pf = load_column<SR>(taps, base, rowstride, (int64_t)pfc * C);
+                return combine_column<SR, FMA>(taps, cur);
+            }
+            return combine_column<SR, FMA>(taps,
+                                           load_column<SR>(taps, base, rowstride, (int64_t)x * C));
+        };
+        for (int pw = 0; pw < P; ++pw) {
+            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int ix = 0; ix < SR; ++ix) {
+                float x = g.sw + pw * g.bw + (ix + .5f) * g.bw / SR;
+                if (x < -1.0f || x > (float)W) continue;  // wave-uniform
+                if (x <= 0) x = 0;
+                int xl = (int)x, xh;
+                if (xl >= W - 1) { xh = xl = W - 1; x = (float)xl; } else xh = xl + 1;
+                const float lx = x - xl, hx = 1.f - lx;
+                if (xl != cl || xh != ch) {
+                    if (xl == ch) va = vb;
+                    else va = column(xl);
+                    vb = (xh == xl) ? va : column(xh);
+                    cl = xl;
+                    ch = xh;
+                }
+                if (FMA) {
+                    acc = fma4(hx, va, acc);
+                    acc = fma4(lx, vb, acc);
+                } else {
+                    acc.x += hx * va.x + lx * vb.x;
+                    acc.y += hx * va.y + lx * vb.y;
+                    acc.z += hx * va.z + lx * vb.z;
+                    acc.w += hx * va.w + lx * vb.w;
+                }
+            }
+            acc = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+            if (!active) continue;
+            if (out_nhwc) {
+                *reinterpret_cast<float4 *>(out + (((int64_t)r * P + ph) * P + pw) * C + c0) = acc;
+            } else {
+                float *t = tile + (int64_t)c0 * P * P + ph * P + pw;
+                t[0] = acc.x;
+                t[P * P] = acc.y;
+                t[2 * P * P] = acc.z;
+                t[3 * P * P] = acc.w;
+            }
+        }
+    }
+    if (out_nhwc) return;
+    __syncthreads();
+    const int n4 = (C * P * P) / 4;
+    float4 *o4 = reinterpret_cast<float4 *>(out + (int64_t)r * C * P * P);
+    const float4 *t4 = reinterpret_cast<const float4 *>(tile);
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) o4[i] = t4[i];
+    float *o = out + (int64_t)r * C * P * P;
+    for (int i = n4 * 4 + threadIdx.x; i < C * P * P; i += blockDim.x) o[i] = tile[i];
+}
+
+// Column-streamed separable row: the row's tap columns form the contiguous
+// range [xa, xb] (sample spacing bw/SR <= 1 px for every RoI the FPN level map
+// sends to P2-P5 at 7x7 / SR 2, except the largest on P5), so the wave walks it
+// left to right with the taps of the next DEPTH columns already in flight (a
+// static ring of raw loads: the memory-level parallelism the dependent
+// column-by-column fetch of roi_align_fpn_nhwc_sep_kernel lacks).  Samples are
+// consumed as soon as their right column has arrived; a bin is stored when its
+// last sample is done.
+template <int SR, int DEPTH>
+__global__ __launch_bounds__(512) void roi_align_fpn_nhwc_stream_kernel(
+    FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
+    const int *__restrict__ roi_order, int P, int out_nhwc, float *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float tile[];  // [C][P][P] (NCHW out)
+    constexpr int T = 2 * SR;
+    const int r = roi_order ? roi_order[blockIdx.x] : (int)blockIdx.x;
+    int li = roi_level ? roi_level[r] : 0;
+    li = __builtin_amdgcn_readfirstlane(li);
+    const RoiGeom g = roi_geom(fa, C, rois + (int64_t)r * 5, li, P, P, SR);
+    const int chunks = (C + 255) / 256;
+    const int lane = lane_id();
+    const int W = g.W;
+    const int64_t rowstride = (int64_t)W * C;
+    const float inv = 1.f / g.count;
+    const int NS = P * SR;
+    // x geometry of sample j (identical for every row)
+    auto sample = [&](int j, int &xl, int &xh, float &lx) -> bool {
+        const int pw = j / SR, ix = j - pw * SR;
+        float x = g.sw + pw * g.bw + (ix + .5f) * g.bw / SR;
+        if (x < -1.0f || x > (float)W) return false;
+        if (x <= 0) x = 0;
+        xl = (int)x;
+        if (xl >= W - 1) { xh = xl = W - 1; x = (float)xl; } else xh = xl + 1;
+        lx = x - xl;
+        return true;
+    };
+    // valid samples are a contiguous index range [ja, jb); columns [xa, xb]
+    int ja = 0, jb = NS, xa = 0, xb = -1;
+    {
+        int xl, xh;
+        float lx;
+        while (ja < NS && !sample(ja, xl, xh, lx)) ++ja;
+        if (ja < NS) xa = xl;
+        while (jb > ja && !sample(jb - 1, xl, xh, lx)) --jb;
+        if (jb > ja) xb = xh;
+    }
+    const int ncols = xb - xa + 1;
+    for (int u = wave_id(); u < P * chunks; u += num_waves()) {
+        const int ph = u / chunks;
+        const int ck = u - ph * chunks;
+        const int c0 = ck * 256 + lane * 4;
+        const bool active = c0 < C;
+        const float *base = g.feat + (active ? c0 : 0);
+        const RowTaps<SR> taps = row_taps<SR>(g, ph);
+        const float *rp[T];
+#pragma unroll
+        for (int k = 0; k < T; ++k) rp[k] = base + taps.row[k] * rowstride;
+        auto store = [&](int pw, float4 a) {
+            if (!active) return;
+            a = make_float4(a.x * inv, a.y * inv, a.z * inv, a.w * inv);
+            if (out_nhwc) {
+                *reinterpret_cast<float4 *>(out + (((int64_t)r * P + ph) * P + pw) * C + c0) = a;
+            } else {
+                float *t = tile + (int64_t)c0 * P * P + ph * P + pw;
+                t[0] = a.x;
+                t[P * P] = a.y;
+                t[2 * P * P] = a.z;
+                t[3 * P * P] = a.w;
+            }
+        };
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        int j = 0;
+        // leading out-of-range samples (contribute 0)
+        for (; j < ja; ++j)
+            if (j % SR == SR - 1) { store(j / SR, acc); acc = make_float4(0.f, 0.f, 0.f, 0.f); }
+        float4 raw[DEPTH][T];
+        auto issue = [&](float4 (&dst)[T], int col) {
+            const int64_t off = (int64_t)min(col, xb) * C;
+#pragma unroll
+            for (int k = 0; k < T; ++k)
+                if (taps.alive[k]) dst[k] = ld4(rp[k] + off);
+        };
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) issue(raw[d], xa + d);
+        float4 vprev = make_float4(0.f, 0.f, 0.f, 0.f);
+        // consume column xa + k from ring slot d, refill the slot with column + DEPTH
+        auto step = [&](int k, float4 (&slot)[T]) {
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+                if (taps.alive[t]) {
+                    v.x += taps.w[t] * slot[t].x;
+                    v.y += taps.w[t] * slot[t].y;
+                    v.z += taps.w[t] * slot[t].z;
+                    v.w += taps.w[t] * slot[t].w;
+                }
+            if (k + DEPTH < ncols) issue(slot, xa + k + DEPTH);
+            const int x = xa + k;
+            int xl, xh;
+            float lx;
+            while (j < jb) {
+                sample(j, xl, xh, lx);
+                if (xh != x) break;
+                const float hx = 1.f - lx;
+                const float4 va = (xl == x) ? v : vprev;
+                acc.x += hx * va.x + lx * v.x;
+                acc.y += hx * va.y + lx * v.y;
+                acc.z += hx * va.z + lx * v.z;
+                acc.w += hx * va.w + lx * v.w;
+                if (j % SR == SR - 1) {
+                    store(j / SR, acc);
+                    acc = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+                ++j;
+            }
+            vprev = v;
+        };
+        for (int k = 0; k < ncols; k += DEPTH) {
+#pragma unroll
+            for (int d = 0; d < DEPTH; ++d)
+                if (k + d < ncols) step(k + d, raw[d]);
+        }
+        // trailing out-of-range samples
+        for (; j < NS; ++j)
+            if (j % SR == SR - 1) { store(j / SR, acc); acc = make_float4(0.f, 0.f, 0.f, 0.f); }
+    }
+    if (out_nhwc) return;
+    __syncthreads();
+    const int n4 = (C * P * P) / 4;
+    float4 *o4 = reinterpret_cast<float4 *>(out + (int64_t)r * C * P * P);
+    const float4 *t4 = reinterpret_cast<const float4 *>(tile);
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) o4[i] = t4[i];
+    float *o = out + (int64_t)r * C * P * P;
+    for (int i = n4 * 4 + threadIdx.x; i < C * P * P; i += blockDim.x) o[i] = tile[i];
 }
 
 template <int P, int SR, int D>
@@ -694,12 +1005,51 @@ static int launch_rows(const FpnLevels &fa, int C, const float *rois, const int 
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
+static int roialign_variant() {  // read per launch so tests can switch kernels
+    const char *e = getenv("VOSDET_ROIALIGN_VARIANT");
+    // 8: separable kernel (product default, RoIAlign tolerance 1e-4);
+    // 3: bit-exact row kernel (the reference's per-sample arithmetic order)
+    return e ? atoi(e) : 8;
+}
+
+template <int SR, bool FMA, bool PF>
+static void launch_sep_t(const FpnLevels &fa, int C, const float *rois, const int *lvl,
+                         const int *order, int R, int P, int out_nhwc, float *out, hipStream_t s,
+                         int waves, size_t lds) {
+    hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_kernel<SR, FMA, PF>), dim3(R), dim3(64 * waves),
+                       lds, s, fa, C, rois, lvl, order, P, out_nhwc, out);
+}
+
+static int launch_sep(const FpnLevels &fa, int C, const float *rois, const int *lvl,
+                      const int *order, int R, int P, int out_nhwc, float *out, hipStream_t s) {
+    const size_t lds = out_nhwc ? 0 : (size_t)C * P * P * 4;
+    if (lds > 160 * 1024) return VD_ERR_SHAPE;
+    int waves = P * ((C + 255) / 256);
+    if (waves > 8) waves = 8;
+    const int v = roialign_variant();
+    if (v == 9)
+        hipLaunchKernelGGL((roi_align_fpn_nhwc_stream_kernel<2, 2>), dim3(R), dim3(64 * waves), lds,
+                           s, fa, C, rois, lvl, order, P, out_nhwc, out);
+    else if (v == 13)
+        launch_sep_t<2, true, false>(fa, C, rois, lvl, order, R, P, out_nhwc, out, s, waves, lds);
+    else if (v == 14)
+        launch_sep_t<2, true, true>(fa, C, rois, lvl, order, R, P, out_nhwc, out, s, waves, lds);
+    else
+        launch_sep_t<2, false, false>(fa, C, rois, lvl, order, R, P, out_nhwc, out, s, waves,
+                                         lds);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+
 int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, const int *lvl,
                               const int *order, int R, int PH, int PW, int sr, int out_nhwc,
                               float *out, hipStream_t s) {
     if (R == 0) return VD_OK;
     if (C % 4 != 0) return VD_ERR_SHAPE;
+    const int variant = roialign_variant();
     if (out_nhwc) {  // product path: [R][P][P][C] written straight from registers
+        if (variant >= 8 && sr == 2 && PH == PW)
+            return launch_sep(fa, C, rois, lvl, order, R, PH, 1, out, s);
         if (PH == PW && PH == 7)
             return sr == 2 ? launch_rows<7, 2, 2>(fa, C, rois, lvl, order, R, sr, out, s, 1)
                            : launch_rows<7, 0>(fa, C, rois, lvl, order, R, sr, out, s, 1);
@@ -708,10 +1058,8 @@ int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, con
                            : launch_rows<14, 0>(fa, C, rois, lvl, order, R, sr, out, s, 1);
         return VD_ERR_SHAPE;
     }
-    static const int variant = [] {
-        const char *e = getenv("VOSDET_ROIALIGN_VARIANT");
-        return e ? atoi(e) : 3;  // 3: row kernel, SR=2 unrolled, 1 sample ahead (best measured)
-    }();
+    if (variant >= 8 && sr == 2 && PH == PW && (int64_t)C * PH * PW * 4 <= 160 * 1024)
+        return launch_sep(fa, C, rois, lvl, order, R, PH, 0, out, s);
     if (C % 32 == 0 && PH * PW <= 196 && (variant == 0 || variant == 7)) {
         const int bins = PH * PW;
         int waves = (bins + 7) / 8;
