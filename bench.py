@@ -103,7 +103,7 @@ ROIALIGN_PMC = {"8": "separable_v8_xcd.json", "3": "rowkernel_v3_xcd.json"}
 
 
 def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=None,
-                              use_order=True, out_layout="nhwc"):
+                              use_order=True, out_layout="nhwc", deal=8):
     """RoIAlign (FPN NHWC, one launch over 4 levels x `frames` images) timed with HIP
     events on the launch stream; >= 8 distinct frames so the working set (>700 MB)
     exceeds the 256 MB Infinity Cache."""
@@ -123,7 +123,7 @@ def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=Non
     rois_np, lv_np = np.concatenate(rois), np.concatenate(lvls)
     rois_t = torch.from_numpy(rois_np).to(dev)
     lv_t = torch.from_numpy(lv_np).to(dev)
-    order = ops.xcd_roi_order(rois_t, lv_t) if use_order else None
+    order = ops.xcd_roi_order(rois_t, lv_t, n_xcd=deal) if use_order else None
     shape = (frames * R, P, P, C) if out_layout == "nhwc" else (frames * R, C, P, P)
     out = torch.empty(shape, device=dev)
     s = torch.cuda.current_stream()

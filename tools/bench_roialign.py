@@ -17,7 +17,8 @@ if __name__ == "__main__":
     order = os.environ.get("ORDER", "1") == "1"
     frames = int(os.environ.get("FRAMES", "8"))
     r = measure_roialign_roofline(torch.device("cuda"), frames=frames, R=R, P=P, use_order=order,
-                                  out_layout=os.environ.get("OUT", "nhwc"))
+                                  out_layout=os.environ.get("OUT", "nhwc"),
+                                  deal=int(os.environ.get("XCD_DEAL", "8")))
     r["variant"] = os.environ.get("VOSDET_ROIALIGN_VARIANT", "default")
     r["xcd_order"] = order
     print(json.dumps(r), flush=True)
