@@ -218,6 +218,79 @@ int vd_bias_act(float *x, const float *bias, const float *residual, const float 
 /* B x C x H x W -> B x H x W x C (pyramid relayout for the NHWC RoIAlign). */
 int vd_nchw_to_nhwc(const float *in, int B, int C, int H, int W, float *out, void *stream);
 
+
+/* ===========================================================================
+ * VOS temporal path (lib_vos): FlowAlign, GroupNorm epilogues, ConvGRU gates.
+ * ======================================================================== */
+
+/* FlowAlign.  Replaces
+ *   int flow_align_forward_cuda(THCudaTensor *bottom, THCudaTensor *flow,
+ *                               THCudaTensor *top)
+ *   lib_vos/vos_model/flow_align/src/flow_align_cuda.c:7-23 (kernel
+ *   flow_align_cuda_kernel.cu:15-55).
+ * features: B x C x H x W (layout VD_LAYOUT_NCHW, the reference's) or
+ * B x H x W x C (VD_LAYOUT_NHWC, C % 4 == 0); flow: B x 2 x H x W fp32 (x, y
+ * displacement in level pixels, already downsampled by the module's
+ * conv_flow_downsample); output: same layout/shape as features, written
+ * entirely (0 where the displaced position leaves [0, H-1) x [0, W-1)). */
+int vd_flow_align_forward(const float *features, const float *flow, int B, int C, int H, int W,
+                          int layout, float *output, void *stream);
+
+/* Replaces flow_align_backward_cuda (flow_align_cuda.c:25-44, kernel :57-117).
+ * NCHW only.  features_grad (B x C x H x W) and flow_grad (B x 2 x H x W) must
+ * be zero-filled by the caller (functions/flow_align.py:36-39); contributions
+ * are accumulated with fp32 atomics. */
+int vd_flow_align_backward(const float *top_grad, const float *features, const float *flow,
+                           int B, int C, int H, int W, float *features_grad, float *flow_grad,
+                           void *stream);
+
+/* GroupNorm + fused epilogue.  Replaces the nn.GroupNorm (+ residual add,
+ * + ReLU) module sequences of the GN ResNet / FPN / heads (ResNet.py:208-345,
+ * FPN.py:96-120,268-274, fast_rcnn_heads.py:228-290,
+ * mask_rcnn_heads.py:191-255) with one statistics pass and one apply pass:
+ *   out = act(GN(x [+ x2]; gamma, beta) + r),  r per residual_mode:
+ *     0: none; 1: residual (same shape); 2: residual nearest-2x upsampled
+ *     (B x H/2 x W/2); 3: GN(residual; res_gamma, res_beta) (its own
+ *     statistics, the basic_gn_shortcut branch).
+ * act: VD_ACT_*.  G groups over C channels (C % G == 0; NHWC needs
+ * (C / G) % 4 == 0).  Statistics in double, normalisation in fp32.
+ * workspace: vd_group_norm_workspace_size(B, G) bytes (x2 for residual_mode 3).
+ * out may alias x (in place) but not residual. */
+enum { VD_ACT_NONE = 0, VD_ACT_RELU = 1, VD_ACT_SIGMOID = 2, VD_ACT_TANH = 3 };
+enum { VD_GN_ACT = 0, VD_GN_GRU_Z = 1, VD_GN_GRU_R = 2, VD_GN_GRU_H = 3 };
+
+size_t vd_group_norm_workspace_size(int B, int G);
+
+int vd_group_norm_act(const float *x, const float *x2, int B, int C, int H, int W, int G,
+                      float eps, const float *gamma, const float *beta, const float *residual,
+                      int residual_mode, const float *res_gamma, const float *res_beta, int act,
+                      int layout, float *out, void *workspace, size_t ws_bytes, void *stream);
+
+/* ConvGRU gates (lib_vos/vos_nn/convgrucell.py:73-92, use_GN branch):
+ *   z  = sigmoid(GN_z(Wz_h(h) + Wz_x(x)))
+ *   hr = h * sigmoid(GN_r(Wr_h(h) + Wr_x(x)))
+ * zh/zx/rh/rx are the convolution outputs (B x C x H x W in `layout`); h the
+ * hidden state.  h == NULL means the zero state (first frame of a sequence, or
+ * the static model's fresh state): zh/rh/hr are then unused (the h-side
+ * convolutions of a zero state are exactly zero) and only z is produced.
+ * workspace: 2 * vd_group_norm_workspace_size(B, G). */
+int vd_convgru_gates(const float *zh, const float *zx, const float *rh, const float *rx,
+                     const float *h, int B, int C, int H, int W, int G, float eps,
+                     const float *gamma_z, const float *beta_z, const float *gamma_r,
+                     const float *beta_r, int layout, float *z, float *hr, void *workspace,
+                     size_t ws_bytes, void *stream);
+
+/* ConvGRU update + VOS top-down fusion (convgrucell.py:88-91;
+ * vos_model_builder.py:335-345):
+ *   hn  = (1 - z) * h + z * tanh(GN_h(Wh_h(h * r) + Wh_x(x)))   (h == NULL: z * tanh(..))
+ *   out = finer ? hn / 2 + bilinear_0.5x(finer) / 2 : hn
+ * hh may be NULL with h (zero state).  finer: the already-fused next-finer level
+ * (B x C x 2H x 2W in `layout`), or NULL for the finest level. */
+int vd_convgru_update(const float *hh, const float *hx, const float *z, const float *h,
+                      const float *finer, int B, int C, int H, int W, int G, float eps,
+                      const float *gamma_h, const float *beta_h, int layout, float *out,
+                      void *workspace, size_t ws_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,6 +66,8 @@ def lib():
         L.or_roi_align_legacy_fwd.argtypes = [f32p, ci, ci, ci, ci, f32p, ci, ci, ci, cf, f32p]
         L.or_roi_pool_fwd.argtypes = [f32p, ci, ci, ci, ci, f32p, ci, ci, ci, cf, f32p, i32p]
         L.or_roi_crop_fwd.argtypes = [f32p, ci, ci, ci, ci, f32p, ci, ci, ci, f32p]
+        L.or_flow_align_fwd.argtypes = [f32p, f32p, ci, ci, ci, ci, f32p]
+        L.or_flow_align_bwd.argtypes = [f32p, f32p, f32p, ci, ci, ci, ci, f32p, f32p]
         L.or_nms.argtypes = [f32p, ci, ci, cf, i64p]
         L.or_nms.restype = ci
         _lib = L
@@ -93,6 +95,39 @@ def roi_align(features, rois, ph, pw, spatial_scale, sampling_ratio):
         lib().or_roi_align_fwd(_p(f), B, C, H, W, _p(r), R, ph, pw,
                                float(spatial_scale), int(sampling_ratio), _p(out))
     return out
+
+
+def flow_align(features, flow):
+    """FlowAlign fwd, lib_vos/vos_model/flow_align/src/flow_align_cuda_kernel.cu:15-55.
+    features B x C x H x W f32, flow B x 2 x H x W f32."""
+    f, fl = _f32(features), _f32(flow)
+    B, C, H, W = f.shape
+    out = np.zeros_like(f)
+    lib().or_flow_align_fwd(_p(f), _p(fl), B, C, H, W, _p(out))
+    return out
+
+
+def flow_align_backward(top_diff, features, flow):
+    """FlowAlign bwd, flow_align_cuda_kernel.cu:57-117 (serial accumulation)."""
+    g, f, fl = _f32(top_diff), _f32(features), _f32(flow)
+    B, C, H, W = f.shape
+    gf = np.zeros_like(f)
+    gfl = np.zeros((B, 2, H, W), np.float32)
+    lib().or_flow_align_bwd(_p(g), _p(f), _p(fl), B, C, H, W, _p(gf), _p(gfl))
+    return gf, gfl
+
+
+def flow_downsample(flow, spatial_scale):
+    """FlowAlign.conv_flow_downsample (modules/flow_align.py:12-25): a 2->2
+    conv, kernel = stride = 1/scale, weight diag = scale**3, no bias (float32
+    torch conv, as the reference module computes it)."""
+    import torch
+    k = int(1.0 / spatial_scale)
+    w = torch.zeros((2, 2, k, k), dtype=torch.float32)
+    for i in range(2):
+        w[i, i] = spatial_scale ** 3
+    return torch.nn.functional.conv2d(torch.as_tensor(flow, dtype=torch.float32), w,
+                                      stride=k).numpy()
 
 
 def roi_align_backward(top_diff, rois, feat_shape, spatial_scale, sampling_ratio):

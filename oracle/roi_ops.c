@@ -365,3 +365,80 @@ int or_nms(const float *dets, int n, int stride, float thresh, int64_t *keep) {
 
 /* Soft-NMS restatement (lib/utils/cython_nms.pyx:98-203) is not on the
  * default inference path (TEST.SOFT_NMS.ENABLED = False, config.py:359). */
+
+/* ------------------------------------------------------------------------ */
+/* FlowAlign forward: lib_vos/vos_model/flow_align/src/flow_align_cuda_kernel.cu
+ * :15-55, grid-stride loop walked serially.  The `1.` literals promote each
+ * tap product and the sum to double before the float store (:46-49). */
+void or_flow_align_fwd(const float *bottom, const float *flow, int batches, int channels,
+                       int height, int width, float *top) {
+    const long nthreads = (long)batches * channels * height * width;
+    for (long index = 0; index < nthreads; ++index) {
+        int w = (int)(index % width);
+        int h = (int)((index / width) % height);
+        int c = (int)((index / width / height) % channels);
+        int n = (int)(index / width / height / channels);
+        long ind_flow_x = w + (long)h * width + (long)n * height * width * 2; /* :26 */
+        long ind_flow_y = w + (long)h * width + (long)width * height + (long)n * height * width * 2;
+        float flo_x = flow[ind_flow_x];
+        float flo_y = flow[ind_flow_y];
+        float w_flo = w + flo_x; /* :31-32 */
+        float h_flo = h + flo_y;
+        if (h_flo < 0 || h_flo >= height - 1 || w_flo < 0 || w_flo >= width - 1) {
+            top[index] = 0; /* :33-37 */
+        } else {
+            int h_start = (int)floorf(h_flo);
+            int w_start = (int)floorf(w_flo);
+            long nc_start = (long)n * height * width * channels + (long)c * height * width;
+            float h_ratio = h_flo - (float)h_start;
+            float w_ratio = w_flo - (float)w_start;
+            long upleft = nc_start + w_start + (long)width * h_start;
+            long upright = upleft + 1;
+            long downleft = upleft + width;
+            long downright = downleft + 1;
+            top[index] = bottom[upleft] * (1. - h_ratio) * (1. - w_ratio) +
+                         bottom[upright] * (1. - h_ratio) * (w_ratio) +
+                         bottom[downleft] * (h_ratio) * (1. - w_ratio) +
+                         bottom[downright] * (h_ratio) * (w_ratio);
+        }
+    }
+}
+
+/* FlowAlign backward: flow_align_cuda_kernel.cu:57-117 (atomics applied in
+ * serial index order). */
+void or_flow_align_bwd(const float *topdiff, const float *bottom, const float *flow, int batches,
+                       int channels, int height, int width, float *bottomdiff, float *flowdiff) {
+    const long nthreads = (long)batches * channels * height * width;
+    for (long index = 0; index < nthreads; ++index) {
+        int w = (int)(index % width);
+        int h = (int)((index / width) % height);
+        int c = (int)((index / width / height) % channels);
+        int n = (int)(index / width / height / channels);
+        long ind_flow_x = w + (long)h * width + (long)n * height * width * 2;
+        long ind_flow_y = w + (long)h * width + (long)width * height + (long)n * height * width * 2;
+        float flo_x = flow[ind_flow_x];
+        float flo_y = flow[ind_flow_y];
+        float w_flo = w + flo_x;
+        float h_flo = h + flo_y;
+        if (h_flo < 0 || h_flo >= height - 1 || w_flo < 0 || w_flo >= width - 1) continue;
+        int h_start = (int)floorf(h_flo);
+        int w_start = (int)floorf(w_flo);
+        long nc_start = (long)n * height * width * channels + (long)c * height * width;
+        float h_ratio = h_flo - (float)h_start;
+        float w_ratio = w_flo - (float)w_start;
+        long upleft = nc_start + w_start + (long)width * h_start;
+        long upright = upleft + 1;
+        long downleft = upleft + width;
+        long downright = downleft + 1;
+        bottomdiff[upleft] += (float)(topdiff[index] * (1. - h_ratio) * (1. - w_ratio));
+        bottomdiff[upright] += (float)(topdiff[index] * (1. - h_ratio) * (w_ratio));
+        bottomdiff[downleft] += (float)(topdiff[index] * (h_ratio) * (1. - w_ratio));
+        bottomdiff[downright] += (float)(topdiff[index] * (h_ratio) * (w_ratio));
+        float f1 = bottom[upleft], f2 = bottom[upright], f3 = bottom[downleft],
+              f4 = bottom[downright];
+        float dx = -f1 * (1. - h_ratio) + f2 * (1. - h_ratio) - f3 * (h_ratio) + f4 * (h_ratio);
+        float dy = -f1 * (1. - w_ratio) - f2 * (w_ratio) + f3 * (1. - w_ratio) + f4 * (w_ratio);
+        flowdiff[ind_flow_x] += topdiff[index] * dx;
+        flowdiff[ind_flow_y] += topdiff[index] * dy;
+    }
+}

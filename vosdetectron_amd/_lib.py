@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(_HERE, "libvosdet.so")
 VD_OK, VD_ERR_ARG, VD_ERR_SHAPE, VD_ERR_LAUNCH, VD_ERR_WORKSPACE = range(5)
 VD_LAYOUT_NCHW, VD_LAYOUT_NHWC = 0, 1
 VD_MAX_LEVELS = 5
+VD_ACT_NONE, VD_ACT_RELU, VD_ACT_SIGMOID, VD_ACT_TANH = range(4)
 
 _lock = threading.Lock()
 _lib = None
@@ -59,6 +60,16 @@ SIGNATURES = {
     "vd_image_to_blob": (_I, [_P, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
     "vd_nchw_to_nhwc": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "vd_bias_act": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    # VOS temporal path
+    "vd_flow_align_forward": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "vd_flow_align_backward": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "vd_group_norm_workspace_size": (_S, [_I, _I]),
+    "vd_group_norm_act": (_I, [_P, _P, _I, _I, _I, _I, _I, _F, _P, _P, _P, _I, _P, _P, _I, _I,
+                               _P, _P, _S, _P]),
+    "vd_convgru_gates": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _I,
+                              _P, _P, _P, _S, _P]),
+    "vd_convgru_update": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _P,
+                               _S, _P]),
 }
 
 

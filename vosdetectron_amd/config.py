@@ -35,7 +35,10 @@ def default_cfg() -> AttrDict:
         MODEL=_d(  # config.py:392-432
             TYPE="generalized_rcnn", CONV_BODY="FPN.fpn_ResNet50_conv5_body", NUM_CLASSES=81,
             CLS_AGNOSTIC_BBOX_REG=False, BBOX_REG_WEIGHTS=(10., 10., 5., 5.),
-            FASTER_RCNN=True, MASK_ON=True, KEYPOINTS_ON=False, RPN_ONLY=False),
+            FASTER_RCNN=True, MASK_ON=True, KEYPOINTS_ON=False, RPN_ONLY=False,
+            # fork additions, config.py:404, 926-931
+            ADD_UNKNOWN_CLASS=False, IDENTITY_TRAINING=False, IDENTITY_REPLACE_CLASS=True,
+            TOTAL_INSTANCE_NUM=0, USE_DELTA_FLOW=False, LOAD_FLOW_FILE=False),
         RESNETS=_d(  # config.py:870-905
             NUM_GROUPS=1, WIDTH_PER_GROUP=64, STRIDE_1X1=True,
             TRANS_FUNC="bottleneck_transformation", STEM_FUNC="basic_bn_stem",
@@ -48,12 +51,17 @@ def default_cfg() -> AttrDict:
             USE_GN=False),
         FAST_RCNN=_d(  # config.py:620-645
             ROI_BOX_HEAD="fast_rcnn_heads.roi_2mlp_head", MLP_HEAD_DIM=1024,
-            ROI_XFORM_METHOD="RoIPoolF", ROI_XFORM_SAMPLING_RATIO=0, ROI_XFORM_RESOLUTION=14),
+            ROI_XFORM_METHOD="RoIPoolF", ROI_XFORM_SAMPLING_RATIO=0, ROI_XFORM_RESOLUTION=14,
+            CONV_HEAD_DIM=256, NUM_STACKED_CONVS=4),
         MRCNN=_d(  # config.py:735-770
             ROI_MASK_HEAD="mask_rcnn_heads.mask_rcnn_fcn_head_v1up4convs", RESOLUTION=14,
             ROI_XFORM_METHOD="RoIAlign", ROI_XFORM_RESOLUTION=7, ROI_XFORM_SAMPLING_RATIO=0,
             DIM_REDUCED=256, DILATION=2, UPSAMPLE_RATIO=1, USE_FC_OUTPUT=False,
-            CLS_SPECIFIC_MASK=True, CONV_INIT="GaussianFill"),
+            CLS_SPECIFIC_MASK=True, CONV_INIT="GaussianFill", THRESH_BINARIZE=0.5),
+        GROUP_NORM=_d(DIM_PER_GP=-1, NUM_GROUPS=32, EPSILON=1e-5),  # config.py:983-989
+        CONVGRU=_d(  # config.py:908-921
+            HIDDEN_STATE_CHANNELS=(256, 256, 256, 256, 256), KERNEL_SIZE=3, STRIDE=1,
+            DILATION=1, GROUPS=1, USE_GN=True, GN_GROUPS=32, DYNAMIC_MODEL=True),
         RPN=_d(CLS_ACTIVATION="sigmoid", SIZES=(64, 128, 256, 512), STRIDE=16,
                ASPECT_RATIOS=(0.5, 1, 2)),  # config.py:655-675
         TEST=_d(  # config.py:180-230, 945-950
@@ -124,10 +132,48 @@ def e2e_mask_rcnn_X_101_32x8d_FPN_1x() -> AttrDict:
     return cfg
 
 
+def vos_R_101_FPN_3x_gn_static_davis() -> AttrDict:
+    """lib_vos/tools/R-101-FPN_3x_gn_static_davis.yaml, with the inference-time
+    rewrite of lib_vos/tools/infer_davis_sequential.py:104-113 (IDENTITY_TRAINING
+    and IDENTITY_REPLACE_CLASS -> NUM_CLASSES = 145, no identity head)."""
+    cfg = load_cfg(overrides={
+        "MODEL.CONV_BODY": "FPN.fpn_ResNet101_conv5_body", "MODEL.FASTER_RCNN": True,
+        "MODEL.MASK_ON": True, "MODEL.CLS_AGNOSTIC_BBOX_REG": True,
+        "MODEL.NUM_CLASSES": 145, "MODEL.IDENTITY_TRAINING": False,
+        "FPN.USE_GN": True, "FPN.COARSEST_STRIDE": 64, "FPN.RPN_ANCHOR_START_SIZE": 32,
+        "FPN.ROI_CANONICAL_SCALE": 224,
+        "RESNETS.STRIDE_1X1": False, "RESNETS.TRANS_FUNC": "bottleneck_gn_transformation",
+        "RESNETS.STEM_FUNC": "basic_gn_stem", "RESNETS.SHORTCUT_FUNC": "basic_gn_shortcut",
+        "RESNETS.USE_GN": True,
+        "FAST_RCNN.ROI_BOX_HEAD": "fast_rcnn_heads.roi_Xconv1fc_gn_head",
+        "FAST_RCNN.ROI_XFORM_METHOD": "RoIAlign", "FAST_RCNN.ROI_XFORM_RESOLUTION": 7,
+        "FAST_RCNN.ROI_XFORM_SAMPLING_RATIO": 2,
+        "MRCNN.ROI_MASK_HEAD": "mask_rcnn_heads.mask_rcnn_fcn_head_v1up4convs_gn",
+        "MRCNN.RESOLUTION": 56, "MRCNN.ROI_XFORM_METHOD": "RoIAlign",
+        "MRCNN.ROI_XFORM_RESOLUTION": 28, "MRCNN.ROI_XFORM_SAMPLING_RATIO": 2,
+        "MRCNN.DILATION": 2, "MRCNN.CONV_INIT": "MSRAFill", "MRCNN.CLS_SPECIFIC_MASK": False,
+        "CONVGRU.DYNAMIC_MODEL": False, "RPN.ASPECT_RATIOS": (0.2, 0.5, 1, 2, 5),
+        "TEST.SCALE": 480, "TEST.MAX_SIZE": 1333, "TEST.NMS": 0.5,
+        "TEST.RPN_PRE_NMS_TOP_N": 1000, "TEST.RPN_POST_NMS_TOP_N": 1000})
+    cfg.VOS = True  # build Generalized_VOS_RCNN (vos_model_builder.py:70)
+    return cfg
+
+
+def vos_R_101_FPN_3x_gn_dynamic_davis() -> AttrDict:
+    """lib_vos/tools/R-101-FPN_3x_gn_dynamic_simple_davis.yaml (ConvGRU hidden
+    states carried across the frames of a sequence), same inference rewrite."""
+    cfg = vos_R_101_FPN_3x_gn_static_davis()
+    cfg.CONVGRU.DYNAMIC_MODEL = True
+    cfg.TEST.MAX_SIZE = 1200
+    return cfg
+
+
 CONFIGS = {
     "e2e_mask_rcnn_R-50-FPN_1x": e2e_mask_rcnn_R_50_FPN_1x,
     "e2e_mask_rcnn_R-101-FPN_2x": e2e_mask_rcnn_R_101_FPN_2x,
     "e2e_mask_rcnn_X-101-32x8d-FPN_1x": e2e_mask_rcnn_X_101_32x8d_FPN_1x,
+    "vos_R-101-FPN_3x_gn_static_davis": vos_R_101_FPN_3x_gn_static_davis,
+    "vos_R-101-FPN_3x_gn_dynamic_davis": vos_R_101_FPN_3x_gn_dynamic_davis,
 }
 
 

@@ -205,4 +205,139 @@ int vd_nchw_to_nhwc(const float *in, int B, int C, int H, int W, float *out, voi
     return launch_nchw_to_nhwc(in, B, C, H, W, out, VD_STREAM(stream));
 }
 
+
+// ---------------------------------------------------------------- VOS path
+int vd_flow_align_forward(const float *features, const float *flow, int B, int C, int H, int W,
+                          int layout, float *output, void *stream) {
+    if (bad_feat(features, B, C, H, W) || !flow || !output) return VD_ERR_ARG;
+    if (layout != VD_LAYOUT_NCHW && layout != VD_LAYOUT_NHWC) return VD_ERR_ARG;
+    return launch_flow_align_fwd(features, flow, B, C, H, W, layout == VD_LAYOUT_NHWC, output,
+                                 VD_STREAM(stream));
+}
+
+int vd_flow_align_backward(const float *top_grad, const float *features, const float *flow,
+                           int B, int C, int H, int W, float *features_grad, float *flow_grad,
+                           void *stream) {
+    if (bad_feat(features, B, C, H, W) || !top_grad || !flow || !features_grad || !flow_grad)
+        return VD_ERR_ARG;
+    return launch_flow_align_bwd(top_grad, features, flow, B, C, H, W, features_grad, flow_grad,
+                                 VD_STREAM(stream));
+}
+
+size_t vd_group_norm_workspace_size(int B, int G) { return gn_workspace_bytes(B, G, 1); }
+
+static bool bad_gn(const float *x, int B, int C, int H, int W, int G, int layout) {
+    if (bad_feat(x, B, C, H, W) || G < 1 || G > 64 || C % G) return true;
+    if (layout != VD_LAYOUT_NCHW && layout != VD_LAYOUT_NHWC) return true;
+    return false;
+}
+
+int vd_group_norm_act(const float *x, const float *x2, int B, int C, int H, int W, int G,
+                      float eps, const float *gamma, const float *beta, const float *residual,
+                      int residual_mode, const float *res_gamma, const float *res_beta, int act,
+                      int layout, float *out, void *workspace, size_t ws_bytes, void *stream) {
+    if (bad_gn(x, B, C, H, W, G, layout) || !gamma || !beta || !out || !workspace)
+        return VD_ERR_ARG;
+    if (residual_mode < 0 || residual_mode > 3 || act < 0 || act > 3) return VD_ERR_ARG;
+    if (residual_mode && !residual) return VD_ERR_ARG;
+    if (residual_mode == 3 && (!res_gamma || !res_beta)) return VD_ERR_ARG;
+    if (residual_mode == 2 && ((H & 1) || (W & 1))) return VD_ERR_SHAPE;
+    const int nsets = residual_mode == 3 ? 2 : 1;
+    if (ws_bytes < gn_workspace_bytes(B, G, nsets)) return VD_ERR_WORKSPACE;
+    double *ws = static_cast<double *>(workspace);
+    const size_t per = (size_t)B * G * 2;
+    GnSets sets = {};
+    sets.s[0] = {x, x2, ws};
+    sets.s[1] = {residual, nullptr, ws + per};
+    hipStream_t s = VD_STREAM(stream);
+    const int nhwc = layout == VD_LAYOUT_NHWC;
+    int st = launch_gn_stats(sets, nsets, B, C, H * W, G, nhwc, s);
+    if (st != VD_OK) return st;
+    GnApply a = {};
+    a.x = x;
+    a.x2 = x2;
+    a.ws = ws;
+    a.gamma = gamma;
+    a.beta = beta;
+    a.res = residual;
+    a.res_ws = residual_mode == 3 ? ws + per : nullptr;
+    a.res_gamma = res_gamma;
+    a.res_beta = res_beta;
+    a.out = out;
+    a.mode = VD_GN_ACT;
+    a.act = act;
+    a.res_mode = residual_mode;
+    a.eps = eps;
+    return launch_gn_apply(a, B, C, H, W, G, nhwc, s);
+}
+
+int vd_convgru_gates(const float *zh, const float *zx, const float *rh, const float *rx,
+                     const float *h, int B, int C, int H, int W, int G, float eps,
+                     const float *gamma_z, const float *beta_z, const float *gamma_r,
+                     const float *beta_r, int layout, float *z, float *hr, void *workspace,
+                     size_t ws_bytes, void *stream) {
+    if (bad_gn(zx, B, C, H, W, G, layout) || !gamma_z || !beta_z || !z || !workspace)
+        return VD_ERR_ARG;
+    if (h && (!zh || !rh || !rx || !gamma_r || !beta_r || !hr)) return VD_ERR_ARG;
+    if (ws_bytes < gn_workspace_bytes(B, G, 2)) return VD_ERR_WORKSPACE;
+    double *ws = static_cast<double *>(workspace);
+    const size_t per = (size_t)B * G * 2;
+    GnSets sets = {};
+    sets.s[0] = {zx, h ? zh : nullptr, ws};
+    sets.s[1] = {rx, rh, ws + per};
+    hipStream_t s = VD_STREAM(stream);
+    const int nhwc = layout == VD_LAYOUT_NHWC;
+    int st = launch_gn_stats(sets, h ? 2 : 1, B, C, H * W, G, nhwc, s);
+    if (st != VD_OK) return st;
+    GnApply a = {};
+    a.x = zx;
+    a.x2 = h ? zh : nullptr;
+    a.ws = ws;
+    a.gamma = gamma_z;
+    a.beta = beta_z;
+    a.out = z;
+    a.mode = VD_GN_GRU_Z;
+    a.eps = eps;
+    st = launch_gn_apply(a, B, C, H, W, G, nhwc, s);
+    if (st != VD_OK || !h) return st;
+    a.x = rx;
+    a.x2 = rh;
+    a.ws = ws + per;
+    a.gamma = gamma_r;
+    a.beta = beta_r;
+    a.res = h;
+    a.out = hr;
+    a.mode = VD_GN_GRU_R;
+    return launch_gn_apply(a, B, C, H, W, G, nhwc, s);
+}
+
+int vd_convgru_update(const float *hh, const float *hx, const float *z, const float *h,
+                      const float *finer, int B, int C, int H, int W, int G, float eps,
+                      const float *gamma_h, const float *beta_h, int layout, float *out,
+                      void *workspace, size_t ws_bytes, void *stream) {
+    if (bad_gn(hx, B, C, H, W, G, layout) || !z || !gamma_h || !beta_h || !out || !workspace)
+        return VD_ERR_ARG;
+    if (h && !hh) return VD_ERR_ARG;
+    if (ws_bytes < gn_workspace_bytes(B, G, 1)) return VD_ERR_WORKSPACE;
+    GnSets sets = {};
+    sets.s[0] = {hx, h ? hh : nullptr, static_cast<double *>(workspace)};
+    hipStream_t s = VD_STREAM(stream);
+    const int nhwc = layout == VD_LAYOUT_NHWC;
+    int st = launch_gn_stats(sets, 1, B, C, H * W, G, nhwc, s);
+    if (st != VD_OK) return st;
+    GnApply a = {};
+    a.x = hx;
+    a.x2 = h ? hh : nullptr;
+    a.ws = static_cast<double *>(workspace);
+    a.gamma = gamma_h;
+    a.beta = beta_h;
+    a.res = h;
+    a.z = z;
+    a.finer = finer;
+    a.out = out;
+    a.mode = VD_GN_GRU_H;
+    a.eps = eps;
+    return launch_gn_apply(a, B, C, H, W, G, nhwc, s);
+}
+
 }  // extern "C"

@@ -70,4 +70,37 @@ int launch_bias_act(float *x, const float *bias, const float *z, const float *bi
                     int C, int H, int W, int nhwc, int mode, int relu, hipStream_t s);
 int launch_nchw_to_nhwc(const float *in, int B, int C, int H, int W, float *out, hipStream_t s);
 
+// ---- VOS temporal path (vos.hip)
+// GroupNorm statistics: ws[n][g] = {sum, sum of squares} (double) of x (+ x2).
+struct GnSet {
+    const float *x;
+    const float *x2;  // optional: statistics of x + x2 (torch's a + b, then GN)
+    double *ws;
+};
+struct GnSets {
+    GnSet s[3];
+};
+// GroupNorm apply + fused epilogue (modes VD_GN_* of vosdet.h, see vos.hip).
+struct GnApply {
+    const float *x, *x2;
+    const double *ws;
+    const float *gamma, *beta;
+    const float *res;      // residual (VD_GN_ACT) or the hidden state h (GRU modes)
+    const double *res_ws;  // res_mode 3: statistics of res
+    const float *res_gamma, *res_beta;
+    const float *z;      // VD_GN_GRU_H: update gate
+    const float *finer;  // VD_GN_GRU_H: finer fused level (2H x 2W), or NULL
+    float *out;
+    int mode, act, res_mode;
+    float eps;
+};
+int launch_flow_align_fwd(const float *feat, const float *flow, int B, int C, int H, int W,
+                          int nhwc, float *out, hipStream_t s);
+int launch_flow_align_bwd(const float *top_diff, const float *feat, const float *flow, int B,
+                          int C, int H, int W, float *feat_diff, float *flow_diff, hipStream_t s);
+size_t gn_workspace_bytes(int B, int G, int sets);
+int launch_gn_stats(const GnSets &sets, int nsets, int B, int C, int HW, int G, int nhwc,
+                    hipStream_t s);
+int launch_gn_apply(const GnApply &a, int B, int C, int H, int W, int G, int nhwc, hipStream_t s);
+
 }  // namespace vd

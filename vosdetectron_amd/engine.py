@@ -110,7 +110,7 @@ class FramePipeline:
         pyr = self.nhwc_pyramid(feats)
         fr = cfg.FAST_RCNN
         flat_rois, flat_lvl = rois.view(-1, 5), rlvl.view(-1)
-        fast = self.channels_last and hasattr(self.model.Box_Head, "fc1_nhwc_weight")
+        fast = self.channels_last and getattr(self.model.Box_Head, "nhwc_ready", False)
         box_feat = ops.roi_align_fpn(pyr, self.roi_scales, flat_rois, flat_lvl,
                                      fr.ROI_XFORM_RESOLUTION, fr.ROI_XFORM_SAMPLING_RATIO,
                                      roi_order=ops.xcd_roi_order(flat_rois, flat_lvl),
@@ -118,6 +118,7 @@ class FramePipeline:
         x = self.model.Box_Head.mlp_nhwc(box_feat) if fast else self.model.Box_Head.mlp(box_feat)
         cls_prob, bbox_pred = self.model.Box_Outs(x)
         K = cls_prob.shape[1]
+        bbox_pred = self.model.Box_Outs.per_class_deltas(bbox_pred, K)
         dets, dcls, dcnt = ops.box_detections(
             rois, cls_prob.view(F, post, K), bbox_pred.view(F, post, 4 * K), rcnt,
             self.im_scale_t[:F], self.im_hw[:F], tst.SCORE_THRESH, tst.NMS,
@@ -151,7 +152,7 @@ class FramePipeline:
         mc = cfg.MRCNN
         mcls = dcls.view(-1).index_select(0, sel)
         out["mask_rois"] = mrois
-        if fast and hasattr(self.model.Mask_Head, "up_w"):
+        if fast and getattr(self.model.Mask_Head, "nhwc_ready", False):
             if Mp > M:
                 mrois = torch.cat([mrois, mrois.new_zeros((Mp - M, 5))])
                 mlvl = torch.cat([mlvl, mlvl.new_zeros((Mp - M,))])
@@ -169,3 +170,41 @@ class FramePipeline:
         out["masks"] = self.model.Mask_Outs.selected(mh, mcls)
         out["mask_feat"] = mfeat
         return out
+
+
+class VOSPipeline(FramePipeline):
+    """The VOS frame loop (lib_vos/tools/infer_davis_sequential.py:134-149 driving
+    Generalized_VOS_RCNN._forward, vos_model_builder.py:289-447) for F sequences
+    in lockstep: batch row b of every step is the next frame of sequence b, and
+    the ConvGRU hidden states (one B x H x W x C tensor per level, in HBM) carry
+    each sequence's state to its next frame.  `reset` starts new sequences
+    (clean_hidden_states, :279-281)."""
+
+    def __init__(self, model, cfg, frame_hw=(480, 854), batch=1, channels_last=False,
+                 det_cap=256, device="cuda"):
+        super().__init__(model, cfg, frame_hw, batch, channels_last, det_cap, device)
+        self._flow = None
+
+    def reset(self, rows=None):
+        """Zero the hidden states of batch rows `rows` (all when None)."""
+        hs = self.model.hidden_states
+        if rows is None or all(h is None for h in hs):
+            self.model.clean_hidden_states()
+            return
+        for h in hs:
+            if h is not None:
+                h[list(rows)] = 0
+
+    def backbone(self, frames):
+        feats = super().backbone(frames)
+        return self.model.temporal_fusion(feats, self._flow)
+
+    @torch.no_grad()
+    def run(self, frames: torch.Tensor, flow: torch.Tensor = None, keep_intermediates=False):
+        """frames: F x H x W x 3 u8 (frame t of each sequence); flow: optional
+        F x 2 x Hp x Wp optical flow at blob resolution (flo_to_blob, data_flow)."""
+        self._flow = flow
+        try:
+            return super().run(frames, keep_intermediates)
+        finally:
+            self._flow = None

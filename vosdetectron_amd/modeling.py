@@ -99,6 +99,78 @@ class Bottleneck(nn.Module):
         return F.relu(out + res, inplace=True)
 
 
+def group_gn(dim: int, cfg) -> int:
+    """utils/net.py get_group_gn (:208-226)."""
+    dpg, ng = cfg.GROUP_NORM.DIM_PER_GP, cfg.GROUP_NORM.NUM_GROUPS
+    assert dpg == -1 or ng == -1, "GroupNorm: can only specify G or C/G."
+    if dpg > 0:
+        assert dim % dpg == 0
+        return dim // dpg
+    assert dim % ng == 0
+    return ng
+
+
+def _gn(dim: int, cfg) -> nn.GroupNorm:
+    return nn.GroupNorm(group_gn(dim, cfg), dim, eps=cfg.GROUP_NORM.EPSILON)
+
+
+def _gn_epi(conv: nn.Conv2d, gn: nn.GroupNorm, x, act="relu", res=None, res_gn=None, up=False):
+    """conv (no bias) -> one vd_group_norm_act: act(GN(conv(x)) + res), the residual
+    optionally normalised by its own GroupNorm (res_gn) or nearest-2x upsampled."""
+    y = _conv_nb(conv, x)
+    return ops.group_norm_act(y, gn.num_groups, gn.weight, gn.bias, gn.eps, residual=res,
+                              residual_gn=(res_gn.weight, res_gn.bias) if res_gn is not None
+                              else None, upsample_residual=up, act=act, out=y)
+
+
+class BottleneckGN(nn.Module):
+    """ResNet.py bottleneck_gn_transformation (:296-345) with basic_gn_shortcut
+    (:208-218).  GPU path: each conv's GroupNorm (+ shortcut GroupNorm, residual
+    add, ReLU) runs as one vd_group_norm_act."""
+
+    def __init__(self, inplanes, outplanes, innerplanes, stride, group, stride_1x1, cfg):
+        super().__init__()
+        s1, s3 = (stride, 1) if stride_1x1 else (1, stride)
+        self.conv1 = nn.Conv2d(inplanes, innerplanes, 1, s1, bias=False)
+        self.gn1 = _gn(innerplanes, cfg)
+        self.conv2 = nn.Conv2d(innerplanes, innerplanes, 3, s3, 1, bias=False, groups=group)
+        self.gn2 = _gn(innerplanes, cfg)
+        self.conv3 = nn.Conv2d(innerplanes, outplanes, 1, 1, bias=False)
+        self.gn3 = _gn(outplanes, cfg)
+        self.downsample = None
+        if stride != 1 or inplanes != outplanes:
+            self.downsample = nn.Sequential(nn.Conv2d(inplanes, outplanes, 1, stride, bias=False),
+                                            _gn(outplanes, cfg))
+        self.epilogue = False
+
+    def forward(self, x):
+        if self.epilogue and x.is_cuda:
+            out = _gn_epi(self.conv1, self.gn1, x)
+            out = _gn_epi(self.conv2, self.gn2, out)
+            if self.downsample is not None:
+                return _gn_epi(self.conv3, self.gn3, out, res=_conv_nb(self.downsample[0], x),
+                               res_gn=self.downsample[1])
+            return _gn_epi(self.conv3, self.gn3, out, res=x)
+        out = F.relu(self.gn1(self.conv1(x)), inplace=True)
+        out = F.relu(self.gn2(self.conv2(out)), inplace=True)
+        out = self.gn3(self.conv3(out))
+        res = self.downsample(x) if self.downsample is not None else x
+        return F.relu(out + res, inplace=True)
+
+
+class _StemGN(nn.Module):
+    """basic_gn_stem (ResNet.py:233-241) with the GroupNorm + ReLU fused."""
+
+    def __init__(self, conv1, gn1, maxpool):
+        super().__init__()
+        self.conv1, self.gn1, self.maxpool = conv1, gn1, maxpool
+
+    def forward(self, x):
+        if x.is_cuda:
+            return self.maxpool(_gn_epi(self.conv1, self.gn1, x))
+        return self.maxpool(F.relu(self.gn1(self.conv1(x)), inplace=True))
+
+
 def _fold(conv: nn.Conv2d, aff: AffineChannel2d) -> nn.Conv2d:
     f = nn.Conv2d(conv.in_channels, conv.out_channels, conv.kernel_size, conv.stride,
                   conv.padding, conv.dilation, conv.groups, bias=True).to(conv.weight.device)
@@ -124,15 +196,19 @@ class _StemEpilogue(nn.Module):
 
 
 class ResNetBody(nn.Module):
-    """ResNet.py ResNet_convX_body with basic_bn_stem (res1..res5)."""
+    """ResNet.py ResNet_convX_body (res1..res5) with basic_bn_stem /
+    bottleneck_transformation, or (cfg given and RESNETS.USE_GN) basic_gn_stem /
+    bottleneck_gn_transformation / basic_gn_shortcut."""
 
-    def __init__(self, block_counts, groups=1, width_per_group=64, stride_1x1=True):
+    def __init__(self, block_counts, groups=1, width_per_group=64, stride_1x1=True, cfg=None):
         super().__init__()
         self.block_counts = block_counts
         self.convX = len(block_counts) + 1
+        self.use_gn = bool(cfg is not None and cfg.RESNETS.USE_GN)
+        norm = ("gn1", _gn(64, cfg)) if self.use_gn else ("bn1", AffineChannel2d(64))
         self.res1 = nn.Sequential(OrderedDict([
             ("conv1", nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)),
-            ("bn1", AffineChannel2d(64)),
+            norm,
             ("relu", nn.ReLU(inplace=True)),
             ("maxpool", nn.MaxPool2d(kernel_size=3, stride=2, padding=1))]))
         inner = groups * width_per_group
@@ -141,8 +217,10 @@ class ResNetBody(nn.Module):
         for i, (n, (out, innerp, stride)) in enumerate(zip(block_counts, specs)):
             blocks = []
             for b in range(n):
-                blocks.append(Bottleneck(dim_in, out, innerp, stride if b == 0 else 1, groups,
-                                         stride_1x1))
+                st = stride if b == 0 else 1
+                blocks.append(BottleneckGN(dim_in, out, innerp, st, groups, stride_1x1, cfg)
+                              if self.use_gn else
+                              Bottleneck(dim_in, out, innerp, st, groups, stride_1x1))
                 dim_in = out
             setattr(self, "res%d" % (i + 2), nn.Sequential(*blocks))
         self.dim_out = dim_in
@@ -156,15 +234,24 @@ class ResNetBody(nn.Module):
 
 
 class TopdownLateral(nn.Module):
-    """FPN.py topdown_lateral_module: lateral 1x1 + nearest 2x top-down."""
+    """FPN.py topdown_lateral_module (:261-299): lateral 1x1 (+ GroupNorm with
+    FPN.USE_GN) + nearest 2x top-down."""
 
-    def __init__(self, dim_top, dim_lateral):
+    def __init__(self, dim_top, dim_lateral, cfg=None):
         super().__init__()
-        self.conv_lateral = nn.Conv2d(dim_lateral, dim_top, 1, 1, 0)
+        self.use_gn = bool(cfg is not None and cfg.FPN.USE_GN)
+        if self.use_gn:
+            self.conv_lateral = nn.Sequential(nn.Conv2d(dim_lateral, dim_top, 1, 1, 0, bias=False),
+                                              _gn(dim_top, cfg))
+        else:
+            self.conv_lateral = nn.Conv2d(dim_lateral, dim_top, 1, 1, 0)
         self.epilogue = False
 
     def forward(self, top, lateral):
         if self.epilogue and lateral.is_cuda:
+            if self.use_gn:
+                return _gn_epi(self.conv_lateral[0], self.conv_lateral[1], lateral, act=None,
+                               res=top, up=True)
             return _conv_epi(self.conv_lateral, lateral, relu=False, res=top, up=True)
         return self.conv_lateral(lateral) + F.interpolate(top, scale_factor=2, mode="nearest")
 
@@ -176,22 +263,42 @@ class FPNBody(nn.Module):
         super().__init__()
         counts = _stage_counts(cfg.MODEL.CONV_BODY)
         self.conv_body = ResNetBody(counts, cfg.RESNETS.NUM_GROUPS, cfg.RESNETS.WIDTH_PER_GROUP,
-                                    cfg.RESNETS.STRIDE_1X1)
+                                    cfg.RESNETS.STRIDE_1X1, cfg)
         dim = cfg.FPN.DIM
         lat_dims = (2048, 1024, 512, 256)
-        self.conv_top = nn.Conv2d(lat_dims[0], dim, 1, 1, 0)
+        self.use_gn = bool(cfg.FPN.USE_GN)
+        if self.use_gn:  # FPN.py:96-101, 113-120
+            self.conv_top = nn.Sequential(nn.Conv2d(lat_dims[0], dim, 1, 1, 0, bias=False),
+                                          _gn(dim, cfg))
+            self.posthoc_modules = nn.ModuleList(
+                [nn.Sequential(nn.Conv2d(dim, dim, 3, 1, 1, bias=False), _gn(dim, cfg))
+                 for _ in range(4)])
+        else:
+            self.conv_top = nn.Conv2d(lat_dims[0], dim, 1, 1, 0)
+            self.posthoc_modules = nn.ModuleList([nn.Conv2d(dim, dim, 3, 1, 1) for _ in range(4)])
         self.topdown_lateral_modules = nn.ModuleList(
-            [TopdownLateral(dim, lat_dims[i + 1]) for i in range(3)])
-        self.posthoc_modules = nn.ModuleList([nn.Conv2d(dim, dim, 3, 1, 1) for _ in range(4)])
+            [TopdownLateral(dim, lat_dims[i + 1], cfg) for i in range(3)])
         self.spatial_scale = [1. / 64, 1. / 32, 1. / 16, 1. / 8, 1. / 4]  # incl. P6
         self.dim_out = dim
+        self.epilogue = False
+
+    def _gn_seq(self, m, x):
+        if self.epilogue and x.is_cuda:
+            return _gn_epi(m[0], m[1], x, act=None)
+        return m(x)
 
     def forward(self, x):
         c = self.conv_body.forward_stages(x)  # res1..res5
-        inner = [self.conv_top(c[-1])]
+        if self.use_gn:
+            inner = [self._gn_seq(self.conv_top, c[-1])]
+        else:
+            inner = [self.conv_top(c[-1])]
         for i in range(3):
             inner.append(self.topdown_lateral_modules[i](inner[-1], c[-(i + 2)]))
-        outs = [self.posthoc_modules[i](inner[i]) for i in range(4)]
+        if self.use_gn:
+            outs = [self._gn_seq(self.posthoc_modules[i], inner[i]) for i in range(4)]
+        else:
+            outs = [self.posthoc_modules[i](inner[i]) for i in range(4)]
         outs.insert(0, F.max_pool2d(outs[0], kernel_size=1, stride=2, padding=0))  # P6
         return outs  # [P6, P5, P4, P3, P2]
 
@@ -262,6 +369,59 @@ class Roi2MLPHead(nn.Module):
         C = w.shape[1] // (res * res)
         self.fc1_nhwc_weight = (w.view(w.shape[0], C, res, res).permute(0, 2, 3, 1)
                                 .reshape(w.shape[0], -1).contiguous())
+        self.nhwc_ready = True
+
+    def forward(self, x, rpn_ret):
+        c = self.cfg.FAST_RCNN
+        x = self.roi_xform(x, rpn_ret, blob_rois="rois", method=c.ROI_XFORM_METHOD,
+                           resolution=c.ROI_XFORM_RESOLUTION, spatial_scale=self.spatial_scale,
+                           sampling_ratio=c.ROI_XFORM_SAMPLING_RATIO)
+        return self.mlp(x)
+
+
+class RoiXconv1fcGNHead(nn.Module):
+    """fast_rcnn_heads.roi_Xconv1fc_gn_head (:227-290): NUM_STACKED_CONVS x
+    (conv 3x3, GroupNorm, ReLU) + fc + ReLU.  The NHWC path runs each
+    GroupNorm + ReLU as one vd_group_norm_act on the R x P x P x C RoI features
+    straight from the RoIAlign kernel; fc's columns are permuted once to match."""
+
+    def __init__(self, dim_in, roi_xform, spatial_scale, cfg):
+        super().__init__()
+        self.roi_xform = roi_xform
+        self.spatial_scale = spatial_scale
+        self.cfg = cfg
+        hid = cfg.FAST_RCNN.CONV_HEAD_DIM
+        mods = []
+        for _ in range(cfg.FAST_RCNN.NUM_STACKED_CONVS):
+            mods += [nn.Conv2d(dim_in, hid, 3, 1, 1, bias=False), _gn(hid, cfg),
+                     nn.ReLU(inplace=True)]
+            dim_in = hid
+        self.convs = nn.Sequential(*mods)
+        res = cfg.FAST_RCNN.ROI_XFORM_RESOLUTION
+        self.dim_out = cfg.FAST_RCNN.MLP_HEAD_DIM
+        self.fc = nn.Linear(dim_in * res * res, self.dim_out)
+
+    def mlp(self, x):
+        x = self.convs(x)
+        return F.relu(self.fc(x.reshape(x.size(0), -1)), inplace=True)
+
+    def mlp_nhwc(self, x):
+        R = x.shape[0]
+        y = x.permute(0, 3, 1, 2)  # NCHW view, channels_last memory
+        for i in range(0, len(self.convs), 3):
+            y = _gn_epi(self.convs[i], self.convs[i + 1], y)
+        y = y.permute(0, 2, 3, 1).reshape(R, -1)
+        return F.relu(F.linear(y, self.fc_nhwc_weight, self.fc.bias), inplace=True)
+
+    @torch.no_grad()
+    def prepare(self):
+        res = self.cfg.FAST_RCNN.ROI_XFORM_RESOLUTION
+        w = self.fc.weight
+        C = w.shape[1] // (res * res)
+        self.fc_nhwc_weight = (w.view(w.shape[0], C, res, res).permute(0, 2, 3, 1)
+                               .reshape(w.shape[0], -1).contiguous())
+        self.convs.to(memory_format=torch.channels_last)
+        self.nhwc_ready = True
 
     def forward(self, x, rpn_ret):
         c = self.cfg.FAST_RCNN
@@ -272,15 +432,24 @@ class Roi2MLPHead(nn.Module):
 
 
 class FastRCNNOutputs(nn.Module):
-    """fast_rcnn_heads.fast_rcnn_outputs (softmax at inference)."""
+    """fast_rcnn_heads.fast_rcnn_outputs (:13-84; softmax at inference).  With
+    CLS_AGNOSTIC_BBOX_REG the box head predicts 2 x 4 deltas (bg, fg)."""
 
-    def __init__(self, dim_in, num_classes):
+    def __init__(self, dim_in, num_classes, cls_agnostic=False):
         super().__init__()
         self.cls_score = nn.Linear(dim_in, num_classes)
-        self.bbox_pred = nn.Linear(dim_in, 4 * num_classes)
+        self.bbox_pred = nn.Linear(dim_in, 4 * (2 if cls_agnostic else num_classes))
+        self.cls_agnostic = cls_agnostic
 
     def forward(self, x):
         return F.softmax(self.cls_score(x), dim=1), self.bbox_pred(x)
+
+    def per_class_deltas(self, bbox_pred, num_classes):
+        """vos_test.py:179-190 decodes the fg deltas once and tiles the boxes over
+        the classes; decoding the tiled deltas per class gives the same boxes."""
+        if not self.cls_agnostic:
+            return bbox_pred
+        return bbox_pred[:, -4:].repeat(1, num_classes)
 
 
 class MaskHeadV1upXconvs(nn.Module):
@@ -311,18 +480,22 @@ class MaskHeadV1upXconvs(nn.Module):
         w = self.upconv.weight  # Cin x Cout x 2 x 2
         self.up_w = w.permute(0, 2, 3, 1).reshape(w.shape[0], -1).contiguous()  # Cin x (i,j,co)
         self.up_b = self.upconv.bias.repeat(4).contiguous()
+        self.nhwc_ready = True
 
     def head_nhwc(self, x_nhwc):
         """x_nhwc: M x P x P x C RoI features.  Returns M x P x P x 2 x 2 x C
         (relu'd upconv output; (h, w, i, j) -> pixel (2h+i, 2w+j))."""
         M, P, _, C = x_nhwc.shape
-        x = x_nhwc.permute(0, 3, 1, 2)  # NCHW view with channels_last strides
-        for m in self.conv_fcn:
-            if isinstance(m, nn.Conv2d):
-                x = _conv_epi(m, x)
+        x = self._convs_nhwc(x_nhwc.permute(0, 3, 1, 2))  # NCHW view, channels_last
         x = x.permute(0, 2, 3, 1).reshape(M * P * P, -1)
         y = torch.addmm(self.up_b, x, self.up_w)
         return F.relu_(y).view(M, P, P, 2, 2, -1)
+
+    def _convs_nhwc(self, x):
+        for m in self.conv_fcn:
+            if isinstance(m, nn.Conv2d):
+                x = _conv_epi(m, x)
+        return x
 
     def forward(self, x, rpn_ret):
         c = self.cfg.MRCNN
@@ -330,6 +503,27 @@ class MaskHeadV1upXconvs(nn.Module):
                            resolution=c.ROI_XFORM_RESOLUTION, spatial_scale=self.spatial_scale,
                            sampling_ratio=c.ROI_XFORM_SAMPLING_RATIO)
         return self.head(x)
+
+
+class MaskHeadV1upXconvsGN(MaskHeadV1upXconvs):
+    """mask_rcnn_heads.mask_rcnn_fcn_head_v1upXconvs_gn (:191-255): X x (conv 3x3
+    no bias, GroupNorm, ReLU), ConvTranspose 2x2 + ReLU."""
+
+    def __init__(self, dim_in, roi_xform, spatial_scale, cfg, num_convs=4):
+        super().__init__(dim_in, roi_xform, spatial_scale, cfg, num_convs)
+        d = cfg.MRCNN.DILATION
+        inner = cfg.MRCNN.DIM_REDUCED
+        mods = []
+        for _ in range(num_convs):
+            mods += [nn.Conv2d(dim_in, inner, 3, 1, padding=d, dilation=d, bias=False),
+                     _gn(inner, cfg), nn.ReLU(inplace=True)]
+            dim_in = inner
+        self.conv_fcn = nn.Sequential(*mods)
+
+    def _convs_nhwc(self, x):
+        for i in range(0, len(self.conv_fcn), 3):
+            x = _gn_epi(self.conv_fcn[i], self.conv_fcn[i + 1], x)
+        return x
 
 
 class MaskRCNNOutputs(nn.Module):
@@ -344,22 +538,42 @@ class MaskRCNNOutputs(nn.Module):
     def forward(self, x):
         return torch.sigmoid(self.classify(x))
 
+    def _channel(self, cls_idx):
+        """Mask channel of each RoI: its class, or 0 for a class-agnostic head
+        (MRCNN.CLS_SPECIFIC_MASK False, mask_rcnn_heads.py:26; segm_results
+        reads masks[i, 0], vos_test.py:885-888)."""
+        if self.classify.out_channels == 1:
+            return torch.zeros_like(cls_idx, dtype=torch.long)
+        return cls_idx.long()
+
     def selected(self, x, cls_idx):
         """Sigmoid of only the channel of each RoI's class: the per-RoI dot
         product with the selected 1x1 filter (what segm_results consumes)."""
-        w = self.classify.weight[cls_idx.long(), :, 0, 0]  # M x D
-        b = self.classify.bias[cls_idx.long()]
+        ch = self._channel(cls_idx)
+        w = self.classify.weight[ch, :, 0, 0]  # M x D
+        b = self.classify.bias[ch]
         y = torch.einsum("mdhw,md->mhw", x, w) + b.view(-1, 1, 1)
         return torch.sigmoid(y)
 
     def selected_from_up(self, up, cls_idx):
         """up: M x P x P x 2 x 2 x D (MaskHead.head_nhwc) -> M x 2P x 2P masks."""
         M, P = up.shape[0], up.shape[1]
-        w = self.classify.weight[cls_idx.long(), :, 0, 0]  # M x D
-        b = self.classify.bias[cls_idx.long()]
+        ch = self._channel(cls_idx)
+        w = self.classify.weight[ch, :, 0, 0]  # M x D
+        b = self.classify.bias[ch]
         y = torch.bmm(up.view(M, P * P * 4, -1), w.unsqueeze(2)).view(M, P, P, 2, 2)
         y = y.permute(0, 1, 3, 2, 4).reshape(M, 2 * P, 2 * P) + b.view(-1, 1, 1)
         return torch.sigmoid(y)
+
+
+# cfg.FAST_RCNN.ROI_BOX_HEAD / cfg.MRCNN.ROI_MASK_HEAD names -> modules (the
+# reference resolves them with get_func, model_builder.py:33-49)
+BOX_HEADS = {"fast_rcnn_heads.roi_2mlp_head": Roi2MLPHead,
+             "fast_rcnn_heads.roi_Xconv1fc_gn_head": RoiXconv1fcGNHead}
+MASK_HEADS = {"mask_rcnn_heads.mask_rcnn_fcn_head_v1up4convs": (MaskHeadV1upXconvs, 4),
+              "mask_rcnn_heads.mask_rcnn_fcn_head_v1up": (MaskHeadV1upXconvs, 2),
+              "mask_rcnn_heads.mask_rcnn_fcn_head_v1up4convs_gn": (MaskHeadV1upXconvsGN, 4),
+              "mask_rcnn_heads.mask_rcnn_fcn_head_v1up_gn": (MaskHeadV1upXconvsGN, 2)}
 
 
 class Generalized_RCNN(nn.Module):
@@ -373,12 +587,15 @@ class Generalized_RCNN(nn.Module):
         self.num_roi_levels = cfg.FPN.ROI_MAX_LEVEL - cfg.FPN.ROI_MIN_LEVEL + 1
         roi_scales = self.Conv_Body.spatial_scale[-self.num_roi_levels:]
         self.roi_spatial_scale = roi_scales  # coarsest first, as the reference
-        self.Box_Head = Roi2MLPHead(self.Conv_Body.dim_out, self.roi_feature_transform,
-                                    roi_scales, cfg)
-        self.Box_Outs = FastRCNNOutputs(self.Box_Head.dim_out, cfg.MODEL.NUM_CLASSES)
-        self.Mask_Head = MaskHeadV1upXconvs(self.Conv_Body.dim_out, self.roi_feature_transform,
-                                            roi_scales, cfg)
-        self.Mask_Outs = MaskRCNNOutputs(self.Mask_Head.dim_out, cfg.MODEL.NUM_CLASSES)
+        self.Box_Head = BOX_HEADS[cfg.FAST_RCNN.ROI_BOX_HEAD](
+            self.Conv_Body.dim_out, self.roi_feature_transform, roi_scales, cfg)
+        self.Box_Outs = FastRCNNOutputs(self.Box_Head.dim_out, cfg.MODEL.NUM_CLASSES,
+                                        cfg.MODEL.CLS_AGNOSTIC_BBOX_REG)
+        mk, nconv = MASK_HEADS[cfg.MRCNN.ROI_MASK_HEAD]
+        self.Mask_Head = mk(self.Conv_Body.dim_out, self.roi_feature_transform, roi_scales, cfg,
+                            nconv)
+        self.Mask_Outs = MaskRCNNOutputs(
+            self.Mask_Head.dim_out, cfg.MODEL.NUM_CLASSES if cfg.MRCNN.CLS_SPECIFIC_MASK else 1)
         anchors = []
         k_min, k_max = cfg.FPN.RPN_MIN_LEVEL, cfg.FPN.RPN_MAX_LEVEL
         for lvl in range(k_min, k_max + 1):
@@ -432,9 +649,27 @@ class Generalized_RCNN(nn.Module):
     @torch.no_grad()
     def fold_affine(self, epilogue: bool = True):
         """Fold the frozen AffineChannel2d into conv weight + bias; with `epilogue`
-        the bias/residual/ReLU after each conv run as one vd_bias_act pass."""
-        body = self.Conv_Body.conv_body
-        stem = body.res1
+        the bias/residual/ReLU after each conv run as one vd_bias_act pass (GN
+        bodies: each GroupNorm + residual + ReLU as one vd_group_norm_act)."""
+        prepare_fpn_body(self.Conv_Body, epilogue)
+        self.RPN.fuse()
+        self.Box_Head.prepare()
+        self.Mask_Head.prepare()
+        return self
+
+
+@torch.no_grad()
+def prepare_fpn_body(fpn: FPNBody, epilogue: bool = True):
+    """Inference-time rewrite of an FPNBody: AffineChannel2d folded into the
+    convs (BN bodies) and the fused HIP epilogues switched on."""
+    body = fpn.conv_body
+    stem = body.res1
+    if body.use_gn:
+        body.res1 = _StemGN(stem.conv1, stem.gn1, stem.maxpool) if epilogue else stem
+        for i in range(2, body.convX + 1):
+            for blk in getattr(body, "res%d" % i):
+                blk.epilogue = epilogue
+    else:
         if epilogue:
             body.res1 = _StemEpilogue(_fold(stem.conv1, stem.bn1), stem.maxpool)
         else:
@@ -450,12 +685,10 @@ class Generalized_RCNN(nn.Module):
                     blk.fd = _fold(blk.downsample[0], blk.downsample[1])
                 blk.fused = True
                 blk.epilogue = epilogue
-        for m in self.Conv_Body.topdown_lateral_modules:
-            m.epilogue = epilogue
-        self.RPN.fuse()
-        self.Box_Head.prepare()
-        self.Mask_Head.prepare()
-        return self
+    for m in fpn.topdown_lateral_modules:
+        m.epilogue = epilogue
+    fpn.epilogue = epilogue
+    return fpn
 
 
 def generate_anchors(stride=16, sizes=(32, 64, 128, 256, 512), aspect_ratios=(0.5, 1, 2)):

@@ -457,3 +457,151 @@ def box_detections(rois, cls_prob, bbox_pred, roi_count, im_scale, im_hw, score_
                                   cls.data_ptr(), cnt.data_ptr(), ws.data_ptr(), ws.numel(),
                                   _stream()), "vd_box_detections")
     return dets, cls, cnt
+
+
+# --------------------------------------------------------------------------- #
+# VOS temporal path: FlowAlign, GroupNorm epilogues, ConvGRU gates             #
+# --------------------------------------------------------------------------- #
+def _fmt(x: torch.Tensor, name: str) -> int:
+    """Memory format of a 4-D fp32 device tensor as a vosdet layout code."""
+    if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 4:
+        raise ValueError("%s must be a 4-D float32 device tensor" % name)
+    if x.is_contiguous():
+        return _lib.VD_LAYOUT_NCHW
+    if x.is_contiguous(memory_format=torch.channels_last):
+        return _lib.VD_LAYOUT_NHWC
+    raise ValueError("%s must be contiguous (NCHW or channels_last)" % name)
+
+
+def _like(x: torch.Tensor, layout: int, name: str) -> torch.Tensor:
+    """x in the memory format `layout` (a copy only if it is not already)."""
+    want = torch.channels_last if layout == _lib.VD_LAYOUT_NHWC else torch.contiguous_format
+    if not x.is_cuda or x.dtype != torch.float32:
+        raise ValueError("%s must be a float32 device tensor" % name)
+    return x if x.is_contiguous(memory_format=want) else x.contiguous(memory_format=want)
+
+
+def _empty_as(x: torch.Tensor, layout: int, shape=None) -> torch.Tensor:
+    shape = tuple(x.shape) if shape is None else shape
+    fmt = torch.channels_last if layout == _lib.VD_LAYOUT_NHWC else torch.contiguous_format
+    return torch.empty(shape, dtype=torch.float32, device=x.device, memory_format=fmt)
+
+
+def flow_align(features: torch.Tensor, flow: torch.Tensor) -> torch.Tensor:
+    """FlowAlignFunction.forward (lib_vos/vos_model/flow_align/functions/flow_align.py:13-30):
+    features B x C x H x W (NCHW, or channels_last -> the NHWC kernel), flow
+    B x 2 x H x W at the feature resolution.  Output in the features' format."""
+    lay = _fmt(features, "features")
+    fl = _need(flow, "flow")
+    B, C, H, W = features.shape
+    if tuple(fl.shape) != (B, 2, H, W):
+        raise ValueError("flow must be B x 2 x H x W = %s, got %s" % ((B, 2, H, W),
+                                                                      tuple(fl.shape)))
+    out = _empty_as(features, lay)
+    check(lib().vd_flow_align_forward(features.data_ptr(), fl.data_ptr(), B, C, H, W, lay,
+                                      out.data_ptr(), _stream()), "vd_flow_align_forward")
+    return out
+
+
+def flow_align_backward(grad_out, features, flow):
+    g = _need(grad_out, "grad_out")
+    f = _need(features, "features")
+    fl = _need(flow, "flow")
+    B, C, H, W = f.shape
+    gf = torch.zeros_like(f)
+    gfl = torch.zeros((B, 2, H, W), dtype=torch.float32, device=f.device)
+    check(lib().vd_flow_align_backward(g.data_ptr(), f.data_ptr(), fl.data_ptr(), B, C, H, W,
+                                       gf.data_ptr(), gfl.data_ptr(), _stream()),
+          "vd_flow_align_backward")
+    return gf, gfl
+
+
+class FlowAlignFunction(torch.autograd.Function):
+    """functions/flow_align.py:7-45 (static autograd Function, as the reference).
+    CPU tensors raise like the reference's NotImplementedError branch (:28-29)."""
+
+    @staticmethod
+    def forward(ctx, features, flows):
+        if not features.is_cuda:
+            raise NotImplementedError
+        ctx.save_for_backward(features, flows)
+        return flow_align(features, flows)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        features, flows = ctx.saved_tensors
+        return flow_align_backward(grad_output, features, flows)
+
+
+_ACT = {None: 0, "none": 0, "relu": 1, "sigmoid": 2, "tanh": 3}
+
+
+def group_norm_act(x: torch.Tensor, num_groups: int, gamma: torch.Tensor, beta: torch.Tensor,
+                   eps: float = 1e-5, x2: Optional[torch.Tensor] = None, residual=None,
+                   residual_gn=None, upsample_residual: bool = False, act=None,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """act(GN(x [+ x2]) + residual) in one statistics + one apply pass
+    (vd_group_norm_act).  residual_gn = (gamma_r, beta_r) normalises the residual
+    with its own statistics (basic_gn_shortcut).  Works on NCHW or channels_last
+    tensors; the output keeps x's memory format.  out may be x (in place)."""
+    lay = _fmt(x, "x")
+    B, C, H, W = x.shape
+    if x2 is not None:
+        x2 = _like(x2, lay, "x2")
+    mode = 0
+    res = None
+    if residual is not None:
+        mode = 3 if residual_gn is not None else (2 if upsample_residual else 1)
+        want = (B, C, H // 2, W // 2) if mode == 2 else (B, C, H, W)
+        if tuple(residual.shape) != want:
+            raise ValueError("residual shape %s, expected %s" % (tuple(residual.shape), want))
+        res = _like(residual, lay, "residual")
+    if out is None:
+        out = _empty_as(x, lay)
+    rg, rb = residual_gn if residual_gn is not None else (None, None)
+    nws = lib().vd_group_norm_workspace_size(B, num_groups) * (2 if mode == 3 else 1)
+    ws = _ws(nws, x.device)
+    check(lib().vd_group_norm_act(
+        x.data_ptr(), x2.data_ptr() if x2 is not None else None, B, C, H, W, int(num_groups),
+        float(eps), gamma.data_ptr(), beta.data_ptr(), res.data_ptr() if res is not None else None,
+        mode, rg.data_ptr() if rg is not None else None, rb.data_ptr() if rb is not None else None,
+        _ACT[act], lay, out.data_ptr(), ws.data_ptr(), ws.numel(), _stream()),
+        "vd_group_norm_act")
+    return out
+
+
+def convgru_gates(zx, rx, h, zh, rh, num_groups, gamma_z, beta_z, gamma_r, beta_r, eps=1e-5):
+    """(z, h*r) of convgrucell.py:85-87 from the six convolution outputs; with
+    h None (zero state) returns (z, None)."""
+    lay = _fmt(zx, "zx")
+    B, C, H, W = zx.shape
+    z = _empty_as(zx, lay)
+    hr = _empty_as(zx, lay) if h is not None else None
+    ws = _ws(2 * lib().vd_group_norm_workspace_size(B, num_groups), zx.device)
+    ptr = lambda t: _like(t, lay, "t").data_ptr() if t is not None else None  # noqa: E731
+    check(lib().vd_convgru_gates(
+        ptr(zh), zx.data_ptr(), ptr(rh), ptr(rx), ptr(h), B, C, H, W, int(num_groups),
+        float(eps), gamma_z.data_ptr(), beta_z.data_ptr(), gamma_r.data_ptr(), beta_r.data_ptr(),
+        lay, z.data_ptr(), hr.data_ptr() if hr is not None else None, ws.data_ptr(), ws.numel(),
+        _stream()), "vd_convgru_gates")
+    return z, hr
+
+
+def convgru_update(hx, hh, z, h, num_groups, gamma_h, beta_h, finer=None, eps=1e-5,
+                   out: Optional[torch.Tensor] = None):
+    """hn = (1-z)*h + z*tanh(GN_h(hh + hx)) (convgrucell.py:88-91), fused with the
+    VOS fusion hn/2 + bilinear_0.5x(finer)/2 (vos_model_builder.py:341-342)."""
+    lay = _fmt(hx, "hx")
+    B, C, H, W = hx.shape
+    if finer is not None and tuple(finer.shape) != (B, C, 2 * H, 2 * W):
+        raise ValueError("finer level must be %s, got %s" % ((B, C, 2 * H, 2 * W),
+                                                             tuple(finer.shape)))
+    if out is None:
+        out = _empty_as(hx, lay)
+    ws = _ws(lib().vd_group_norm_workspace_size(B, num_groups), hx.device)
+    ptr = lambda t: _like(t, lay, "t").data_ptr() if t is not None else None  # noqa: E731
+    check(lib().vd_convgru_update(
+        ptr(hh), hx.data_ptr(), ptr(z), ptr(h), ptr(finer), B, C, H, W, int(num_groups),
+        float(eps), gamma_h.data_ptr(), beta_h.data_ptr(), lay, out.data_ptr(), ws.data_ptr(),
+        ws.numel(), _stream()), "vd_convgru_update")
+    return out

@@ -27,6 +27,9 @@ def synthetic_state_dict(model: torch.nn.Module, seed: int = 0) -> dict:
     sd = {}
     for name, p in model.state_dict().items():
         shape = tuple(p.shape)
+        if "conv_flow_downsample" in name:  # frozen, fixed by construction
+            sd[name] = p.detach().clone().cpu()
+            continue
         is_affine = name.endswith(".weight") and len(shape) == 1
         if is_affine:  # AffineChannel2d scale
             sd[name] = torch.ones(shape)
@@ -78,16 +81,20 @@ def calibrate(model, frame_u8: np.ndarray, device):
         if isinstance(m, AffineChannel2d):
             hooks.append(m.register_forward_pre_hook(affine_pre))
     body = model.Conv_Body
-    hooks.append(body.conv_top.register_forward_hook(unit_out()))
-    for t in body.topdown_lateral_modules:
-        hooks.append(t.conv_lateral.register_forward_hook(unit_out()))
-    for p in body.posthoc_modules:
-        hooks.append(p.register_forward_hook(unit_out()))
+    if not body.use_gn:  # GroupNorm FPN outputs are already unit-scale
+        hooks.append(body.conv_top.register_forward_hook(unit_out()))
+        for t in body.topdown_lateral_modules:
+            hooks.append(t.conv_lateral.register_forward_hook(unit_out()))
+        for p in body.posthoc_modules:
+            hooks.append(p.register_forward_hook(unit_out()))
     rpn = model.RPN
     hooks.append(rpn.FPN_RPN_conv.register_forward_hook(unit_out()))
     hooks.append(rpn.FPN_RPN_cls_score.register_forward_hook(unit_out(1.5, -1.5)))
     hooks.append(rpn.FPN_RPN_bbox_pred.register_forward_hook(unit_out(0.2)))
     feats = body(blob)
+    if hasattr(model, "temporal_fusion"):  # VOS: the RPN sees the ConvGRU-fused pyramid
+        feats = model.temporal_fusion(feats, fused=False)
+        model.clean_hidden_states()
     rpn.level_outputs(feats[-1])  # calibrate the shared RPN convs on P2
     for h in hooks:
         h.remove()
@@ -102,11 +109,15 @@ def calibrate(model, frame_u8: np.ndarray, device):
 
 def build_model(cfg, seed: int = 0, device="cuda", fold=True, channels_last=False,
                 calibrate_frame: np.ndarray | None = None):
-    """Generalized_RCNN with synthetic (calibrated) weights in eval mode.
-    Returns (model, state_dict) where state_dict has the reference's names and
-    the unfolded AffineChannel parameters (what the oracle pipeline loads)."""
+    """Generalized_RCNN (Generalized_VOS_RCNN for the VOS configs, i.e. when
+    cfg.CONVGRU is set and the config names a VOS model) with synthetic
+    (calibrated) weights in eval mode.  Returns (model, state_dict) where
+    state_dict has the reference's names and the unfolded AffineChannel
+    parameters (what the oracle pipelines load)."""
     from .modeling import Generalized_RCNN
-    m = Generalized_RCNN(cfg)
+    from .vos import Generalized_VOS_RCNN
+    vos = bool(cfg.get("VOS", False))
+    m = (Generalized_VOS_RCNN if vos else Generalized_RCNN)(cfg)
     sd = synthetic_state_dict(m, seed)
     missing, unexpected = m.load_state_dict(sd, strict=False)
     assert not unexpected, unexpected
@@ -115,7 +126,8 @@ def build_model(cfg, seed: int = 0, device="cuda", fold=True, channels_last=Fals
     for p in m.parameters():
         p.requires_grad_(False)
     if calibrate_frame is None:
-        calibrate_frame = np.random.RandomState(0).randint(0, 256, (800, 1333, 3), np.uint8)
+        hw = (480, 854) if vos else (800, 1333)
+        calibrate_frame = np.random.RandomState(0).randint(0, 256, hw + (3,), np.uint8)
     calibrate(m, calibrate_frame, device)
     sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
     if fold:
@@ -124,4 +136,6 @@ def build_model(cfg, seed: int = 0, device="cuda", fold=True, channels_last=Fals
         m.Conv_Body.to(memory_format=torch.channels_last)
         m.RPN.to(memory_format=torch.channels_last)
         m.Mask_Head.conv_fcn.to(memory_format=torch.channels_last)
+        if vos:
+            m.ConvGRUs.to(memory_format=torch.channels_last)
     return m, sd
