@@ -157,15 +157,24 @@ def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=Non
             "algorithmic_bytes_per_launch": int(nbytes), "avg_launch_us": round(t * 1e6, 2)}
 
 
-def cpu_baseline(cfg_name, sd, n_frames=2, threads=None):
-    """The reference's CPU path (oracle/pipeline.py) on a bounded sample."""
+def cpu_baseline(cfg_name, sd, n_frames=2, threads=None, cfg=None):
+    """The reference's CPU path (oracle/pipeline.py, oracle/vos_pipeline.py) on a
+    bounded sample."""
     from oracle.pipeline import RefCPUPipeline
     threads = threads or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    blocks = {"e2e_mask_rcnn_R-50-FPN_1x": (3, 4, 6, 3),
-              "e2e_mask_rcnn_R-101-FPN_2x": (3, 4, 23, 3)}[cfg_name]
-    ref = RefCPUPipeline(sd, block_counts=blocks)
-    fr = synthetic_frames(n_frames + 1, 1000)
+    if cfg is not None and cfg.get("VOS", False):
+        from oracle.vos_pipeline import RefCPUVOSPipeline
+        ref = RefCPUVOSPipeline(sd, dynamic=cfg.CONVGRU.DYNAMIC_MODEL,
+                                num_classes=cfg.MODEL.NUM_CLASSES, max_size=cfg.TEST.MAX_SIZE)
+        fr = synthetic_frames(n_frames + 1, 1000, 480, 854)
+        what = "DAVIS-shaped 480x854 frames of one sequence, Generalized_VOS_RCNN"
+    else:
+        blocks = {"e2e_mask_rcnn_R-50-FPN_1x": (3, 4, 6, 3),
+                  "e2e_mask_rcnn_R-101-FPN_2x": (3, 4, 23, 3)}[cfg_name]
+        ref = RefCPUPipeline(sd, block_counts=blocks)
+        fr = synthetic_frames(n_frames + 1, 1000)
+        what = "800x1333 frames"
     ref(fr[0])  # warm-up
     t0 = time.perf_counter()
     for i in range(n_frames):
@@ -173,9 +182,9 @@ def cpu_baseline(cfg_name, sd, n_frames=2, threads=None):
     dt = time.perf_counter() - t0
     return {"value": round(n_frames / dt, 4), "unit": "frames/s", "cores": threads,
             "kind": "port",
-            "sample": "%d synthetic 800x1333 frames, full im_detect_all path (torch-CPU convs, "
+            "sample": "%d synthetic %s, full im_detect_all path (torch-CPU convs, "
                       "oracle C RoIAlign/NMS, numpy proposals), %.1f s, cpu=%s" % (
-                          n_frames, dt, platform.processor() or platform.machine())}
+                          n_frames, what, dt, platform.processor() or platform.machine())}
 
 
 def main():
@@ -189,6 +198,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--seq-len", type=int, default=50,
+                    help="VOS configs: frames per synthetic sequence (hidden states reset)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -207,17 +218,35 @@ def main():
     from vosdetectron_amd.weights import build_model
 
     cfg = vcfg.get(args.config)
+    vos = bool(cfg.get("VOS", False))
     model, sd = build_model(cfg, seed=0, device=dev, channels_last=args.layout == "nhwc")
-    pipe = FramePipeline(model, cfg, batch=args.batch, channels_last=args.layout == "nhwc",
-                         device=dev)
     F = args.batch
-    frames = torch.from_numpy(synthetic_frames(F, 1 + rank * F)).to(dev)
+    if vos:
+        # configs[3]: DAVIS-shaped 480p sequences; batch row b = sequence b of
+        # this rank (sequences shard across ranks), a step = the
+        # next frame of every sequence, hidden states reset every --seq-len steps
+        from vosdetectron_amd.engine import VOSPipeline
+        fh, fw = 480, 854
+        pipe = VOSPipeline(model, cfg, frame_hw=(fh, fw), batch=F,
+                           channels_last=args.layout == "nhwc", device=dev)
+        ring = [torch.from_numpy(synthetic_frames(F, 1 + rank * F + 7919 * t, fh, fw)).to(dev)
+                for t in range(4)]
+    else:
+        pipe = FramePipeline(model, cfg, batch=F, channels_last=args.layout == "nhwc",
+                             device=dev)
+        ring = [torch.from_numpy(synthetic_frames(F, 1 + rank * F)).to(dev)]
+    frames = ring[0]
+    step_no = [0]
 
     from vosdetectron_amd.runner import ResultGatherer
     gatherer = ResultGatherer(F, pipe.det_cap, cfg.MRCNN.RESOLUTION, world, dev)
 
     def step():
-        out = pipe.run(frames)
+        t = step_no[0]
+        step_no[0] += 1
+        if vos and t % args.seq_len == 0:
+            pipe.reset()
+        out = pipe.run(ring[t % len(ring)])
         if world > 1:  # one all_gather per result tensor over RCCL (runner.py)
             gatherer.gather(out["dets"], out["classes"], out["counts"], out["masks"],
                             out["counts_host"])
@@ -248,7 +277,7 @@ def main():
         roof = measure_roialign_roofline(dev)
     cpu = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:
-        cpu = cpu_baseline(args.config, sd, args.cpu_frames)
+        cpu = cpu_baseline(args.config, sd, args.cpu_frames, cfg=cfg)
 
     if rank == 0:
         fps = world * F * args.steps / dt
@@ -260,9 +289,13 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (u8 800x1333 frames, RandomState seeds; deterministic "
                     "N(0,1/fan_in) weights)",
-            "config": {"workload": "%s inference, %d synthetic 800x1333 frames per GPU per step, "
-                                   "full im_detect_all path (proposals, box head, class NMS, "
-                                   "mask head)" % (args.config, F),
+            "config": {"workload": (
+                "%s inference, %d DAVIS-shaped 480x854 synthetic sequences per GPU (one frame "
+                "of each per step, ConvGRU hidden states carried, reset every %d frames), full "
+                "vos im_detect_all path" % (args.config, F, args.seq_len)) if vos else (
+                "%s inference, %d synthetic 800x1333 frames per GPU per step, full "
+                "im_detect_all path (proposals, box head, class NMS, mask head)"
+                % (args.config, F)),
                        "frames_per_gpu_step": F, "global_batch": world * F,
                        "parallelism": "frame-sharded dp%d + RCCL all_gather" % world,
                        "layout": args.layout, "dets_per_frame": dets_per_frame},
