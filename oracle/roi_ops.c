@@ -368,8 +368,10 @@ int or_nms(const float *dets, int n, int stride, float thresh, int64_t *keep) {
 
 /* ------------------------------------------------------------------------ */
 /* FlowAlign forward: lib_vos/vos_model/flow_align/src/flow_align_cuda_kernel.cu
- * :15-55, grid-stride loop walked serially.  The `1.` literals promote each
- * tap product and the sum to double before the float store (:46-49). */
+ * :15-55, grid-stride loop walked serially.  The tap expression (:46-49) is
+ * kept verbatim: C's usual conversions make the first two terms double, the
+ * third a float product promoted by (1. - w_ratio), the fourth all-float; the
+ * sum is double, stored as float. */
 void or_flow_align_fwd(const float *bottom, const float *flow, int batches, int channels,
                        int height, int width, float *top) {
     const long nthreads = (long)batches * channels * height * width;

@@ -13,8 +13,9 @@
 //                vos_model_builder.py:335-345 (blob/2 + bilinear-0.5x(finer)/2).
 //
 // FlowAlign keeps the reference's arithmetic exactly: float position, float
-// ratios, and the `1.` double literals that promote each tap product and the sum
-// to double before the float store -- bit-identical to the C restatement.
+// ratios, and the reference's mixed float/double tap expression (the `1.`
+// literals promote some products to double, others stay float) -- bit-identical
+// to the C restatement, which compiles the same expression text.
 // GroupNorm statistics are accumulated in double (sum, sum of squares) and the
 // normalisation runs in fp32; it matches torch's fp32 GroupNorm to rounding.
 #include "common.hpp"
@@ -53,10 +54,13 @@ __device__ __forceinline__ FlowTap flow_tap(const float *flow, int n, int h, int
     return t;
 }
 
+// The reference expression verbatim (flow_align_cuda_kernel.cu:46-49): C's
+// usual conversions make f1, f2 terms double, f3 * hr a float product promoted
+// by (1. - wr), and f4 * hr * wr an all-float product -- summed in double.
 __device__ __forceinline__ float flow_blend(float f1, float f2, float f3, float f4, float hr,
                                             float wr) {
-    return (float)((double)f1 * (1. - hr) * (1. - wr) + (double)f2 * (1. - hr) * (wr) +
-                   (double)f3 * (hr) * (1. - wr) + (double)f4 * (hr) * (wr));
+    return (float)(f1 * (1. - hr) * (1. - wr) + f2 * (1. - hr) * (wr) + f3 * (hr) * (1. - wr) +
+                   f4 * (hr) * (wr));
 }
 
 // Reference decomposition (NCHW, one lane per output element).
@@ -127,7 +131,7 @@ __global__ __launch_bounds__(256) void flow_align_bwd_nchw_kernel(
         const FlowTap t = flow_tap(flow, n, h, w, H, W);
         if (!t.ok) continue;
         const int64_t HW = (int64_t)H * W;
-        const double hr = t.hr, wr = t.wr;
+        const float hr = t.hr, wr = t.wr;  // float, as the reference (promotions matter)
         const float g = top_diff[i];
         float *bd = feat_diff + nc * HW + t.off;
         atomicAdd(bd, (float)(g * (1. - hr) * (1. - wr)));
@@ -173,8 +177,10 @@ int launch_flow_align_bwd(const float *top_diff, const float *feat, const float 
 // Statistics: ws[set][n][g] = {sum, sum of squares} (double) of x (+ x2) over
 // the group's C/G channels x H*W pixels.  Up to 3 independent tensors per
 // launch (blockIdx.z = set): the ConvGRU's update and reset gates share one.
-// NHWC, C % 4 == 0 and (C / G) % 4 == 0.  Thread t owns channel quad
-// t % C4 of pixels t / C4, t / C4 + ppi, ...
+// NHWC, C % 4 == 0, C <= 1024, G <= 64.  Thread t owns channel quad t % C4 of
+// pixels t / C4, t / C4 + ppi, ...; the four lanes of its quad are summed
+// separately and folded into their groups at the end, so any C / G works
+// (the GN ResNet's 64-channel stages have 2 channels per group).
 __global__ __launch_bounds__(256) void gn_stats_nhwc_kernel(GnSets sets, int HW, int C, int G,
                                                             int pix_per_block) {
     __shared__ double red[2][64];  // per group (G <= 64)
@@ -182,29 +188,41 @@ __global__ __launch_bounds__(256) void gn_stats_nhwc_kernel(GnSets sets, int HW,
     const int n = blockIdx.y;
     const int C4 = C >> 2;
     const int cg = C / G;
-    for (int i = threadIdx.x; i < 2 * G; i += blockDim.x) red[i / G][i % G] = 0.0;
+    for (int i = threadIdx.x; i < 2 * 64; i += blockDim.x) red[i / 64][i % 64] = 0.0;
     __syncthreads();
-    const int q = threadIdx.x % C4;
-    const int ppi = blockDim.x / C4;  // pixels per block iteration
     const int p0 = blockIdx.x * pix_per_block;
     const int p1 = min(p0 + pix_per_block, HW);
-    double s = 0.0, ss = 0.0;
-    if ((int)threadIdx.x < ppi * C4) {
-        const float4 *x = reinterpret_cast<const float4 *>(st.x) + (int64_t)n * HW * C4;
-        const float4 *x2 = st.x2 ? reinterpret_cast<const float4 *>(st.x2) + (int64_t)n * HW * C4
-                                 : nullptr;
-        for (int p = p0 + (int)threadIdx.x / C4; p < p1; p += ppi) {
+    const float4 *x = reinterpret_cast<const float4 *>(st.x) + (int64_t)n * HW * C4;
+    const float4 *x2 =
+        st.x2 ? reinterpret_cast<const float4 *>(st.x2) + (int64_t)n * HW * C4 : nullptr;
+    for (int q0 = 0; q0 < C4; q0 += blockDim.x) {  // C4 > 256: several quad blocks
+        const int nq = min(C4 - q0, (int)blockDim.x);
+        const int ppi = blockDim.x / nq;  // pixels per block iteration
+        const int q = q0 + (int)threadIdx.x % nq;
+        if ((int)threadIdx.x >= ppi * nq) continue;
+        double s[4] = {0, 0, 0, 0}, ss[4] = {0, 0, 0, 0};
+        for (int p = p0 + (int)threadIdx.x / nq; p < p1; p += ppi) {
             float4 v = x[(int64_t)p * C4 + q];
             if (x2) {
                 const float4 u = x2[(int64_t)p * C4 + q];
                 v.x = v.x + u.x; v.y = v.y + u.y; v.z = v.z + u.z; v.w = v.w + u.w;
             }
-            s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
-            ss += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+            s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
+            ss[0] += (double)v.x * v.x; ss[1] += (double)v.y * v.y;
+            ss[2] += (double)v.z * v.z; ss[3] += (double)v.w * v.w;
         }
-        const int g = (q * 4) / cg;
-        atomicAdd(&red[0][g], s);
-        atomicAdd(&red[1][g], ss);
+        if (cg % 4 == 0) {
+            const int g = (q * 4) / cg;
+            atomicAdd(&red[0][g], (s[0] + s[1]) + (s[2] + s[3]));
+            atomicAdd(&red[1][g], (ss[0] + ss[1]) + (ss[2] + ss[3]));
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int g = (q * 4 + k) / cg;
+                atomicAdd(&red[0][g], s[k]);
+                atomicAdd(&red[1][g], ss[k]);
+            }
+        }
     }
     __syncthreads();
     for (int g = threadIdx.x; g < G; g += blockDim.x) {
@@ -364,10 +382,10 @@ int launch_gn_stats(const GnSets &sets, int nsets, int B, int C, int HW, int G, 
     for (int k = 0; k < nsets; ++k)
         if (hipMemsetAsync(sets.s[k].ws, 0, (size_t)B * G * 2 * sizeof(double), s) != hipSuccess)
             return VD_ERR_LAUNCH;
-    if (nhwc && C % 4 == 0 && (C / G) % 4 == 0 && C / 4 <= 256 && G <= 64) {
+    if (nhwc && C % 4 == 0 && G <= 64) {
         const int C4 = C / 4;
-        const int ppi = 256 / C4;
-        int ppb = ppi * 32;  // 32 iterations per thread
+        const int ppi = C4 >= 256 ? 1 : 256 / C4;
+        const int ppb = ppi * 32;  // 32 iterations per thread
         const dim3 grid((HW + ppb - 1) / ppb, B, nsets);
         hipLaunchKernelGGL(gn_stats_nhwc_kernel, grid, dim3(256), 0, s, sets, HW, C, G, ppb);
     } else if (!nhwc) {
