@@ -374,6 +374,132 @@ __global__ __launch_bounds__(256) void gn_apply_nchw_kernel(GnApply a, int B, in
     }
 }
 
+
+// NHWC, C % 4 == 0 (product path): one image per blockIdx.y, the per-channel
+// mean / rstd of that image staged in LDS once per block (instead of being
+// rebuilt from the double sums per element), one float4 = 4 channels per
+// thread step.  Same arithmetic per element as gn_apply_one.
+__device__ __forceinline__ float gn_act_(float v, int act) {
+    if (act == 1) return fmaxf(v, 0.f);
+    if (act == 2) return sigmoidf_(v);
+    if (act == 3) return tanhf(v);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void gn_apply_nhwc4_kernel(GnApply a, int H, int W, int C, int G,
+                                                             int pix_per_block) {
+    extern __shared__ float cst[];  // [4][C]: mean, rstd, residual mean, residual rstd
+    const int n = blockIdx.y;
+    const int cg = C / G;
+    const int HW = H * W;
+    const double count = (double)cg * HW;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        const float2 mr = gn_consts(a.ws, n, G, c / cg, count, a.eps);
+        cst[c] = mr.x;
+        cst[C + c] = mr.y;
+        if (a.res_mode == 3) {
+            const float2 rm = gn_consts(a.res_ws, n, G, c / cg, count, a.eps);
+            cst[2 * C + c] = rm.x;
+            cst[3 * C + c] = rm.y;
+        }
+    }
+    __syncthreads();
+    const int C4 = C >> 2;
+    const int p0 = blockIdx.x * pix_per_block;
+    const int p1 = min(p0 + pix_per_block, HW);
+    const int64_t img4 = (int64_t)n * HW * C4;
+    const float4 *x4 = reinterpret_cast<const float4 *>(a.x);
+    const float4 *x24 = reinterpret_cast<const float4 *>(a.x2);
+    const float4 *r4 = reinterpret_cast<const float4 *>(a.res);
+    const float4 *z4 = reinterpret_cast<const float4 *>(a.z);
+    const float4 *g4 = reinterpret_cast<const float4 *>(a.gamma);
+    const float4 *b4 = reinterpret_cast<const float4 *>(a.beta);
+    float4 *o4 = reinterpret_cast<float4 *>(a.out);
+    for (int64_t e = (int64_t)p0 * C4 + threadIdx.x; e < (int64_t)p1 * C4; e += blockDim.x) {
+        const int q = (int)(e % C4);
+        const int p = (int)(e / C4);
+        const int c = q * 4;
+        const int64_t i4 = img4 + e;
+        float v[4], y[4];
+        {
+            float4 t = x4[i4];
+            if (a.x2) {
+                const float4 u = x24[i4];
+                t.x = t.x + u.x; t.y = t.y + u.y; t.z = t.z + u.z; t.w = t.w + u.w;
+            }
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        }
+        const float4 gg = g4[q], bb = b4[q];
+        const float gk[4] = {gg.x, gg.y, gg.z, gg.w}, bk[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            y[k] = (v[k] - cst[c + k]) * cst[C + c + k] * gk[k] + bk[k];
+        if (a.mode == VD_GN_ACT) {
+            if (a.res_mode) {
+                int64_t j4 = i4;
+                if (a.res_mode == 2) {
+                    const int h = p / W, w = p - (p / W) * W;
+                    j4 = (((int64_t)n * (H / 2) + h / 2) * (W / 2) + w / 2) * C4 + q;
+                }
+                const float4 rt = r4[j4];
+                float rv[4] = {rt.x, rt.y, rt.z, rt.w};
+                if (a.res_mode == 3) {
+                    const float4 rg = reinterpret_cast<const float4 *>(a.res_gamma)[q];
+                    const float4 rb = reinterpret_cast<const float4 *>(a.res_beta)[q];
+                    const float rgk[4] = {rg.x, rg.y, rg.z, rg.w}, rbk[4] = {rb.x, rb.y, rb.z, rb.w};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        rv[k] = (rv[k] - cst[2 * C + c + k]) * cst[3 * C + c + k] * rgk[k] + rbk[k];
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) y[k] = y[k] + rv[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) y[k] = gn_act_(y[k], a.act);
+        } else if (a.mode == VD_GN_GRU_Z) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) y[k] = sigmoidf_(y[k]);
+        } else if (a.mode == VD_GN_GRU_R) {
+            const float4 ht = a.res ? r4[i4] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float hk[4] = {ht.x, ht.y, ht.z, ht.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) y[k] = a.res ? hk[k] * sigmoidf_(y[k]) : 0.f;
+        } else {  // VD_GN_GRU_H
+            const float4 zt = z4[i4];
+            const float zk[4] = {zt.x, zt.y, zt.z, zt.w};
+            float hk[4] = {0.f, 0.f, 0.f, 0.f};
+            if (a.res) {
+                const float4 ht = r4[i4];
+                hk[0] = ht.x; hk[1] = ht.y; hk[2] = ht.z; hk[3] = ht.w;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float hh = tanhf(y[k]);
+                y[k] = a.res ? (1.f - zk[k]) * hk[k] + zk[k] * hh : zk[k] * hh;
+            }
+            if (a.finer) {
+                const int h = p / W, w = p - (p / W) * W;
+                const int W2 = 2 * W, H2 = 2 * H;
+                const float4 *f4 = reinterpret_cast<const float4 *>(a.finer);
+                const int64_t b0 = (((int64_t)n * H2 + 2 * h) * W2 + 2 * w) * C4 + q;
+                const float4 t00 = f4[b0], t01 = f4[b0 + C4];
+                const float4 t10 = f4[b0 + (int64_t)W2 * C4], t11 = f4[b0 + (int64_t)W2 * C4 + C4];
+                const float f00[4] = {t00.x, t00.y, t00.z, t00.w},
+                            f01[4] = {t01.x, t01.y, t01.z, t01.w},
+                            f10[4] = {t10.x, t10.y, t10.z, t10.w},
+                            f11[4] = {t11.x, t11.y, t11.z, t11.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float down = 0.5f * (0.5f * f00[k] + 0.5f * f01[k]) +
+                                       0.5f * (0.5f * f10[k] + 0.5f * f11[k]);
+                    y[k] = y[k] / 2.0f + down / 2.0f;
+                }
+            }
+        }
+        o4[i4] = make_float4(y[0], y[1], y[2], y[3]);
+    }
+}
+
 size_t gn_workspace_bytes(int B, int G, int sets) { return (size_t)sets * B * G * 2 * sizeof(double); }
 
 int launch_gn_stats(const GnSets &sets, int nsets, int B, int C, int HW, int G, int nhwc,
@@ -403,7 +529,12 @@ int launch_gn_apply(const GnApply &a, int B, int C, int H, int W, int G, int nhw
                     hipStream_t s) {
     const int64_t n = (int64_t)B * C * H * W;
     if (n == 0) return VD_OK;
-    if (nhwc)
+    if (nhwc && C % 4 == 0) {
+        const int ppb = max(1, 4096 / (C / 4));  // ~16 float4 per thread
+        const dim3 grid((H * W + ppb - 1) / ppb, B);
+        hipLaunchKernelGGL(gn_apply_nhwc4_kernel, grid, dim3(256), (size_t)4 * C * sizeof(float),
+                           s, a, H, W, C, G, ppb);
+    } else if (nhwc)
         hipLaunchKernelGGL(gn_apply_nhwc_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, a, B, H,
                            W, C, G);
     else

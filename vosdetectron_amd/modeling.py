@@ -488,8 +488,10 @@ class MaskHeadV1upXconvs(nn.Module):
         M, P, _, C = x_nhwc.shape
         x = self._convs_nhwc(x_nhwc.permute(0, 3, 1, 2))  # NCHW view, channels_last
         x = x.permute(0, 2, 3, 1).reshape(M * P * P, -1)
-        y = torch.addmm(self.up_b, x, self.up_w)
-        return F.relu_(y).view(M, P, P, 2, 2, -1)
+        # bias + ReLU in the GEMM epilogue (hipBLASLt) instead of a separate pass
+        # over the (M*P*P x 4C) upconv output
+        y = torch._addmm_activation(self.up_b, x, self.up_w)
+        return y.view(M, P, P, 2, 2, -1)
 
     def _convs_nhwc(self, x):
         for m in self.conv_fcn:
