@@ -372,7 +372,12 @@ __device__ __forceinline__ float4 combine_column(const RowTaps<SR> &t, const Tap
 
 // PF: while the bins consume column x, the taps of column x+1 (the next one the
 // left-to-right sweep needs unless it skips) are already in flight.
-template <int SR, bool FMA, bool PF>
+typedef float vf4 __attribute__((ext_vector_type(4)));
+
+// NT: output rows are written once and never re-read by this launch; storing
+// them non-temporal keeps them from evicting pyramid lines that overlapping
+// RoIs on the same XCD are about to re-read from L2.
+template <int SR, bool FMA, bool PF, bool NT = false>
 __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
     FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
     const int *__restrict__ roi_order, int P, int out_nhwc, float *__restrict__ out) {
@@ -438,7 +443,13 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
             acc = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
             if (!active) continue;
             if (out_nhwc) {
-                *reinterpret_cast<float4 *>(out + (((int64_t)r * P + ph) * P + pw) * C + c0) = acc;
+                float *dst = out + (((int64_t)r * P + ph) * P + pw) * C + c0;
+                if (NT) {
+                    vf4 v = {acc.x, acc.y, acc.z, acc.w};
+                    __builtin_nontemporal_store(v, reinterpret_cast<vf4 *>(dst));
+                } else {
+                    *reinterpret_cast<float4 *>(dst) = acc;
+                }
             } else {
                 float *t = tile + (int64_t)c0 * P * P + ph * P + pw;
                 t[0] = acc.x;
@@ -1139,11 +1150,11 @@ static int roialign_variant() {  // read per launch so tests can switch kernels
     return e ? atoi(e) : 8;
 }
 
-template <int SR, bool FMA, bool PF>
+template <int SR, bool FMA, bool PF, bool NT = false>
 static void launch_sep_t(const FpnLevels &fa, int C, const float *rois, const int *lvl,
                          const int *order, int R, int P, int out_nhwc, float *out, hipStream_t s,
                          int waves, size_t lds) {
-    hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_kernel<SR, FMA, PF>), dim3(R), dim3(64 * waves),
+    hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_kernel<SR, FMA, PF, NT>), dim3(R), dim3(64 * waves),
                        lds, s, fa, C, rois, lvl, order, P, out_nhwc, out);
 }
 
@@ -1161,9 +1172,15 @@ static int launch_sep(const FpnLevels &fa, int C, const float *rois, const int *
         launch_sep_t<2, true, false>(fa, C, rois, lvl, order, R, P, out_nhwc, out, s, waves, lds);
     else if (v == 14)
         launch_sep_t<2, true, true>(fa, C, rois, lvl, order, R, P, out_nhwc, out, s, waves, lds);
-    else
+    else if (v == 20)  // plain (write-back) output stores: 306 us vs 297 us with NT
         launch_sep_t<2, false, false>(fa, C, rois, lvl, order, R, P, out_nhwc, out, s, waves,
-                                         lds);
+                                      lds);
+    else if (v == 22)
+        launch_sep_t<2, true, false, true>(fa, C, rois, lvl, order, R, P, out_nhwc, out, s, waves,
+                                           lds);
+    else  // product default (variant 8): non-temporal output stores
+        launch_sep_t<2, false, false, true>(fa, C, rois, lvl, order, R, P, out_nhwc, out, s, waves,
+                                            lds);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
