@@ -171,10 +171,18 @@ def cpu_baseline(cfg_name, sd, n_frames=2, threads=None, cfg=None):
                                 num_classes=cfg.MODEL.NUM_CLASSES, max_size=cfg.TEST.MAX_SIZE)
         fr = synthetic_frames(n_frames + 1, 1000, 480, 854)
         what = "DAVIS-shaped 480x854 frames of one sequence, Generalized_VOS_RCNN"
+    elif not cfg.FPN.FPN_ON:
+        from oracle.pipeline import RefCPUPipelineC4
+        from vosdetectron_amd.c4 import _conv4_counts
+        ref = RefCPUPipelineC4(sd, block_counts=_conv4_counts(cfg.MODEL.CONV_BODY),
+                               groups=cfg.RESNETS.NUM_GROUPS,
+                               post_nms=cfg.TEST.RPN_POST_NMS_TOP_N)
+        fr = synthetic_frames(n_frames + 1, 1000)
+        what = "800x1333 frames, C4 (res5 head on every proposal)"
     else:
-        blocks = {"e2e_mask_rcnn_R-50-FPN_1x": (3, 4, 6, 3),
-                  "e2e_mask_rcnn_R-101-FPN_2x": (3, 4, 23, 3)}[cfg_name]
-        ref = RefCPUPipeline(sd, block_counts=blocks)
+        from vosdetectron_amd.modeling import _stage_counts
+        ref = RefCPUPipeline(sd, block_counts=_stage_counts(cfg.MODEL.CONV_BODY),
+                             groups=cfg.RESNETS.NUM_GROUPS)
         fr = synthetic_frames(n_frames + 1, 1000)
         what = "800x1333 frames"
     ref(fr[0])  # warm-up
@@ -233,6 +241,11 @@ def main():
                            channels_last=args.layout == "nhwc", device=dev)
         ring = [torch.from_numpy(synthetic_frames(F, 1 + rank * F + 7919 * t, fh, fw)).to(dev)
                 for t in range(4)]
+    elif not cfg.FPN.FPN_ON:  # configs[0]: the C4 single-scale family
+        from vosdetectron_amd.c4 import C4FramePipeline
+        pipe = C4FramePipeline(model, cfg, batch=F, channels_last=args.layout == "nhwc",
+                               device=dev)
+        ring = [torch.from_numpy(synthetic_frames(F, 1 + rank * F)).to(dev)]
     else:
         pipe = FramePipeline(model, cfg, batch=F, channels_last=args.layout == "nhwc",
                              device=dev)

@@ -133,3 +133,94 @@ class RefCPUPipeline:
         masks = m[np.arange(len(classes)), classes]
         extra.update(mask_rois=mrois, mask_feat=mf)
         return sc, bx, classes, masks, extra
+
+
+class RefCPUPipelineC4(RefCPUPipeline):
+    """The reference's CPU im_detect_all for e2e_mask_rcnn_R-50-C4 (no FPN):
+    ResNet50_conv4_body (ResNet.py:17-116) -> single_scale_rpn_outputs
+    (rpn_heads.py:37-126) -> GenerateProposalsOp (15 anchors, pre/post
+    6000/1000) -> roi_feature_transform single blob (model_builder.py:304-322,
+    RoIAlign 14x14, adaptive sr 0) -> ResNet_roi_conv5_head (res5, avgpool 7) ->
+    fast_rcnn_outputs -> box_results_with_nms_and_limit -> mask RoIAlign 14x14
+    -> shared res5 -> upconv5 + ReLU (mask_rcnn_fcn_head_v0upshare,
+    mask_rcnn_heads.py:263-331) -> sigmoid (R x 81 x 14 x 14)."""
+
+    def __init__(self, sd, block_counts=(3, 4, 6), pre_nms=6000, post_nms=1000,
+                 test_scale=800, **kw):
+        self.test_scale = test_scale  # TEST.SCALE (frames must be at identity scale)
+        kw.setdefault("box_res", 14)
+        kw.setdefault("box_sr", 0)
+        kw.setdefault("mask_res", 14)
+        kw.setdefault("mask_sr", 0)
+        super().__init__(sd, block_counts=block_counts, pre_nms=pre_nms, post_nms=post_nms,
+                         **kw)
+        self.anchors = orc.generate_anchors(16, (32, 64, 128, 256, 512), (0.5, 1, 2))
+
+    def _block(self, x, p, stride):
+        o = F.relu(self._aff(self._conv(x, p + "conv1", stride, bias=False), p + "bn1"))
+        o = F.relu(self._aff(self._conv(o, p + "conv2", 1, 1, groups=self.groups, bias=False),
+                             p + "bn2"))
+        o = self._aff(self._conv(o, p + "conv3", bias=False), p + "bn3")
+        if (p + "downsample.0.weight") in self.sd:
+            r = self._aff(self._conv(x, p + "downsample.0", stride, bias=False),
+                          p + "downsample.1")
+        else:
+            r = x
+        return F.relu(o + r)
+
+    def backbone(self, blob):
+        pre = "Conv_Body."
+        x = self._conv(blob, pre + "res1.conv1", 2, 3, bias=False)
+        x = F.relu(self._aff(x, pre + "res1.bn1"))
+        x = F.max_pool2d(x, 3, 2, 1)
+        for si, n in enumerate(self.block_counts):
+            for b in range(n):
+                x = self._block(x, pre + "res%d.%d." % (si + 2, b),
+                                2 if (b == 0 and si > 0) else 1)
+        return x  # res4, 1/16
+
+    def res5(self, x):
+        for b in range(3):
+            x = self._block(x, "Box_Head.res5.%d." % b, 2 if b == 0 else 1)
+        return x
+
+    @torch.no_grad()
+    def __call__(self, im_u8):
+        """im_u8: H x W x 3 uint8 BGR.  Returns (scores, boxes, classes, masks, extra)."""
+        blob, im_scale, im_info = orc.get_image_blob(im_u8, self.test_scale,
+                                                     stride=1)  # no FPN padding
+        res4 = self.backbone(torch.from_numpy(blob))
+        h = F.relu(self._conv(res4, "RPN.RPN_conv", 1, 1))
+        cls = torch.sigmoid(self._conv(h, "RPN.RPN_cls_score")).numpy()
+        dl = self._conv(h, "RPN.RPN_bbox_pred").numpy()
+        rois, _ = orc.generate_proposals(self.anchors, 1. / 16, cls, dl, im_info, self.pre_nms,
+                                         self.post_nms, self.rpn_nms, 0)
+        extra = {"probs": cls, "deltas": dl, "rois": rois}
+        feat = res4.numpy()
+        bf = orc.roi_align(feat, rois, self.box_res, self.box_res, 1. / 16, self.box_sr)
+        x = F.avg_pool2d(self.res5(torch.from_numpy(bf)), 7).flatten(1)
+        scores = F.softmax(F.linear(x, self.sd["Box_Outs.cls_score.weight"],
+                                    self.sd["Box_Outs.cls_score.bias"]), dim=1).numpy()
+        deltas = F.linear(x, self.sd["Box_Outs.bbox_pred.weight"],
+                          self.sd["Box_Outs.bbox_pred.bias"]).numpy()
+        boxes = rois[:, 1:5] / im_scale
+        pred = orc.bbox_transform(boxes, deltas, (10., 10., 5., 5.))
+        pred = orc.clip_tiled_boxes(pred, im_u8.shape)
+        sc, bx, cls_boxes = orc.box_results_with_nms_and_limit(
+            scores, pred, self.K, self.score_thresh, self.test_nms, self.dets_per_im)
+        classes = np.concatenate([[j] * len(cls_boxes[j]) for j in range(1, self.K)] +
+                                 [np.zeros((0,))]).astype(np.int32)
+        extra.update(scores_all=scores, deltas_all=deltas, box_feat=bf)
+        R = self.mask_res
+        if bx.shape[0] == 0:
+            return sc, bx, classes, np.zeros((0, R, R), np.float32), extra
+        mrois = np.hstack([np.zeros((bx.shape[0], 1)), bx.astype(np.float64) * im_scale])
+        mrois = mrois.astype(np.float32)
+        mf = orc.roi_align(feat, mrois, self.mask_res, self.mask_res, 1. / 16, self.mask_sr)
+        y = F.relu(F.conv_transpose2d(self.res5(torch.from_numpy(mf)),
+                                      self.sd["Mask_Head.upconv5.weight"],
+                                      self.sd["Mask_Head.upconv5.bias"], 2))
+        m = torch.sigmoid(self._conv(y, "Mask_Outs.classify")).numpy()
+        masks = m[np.arange(len(classes)), classes]
+        extra.update(mask_rois=mrois, mask_feat=mf)
+        return sc, bx, classes, masks, extra

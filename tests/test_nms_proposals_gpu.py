@@ -86,6 +86,49 @@ def test_generate_proposals_golden(golden):
         assert np.array_equal(sel, c["rois_fpn%d" % (k + 2)])
 
 
+def test_generate_proposals_c4_golden(golden):
+    """Single-scale C4 RPN (15 anchors, pre 6000 -> the large-candidate kernel)
+    against the reference-executed GenerateProposalsOp (proposals_c4.npz)."""
+    from vosdetectron_amd import ops
+    g = golden("proposals_c4")
+    rois, pr, cnt = ops.generate_proposals(
+        [torch.from_numpy(g["probs"]).to(DEV)], [torch.from_numpy(g["deltas"]).to(DEV)],
+        [torch.from_numpy(g["anchors"]).to(DEV)], [1. / 16],
+        torch.from_numpy(g["im_info"]).to(DEV), 6000, 1000, 0.7, 0)
+    k = int(cnt[0, 0].item())
+    assert k == len(g["rois"])
+    assert np.array_equal(rois[0, 0, :k].cpu().numpy(), g["rois"])
+    assert np.array_equal(pr[0, 0, :k].cpu().numpy(), g["roi_probs"][:, 0])
+
+
+@pytest.mark.parametrize("seed,pre,A,H,W", [(0, 6000, 15, 50, 84), (1, 6000, 15, 50, 84),
+                                           (2, 8192, 15, 38, 60), (3, 3000, 9, 25, 42),
+                                           (4, 0, 15, 20, 25)])
+def test_generate_proposals_large_vs_oracle(seed, pre, A, H, W):
+    """Large-candidate variant with ties, two images (seed 1/4: heavy ties; pre=0 and
+    n_all = 7500 <= 8192: take-all)."""
+    from vosdetectron_amd import ops
+    rng = np.random.default_rng(100 + seed)
+    N = 2
+    an = orc.generate_anchors(16, (32, 64, 128, 256, 512)[:A // 3], (0.5, 1, 2))
+    p = rng.uniform(0, 1, (N, A, H, W)).astype(np.float32)
+    if seed in (1, 4):
+        p = (np.round(p * 256) / 256).astype(np.float32)
+    d = rng.normal(0, 0.5, (N, 4 * A, H, W)).astype(np.float32)
+    info = np.array([[H * 16, W * 16, 1.0]] * N, np.float32)
+    rois, pr, cnt = [t.cpu().numpy() for t in ops.generate_proposals(
+        [torch.from_numpy(p).to(DEV)], [torch.from_numpy(d).to(DEV)],
+        [torch.from_numpy(an).to(DEV)], [1. / 16], torch.from_numpy(info).to(DEV), pre, 1000,
+        0.7, 0)]
+    ref_r, ref_p = orc.generate_proposals(an, 1. / 16, p, d, info, pre, 1000, 0.7, 0)
+    for img in range(N):
+        sel = ref_r[:, 0] == img
+        k = cnt[img, 0]
+        assert k == sel.sum(), img
+        assert np.array_equal(rois[img, 0, :k], ref_r[sel]), img
+        assert np.array_equal(pr[img, 0, :k], ref_p[sel, 0]), img
+
+
 @pytest.mark.parametrize("seed,ties", [(0, False), (1, True), (2, True)])
 def test_generate_proposals_vs_oracle_batched(seed, ties):
     """Two images, full-size P2..P6 of an 800x1344 blob, tied scores."""

@@ -43,6 +43,17 @@ def test_generate_proposals(golden):
         assert np.array_equal(probs, g["roi_probs_fpn%d" % lvl]), lvl
 
 
+def test_generate_proposals_c4(golden):
+    """Single-scale C4 RPN: 15 anchors, pre/post 6000/1000 (proposals_c4.npz)."""
+    g = golden("proposals_c4")
+    assert np.array_equal(orc.generate_anchors(16, (32, 64, 128, 256, 512), (0.5, 1, 2)),
+                          g["anchors"])
+    rois, probs = orc.generate_proposals(g["anchors"], 1. / 16, g["probs"], g["deltas"],
+                                         g["im_info"], 6000, 1000, 0.7, 0)
+    assert np.array_equal(rois, g["rois"])
+    assert np.array_equal(probs, g["roi_probs"])
+
+
 def test_collect_distribute(golden):
     g = golden("proposals")
     rois = [g["rois_fpn%d" % l] for l in range(2, 7)]

@@ -186,6 +186,25 @@ def main():
     np.savez(os.path.join(OUT, "multilevel_mask_rois.npz"), mask_rois=mrois,
              **{k: np.asarray(v) for k, v in blobs.items()})
 
+    # ---- single-scale C4 RPN (rpn_heads.single_scale_rpn_outputs, :38-55 and
+    # GenerateProposalsOp with e2e_mask_rcnn_R-50-C4_1x.yaml TEST pre/post
+    # 6000/1000): 15 anchors at stride 16 on a 50x84 res4 map
+    rng4 = np.random.default_rng(20241016)
+    cfg.TEST.RPN_PRE_NMS_TOP_N = 6000
+    cfg.TEST.RPN_POST_NMS_TOP_N = 1000
+    anchors = generate_anchors(stride=16, sizes=(32, 64, 128, 256, 512),
+                               aspect_ratios=(0.5, 1, 2))
+    A, H, W = anchors.shape[0], 50, 84
+    probs = distinct_scores(rng4, A * H * W).reshape(1, A, H, W)
+    deltas = rng4.normal(0, 0.3, (1, 4 * A, H, W)).astype(np.float32)
+    op = GenerateProposalsOp(anchors, 1. / 16)
+    op.eval()
+    import torch
+    rois, rprobs = op(torch.from_numpy(probs), torch.from_numpy(deltas), torch.from_numpy(im_info))
+    np.savez(os.path.join(OUT, "proposals_c4.npz"), anchors=anchors, probs=probs, deltas=deltas,
+             rois=rois, roi_probs=rprobs, im_info=im_info, pre_nms=6000, post_nms=1000)
+    cfg.TEST.RPN_PRE_NMS_TOP_N = 1000
+
     print("wrote", sorted(os.listdir(OUT)))
 
 

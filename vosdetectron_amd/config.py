@@ -118,6 +118,27 @@ def e2e_mask_rcnn_R_50_FPN_1x() -> AttrDict:
         "TEST.RPN_POST_NMS_TOP_N": 1000})
 
 
+def e2e_mask_rcnn_R_50_C4_1x() -> AttrDict:
+    """configs/baselines/e2e_mask_rcnn_R-50-C4_1x.yaml (BASELINE.json configs[0]):
+    no FPN (FPN_ON default False, config.py:682), ResNet50_conv4_body,
+    ResNet_roi_conv5_head, mask_rcnn_fcn_head_v0upshare (-> MODEL.SHARE_RES5,
+    config.py:1072-1095), RoIAlign 14x14 with the adaptive sampling ratio
+    (ROI_XFORM_SAMPLING_RATIO default 0), RPN pre/post 6000/1000."""
+    return load_cfg(overrides={
+        "MODEL.CONV_BODY": "ResNet.ResNet50_conv4_body", "MODEL.FASTER_RCNN": True,
+        "MODEL.MASK_ON": True, "FPN.FPN_ON": False, "FPN.MULTILEVEL_ROIS": False,
+        "FPN.MULTILEVEL_RPN": False, "RPN.SIZES": (32, 64, 128, 256, 512),
+        "FAST_RCNN.ROI_BOX_HEAD": "ResNet.ResNet_roi_conv5_head",
+        "FAST_RCNN.ROI_XFORM_METHOD": "RoIAlign", "FAST_RCNN.ROI_XFORM_RESOLUTION": 14,
+        "FAST_RCNN.ROI_XFORM_SAMPLING_RATIO": 0,
+        "MRCNN.ROI_MASK_HEAD": "mask_rcnn_heads.mask_rcnn_fcn_head_v0upshare",
+        "MRCNN.RESOLUTION": 14, "MRCNN.ROI_XFORM_METHOD": "RoIAlign",
+        "MRCNN.ROI_XFORM_RESOLUTION": 14, "MRCNN.ROI_XFORM_SAMPLING_RATIO": 0,
+        "MRCNN.DILATION": 1, "MRCNN.CONV_INIT": "MSRAFill", "TEST.SCALE": 800,
+        "TEST.MAX_SIZE": 1333, "TEST.NMS": 0.5, "TEST.RPN_PRE_NMS_TOP_N": 6000,
+        "TEST.RPN_POST_NMS_TOP_N": 1000})
+
+
 def e2e_mask_rcnn_R_101_FPN_2x() -> AttrDict:
     cfg = e2e_mask_rcnn_R_50_FPN_1x()
     cfg.MODEL.CONV_BODY = "FPN.fpn_ResNet101_conv5_body"
@@ -169,6 +190,7 @@ def vos_R_101_FPN_3x_gn_dynamic_davis() -> AttrDict:
 
 
 CONFIGS = {
+    "e2e_mask_rcnn_R-50-C4_1x": e2e_mask_rcnn_R_50_C4_1x,
     "e2e_mask_rcnn_R-50-FPN_1x": e2e_mask_rcnn_R_50_FPN_1x,
     "e2e_mask_rcnn_R-101-FPN_2x": e2e_mask_rcnn_R_101_FPN_2x,
     "e2e_mask_rcnn_X-101-32x8d-FPN_1x": e2e_mask_rcnn_X_101_32x8d_FPN_1x,

@@ -28,6 +28,12 @@ namespace vd {
 static constexpr int kSelCap = 8192;      // candidate keys held in LDS
 static constexpr int kPreMax = 2048;      // pre_nms_topN per level
 static constexpr int kSampleMax = 2048;
+// Large variant (single-scale C4 RPN: 15 anchors, TEST.RPN_PRE_NMS_TOP_N 6000,
+// e2e_mask_rcnn_R-50-C4_1x.yaml): 128 KiB of candidate keys in LDS, the
+// per-candidate box arrays in the global workspace.
+static constexpr int kSelCapL = 16384;
+static constexpr int kPreMaxL = 8192;
+static_assert(sizeof(uint64_t) * kSelCapL + 2 * kPreMaxL + 128 <= 160 * 1024, "LDS");
 static constexpr double kBboxXformClip = 4.135166556742356;  // np.log(1000. / 16.)
 
 struct RpnArgs {
@@ -39,12 +45,36 @@ static inline size_t rpn_mask_bytes(int pre) {
     return a256(sizeof(uint64_t) * (size_t)pre * (size_t)((pre + 63) / 64));
 }
 
+static inline size_t rpn_box_bytes(int pre) { return a256(sizeof(float) * 10 * (size_t)pre); }
+
+// pre_nms_topN actually used per level and whether the large variant is needed
+static bool rpn_plan(const VdRpnLevel *levels, int num_levels, int pre_nms_topN, int *max_pre,
+                     bool *large) {
+    *max_pre = 0;
+    *large = false;
+    for (int l = 0; l < num_levels; ++l) {
+        const int n_all = levels[l].A * levels[l].H * levels[l].W;
+        const bool take_all = pre_nms_topN <= 0 || pre_nms_topN >= n_all;
+        const int pre = take_all ? n_all : pre_nms_topN;
+        if (pre > kPreMax || (take_all && n_all > kSelCap)) *large = true;
+        if (pre > kPreMaxL || (take_all && n_all > kSelCapL)) return false;
+        *max_pre = pre > *max_pre ? pre : *max_pre;
+    }
+    return true;
+}
+
+static inline size_t rpn_slot_bytes(int max_pre, bool large) {
+    const int p = max_pre < 64 ? 64 : max_pre;
+    return large ? rpn_mask_bytes(p) + rpn_box_bytes(p) : rpn_mask_bytes(p);
+}
+
 size_t rpn_workspace_bytes(const VdRpnLevel *levels, int num_levels, int num_images,
                            int pre_nms_topN) {
-    (void)levels;
-    int pre = pre_nms_topN > 0 ? pre_nms_topN : kPreMax;
-    if (pre > kPreMax) pre = kPreMax;
-    return rpn_mask_bytes(pre) * (size_t)num_levels * (size_t)num_images + 256;
+    int max_pre;
+    bool large;
+    if (num_levels < 1 || !rpn_plan(levels, num_levels, pre_nms_topN, &max_pre, &large))
+        return 256;
+    return rpn_slot_bytes(max_pre, large) * (size_t)num_levels * (size_t)num_images + 256;
 }
 
 // numpy-2 bbox_transform of one box with weights (wx, wy, ww, wh): returns
@@ -88,22 +118,25 @@ __device__ __forceinline__ int fpn_level(float x1, float y1, float x2, float y2,
     return (int)lv;
 }
 
+// Small variant: everything in LDS.  Large variant (GB = true): the ten
+// per-candidate float arrays live in the slot's global workspace.
+template <int SelCap, int PreMax, bool GB>
 struct RpnLds {
-    uint64_t keys[kSelCap];          // 64 KiB: candidates, later NMS order keys
-    float px1[kPreMax], py1[kPreMax], px2[kPreMax], py2[kPreMax], psc[kPreMax];
-    float ox1[kPreMax], oy1[kPreMax], ox2[kPreMax], oy2[kPreMax], oar[kPreMax];
-    uint8_t keep_rank[kPreMax];
-    uint8_t keep_pos[kPreMax];
+    uint64_t keys[SelCap];           // candidates, later NMS order keys
+    float box[GB ? 1 : 10][GB ? 1 : PreMax];
+    uint8_t keep_rank[PreMax];
+    uint8_t keep_pos[PreMax];
     int scratch[32];
 };
 
+template <int SelCap, int PreMax, bool GB>
 __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
     RpnArgs args, int num_levels, const float *__restrict__ im_info, int pre_nms_topN,
     int post_nms_topN, float nms_thresh, float min_size, float *__restrict__ rois_out,
     float *__restrict__ probs_out, int32_t *__restrict__ counts_out, char *__restrict__ ws,
-    size_t mask_bytes) {
+    size_t slot_bytes, size_t mask_bytes) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-    RpnLds &L = *reinterpret_cast<RpnLds *>(lds_raw);
+    auto &L = *reinterpret_cast<RpnLds<SelCap, PreMax, GB> *>(lds_raw);
     const int l = blockIdx.x, img = blockIdx.y;
     const VdRpnLevel lv = args.lv[l];
     const int A = lv.A, H = lv.H, W = lv.W, K = H * W;
@@ -111,7 +144,16 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
     const float *probs = lv.cls_prob + (int64_t)img * A * K;
     const float *deltas = lv.bbox_pred + (int64_t)img * 4 * A * K;
     const int slot = img * num_levels + l;
-    uint64_t *mask = reinterpret_cast<uint64_t *>(ws + (size_t)slot * mask_bytes);
+    uint64_t *mask = reinterpret_cast<uint64_t *>(ws + (size_t)slot * slot_bytes);
+    float *boxes = GB ? reinterpret_cast<float *>(ws + (size_t)slot * slot_bytes + mask_bytes)
+                      : &L.box[0][0];
+    // box-array stride: the slot's box region holds >= max_pre entries (rpn_box_bytes)
+    const int bstride = GB ? (int)((slot_bytes - mask_bytes) / (10 * sizeof(float))) : PreMax;
+    float *const px1 = boxes, *const py1 = boxes + bstride, *const px2 = boxes + 2 * bstride;
+    float *const py2 = boxes + 3 * bstride, *const psc = boxes + 4 * bstride;
+    float *const ox1 = boxes + 5 * bstride, *const oy1 = boxes + 6 * bstride;
+    float *const ox2 = boxes + 7 * bstride, *const oy2 = boxes + 8 * bstride;
+    float *const oar = boxes + 9 * bstride;
 
     // element e = (h*W + w)*A + a lives at probs[a*K + h*W + w]
     auto key_of = [&](int e) -> uint64_t {
@@ -151,7 +193,7 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
             int c = 0;
             for (int m = threadIdx.x; m < n_all; m += blockDim.x) c += key_mem(m) >= thr;
             c = block_sum(c, L.scratch);
-            if (c >= pre && c <= kSelCap) { ncand = c; break; }
+            if (c >= pre && c <= SelCap) { ncand = c; break; }
             if (c < pre) lo = rank + 1; else hi = rank - 1;
             if (lo > hi) break;
             rank = (lo + hi) >> 1;
@@ -191,26 +233,26 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
         y1 = clip_coord(y1, im_h - 1.f);
         x2 = clip_coord(x2, im_w - 1.f);
         y2 = clip_coord(y2, im_h - 1.f);
-        L.ox1[t] = x1;
-        L.oy1[t] = y1;
-        L.ox2[t] = x2;
-        L.oy2[t] = y2;
-        L.oar[t] = key_float((uint32_t)(k >> 32));
+        ox1[t] = x1;
+        oy1[t] = y1;
+        ox2[t] = x2;
+        oy2[t] = y2;
+        oar[t] = key_float((uint32_t)(k >> 32));
     }
     __syncthreads();
     const int m = block_compact(
         pre,
         [&](int t) {
-            const float ws_ = L.ox2[t] - L.ox1[t] + 1.f, hs = L.oy2[t] - L.oy1[t] + 1.f;
-            const float xc = L.ox1[t] + ws_ / 2.f, yc = L.oy1[t] + hs / 2.f;
+            const float ws_ = ox2[t] - ox1[t] + 1.f, hs = oy2[t] - oy1[t] + 1.f;
+            const float xc = ox1[t] + ws_ / 2.f, yc = oy1[t] + hs / 2.f;
             return (ws_ >= ms) && (hs >= ms) && (xc < im_w) && (yc < im_h);
         },
         [&](int p, int t) {
-            L.px1[p] = L.ox1[t];
-            L.py1[p] = L.oy1[t];
-            L.px2[p] = L.ox2[t];
-            L.py2[p] = L.oy2[t];
-            L.psc[p] = L.oar[t];
+            px1[p] = ox1[t];
+            py1[p] = oy1[t];
+            px2[p] = ox2[t];
+            py2[p] = oy2[t];
+            psc[p] = oar[t];
         },
         L.scratch);
 
@@ -221,11 +263,11 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
         const int n_out = min(m, cap);
         for (int p = threadIdx.x; p < n_out; p += blockDim.x) {
             ro[p * 5 + 0] = (float)img;
-            ro[p * 5 + 1] = L.px1[p];
-            ro[p * 5 + 2] = L.py1[p];
-            ro[p * 5 + 3] = L.px2[p];
-            ro[p * 5 + 4] = L.py2[p];
-            po[p] = L.psc[p];
+            ro[p * 5 + 1] = px1[p];
+            ro[p * 5 + 2] = py1[p];
+            ro[p * 5 + 3] = px2[p];
+            ro[p * 5 + 4] = py2[p];
+            po[p] = psc[p];
         }
         if (threadIdx.x == 0) counts_out[slot] = n_out;
         return;
@@ -235,21 +277,21 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
     {
         const int np2 = next_pow2(m);
         for (int p = threadIdx.x; p < np2; p += blockDim.x)
-            L.keys[p] = p < m ? ((uint64_t)float_key(L.psc[p]) << 32) | (uint32_t)p : 0ull;
+            L.keys[p] = p < m ? ((uint64_t)float_key(psc[p]) << 32) | (uint32_t)p : 0ull;
         __syncthreads();
         if (m > 1) bitonic_sort_desc(L.keys, np2);
     }
     for (int r = threadIdx.x; r < m; r += blockDim.x) {
         const int p = (int)(uint32_t)L.keys[r];
-        const float a = L.px1[p], b = L.py1[p], c = L.px2[p], e = L.py2[p];
-        L.ox1[r] = a;
-        L.oy1[r] = b;
-        L.ox2[r] = c;
-        L.oy2[r] = e;
-        L.oar[r] = (c - a + 1) * (e - b + 1);
+        const float a = px1[p], b = py1[p], c = px2[p], e = py2[p];
+        ox1[r] = a;
+        oy1[r] = b;
+        ox2[r] = c;
+        oy2[r] = e;
+        oar[r] = (c - a + 1) * (e - b + 1);
     }
     __syncthreads();
-    nms_build_mask_rows(L.ox1, L.oy1, L.ox2, L.oy2, L.oar, m, nms_thresh, mask, wave_id(),
+    nms_build_mask_rows(ox1, oy1, ox2, oy2, oar, m, nms_thresh, mask, wave_id(),
                         num_waves());
     __threadfence_block();
     __syncthreads();
@@ -263,11 +305,11 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
         [&](int pos, int p) {
             if (pos < cap) {
                 ro[pos * 5 + 0] = (float)img;
-                ro[pos * 5 + 1] = L.px1[p];
-                ro[pos * 5 + 2] = L.py1[p];
-                ro[pos * 5 + 3] = L.px2[p];
-                ro[pos * 5 + 4] = L.py2[p];
-                po[pos] = L.psc[p];
+                ro[pos * 5 + 1] = px1[p];
+                ro[pos * 5 + 2] = py1[p];
+                ro[pos * 5 + 3] = px2[p];
+                ro[pos * 5 + 4] = py2[p];
+                po[pos] = psc[p];
             }
         },
         L.scratch);
@@ -279,26 +321,31 @@ int launch_rpn_proposals(const VdRpnLevel *levels, int num_levels, int num_image
                          float nms_thresh, float min_size, float *rois_out, float *probs_out,
                          int32_t *counts_out, void *workspace, size_t ws_bytes, hipStream_t s) {
     if (num_levels < 1 || num_levels > VD_MAX_LEVELS || num_images < 1) return VD_ERR_ARG;
-    RpnArgs args;
-    int max_pre = 0;
-    for (int l = 0; l < num_levels; ++l) {
-        args.lv[l] = levels[l];
-        const int n_all = levels[l].A * levels[l].H * levels[l].W;
-        const bool take_all = pre_nms_topN <= 0 || pre_nms_topN >= n_all;
-        const int pre = take_all ? n_all : pre_nms_topN;
-        if (take_all && n_all > kSelCap) return VD_ERR_SHAPE;
-        if (pre > kPreMax) return VD_ERR_SHAPE;
-        if (post_nms_topN <= 0 && pre > kPreMax) return VD_ERR_SHAPE;
-        max_pre = pre > max_pre ? pre : max_pre;
-    }
     if (post_nms_topN <= 0) return VD_ERR_ARG;  // output capacity is post_nms_topN
-    const size_t mb = rpn_mask_bytes(kPreMax < max_pre ? kPreMax : (max_pre < 64 ? 64 : max_pre));
-    if (!workspace || ws_bytes < mb * (size_t)num_levels * (size_t)num_images)
+    RpnArgs args;
+    for (int l = 0; l < num_levels; ++l) args.lv[l] = levels[l];
+    int max_pre;
+    bool large;
+    if (!rpn_plan(levels, num_levels, pre_nms_topN, &max_pre, &large)) return VD_ERR_SHAPE;
+    const int p = max_pre < 64 ? 64 : max_pre;
+    const size_t mb = rpn_mask_bytes(p);
+    const size_t sb = rpn_slot_bytes(max_pre, large);
+    if (!workspace || ws_bytes < sb * (size_t)num_levels * (size_t)num_images)
         return VD_ERR_WORKSPACE;
-    hipLaunchKernelGGL(rpn_proposals_kernel, dim3(num_levels, num_images), dim3(1024),
-                       sizeof(RpnLds), s, args, num_levels, im_info, pre_nms_topN, post_nms_topN,
-                       nms_thresh, min_size, rois_out, probs_out, counts_out, (char *)workspace,
-                       mb);
+    const dim3 grid(num_levels, num_images);
+    if (large) {
+        using Lds = RpnLds<kSelCapL, kPreMaxL, true>;
+        hipLaunchKernelGGL((rpn_proposals_kernel<kSelCapL, kPreMaxL, true>), grid, dim3(1024),
+                           sizeof(Lds), s, args, num_levels, im_info,
+                           pre_nms_topN, post_nms_topN, nms_thresh, min_size, rois_out,
+                           probs_out, counts_out, (char *)workspace, sb, mb);
+    } else {
+        using Lds = RpnLds<kSelCap, kPreMax, false>;
+        hipLaunchKernelGGL((rpn_proposals_kernel<kSelCap, kPreMax, false>), grid, dim3(1024),
+                           sizeof(Lds), s, args, num_levels, im_info, pre_nms_topN,
+                           post_nms_topN, nms_thresh, min_size, rois_out, probs_out, counts_out,
+                           (char *)workspace, sb, mb);
+    }
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 

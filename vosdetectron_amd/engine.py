@@ -56,13 +56,14 @@ class FramePipeline:
                                     device=self.device)
         self.im_scale_t = torch.full((F,), scale, dtype=torch.float32, device=self.device)
         self.im_hw = torch.tensor([[self.H, self.W]] * F, dtype=torch.int32, device=self.device)
-        k_min, k_max = cfg.FPN.RPN_MIN_LEVEL, cfg.FPN.RPN_MAX_LEVEL
-        self.rpn_levels = list(range(k_min, k_max + 1))
-        self.anchors = [getattr(model, "anchors_fpn%d" % l).to(self.device)
-                        for l in self.rpn_levels]
-        self.rpn_scales = [1. / 2 ** l for l in self.rpn_levels]
-        self.roi_levels = list(range(cfg.FPN.ROI_MIN_LEVEL, cfg.FPN.ROI_MAX_LEVEL + 1))
-        self.roi_scales = [1. / 2 ** l for l in self.roi_levels]
+        if cfg.FPN.FPN_ON:
+            k_min, k_max = cfg.FPN.RPN_MIN_LEVEL, cfg.FPN.RPN_MAX_LEVEL
+            self.rpn_levels = list(range(k_min, k_max + 1))
+            self.anchors = [getattr(model, "anchors_fpn%d" % l).to(self.device)
+                            for l in self.rpn_levels]
+            self.rpn_scales = [1. / 2 ** l for l in self.rpn_levels]
+            self.roi_levels = list(range(cfg.FPN.ROI_MIN_LEVEL, cfg.FPN.ROI_MAX_LEVEL + 1))
+            self.roi_scales = [1. / 2 ** l for l in self.roi_levels]
         self.timers = None
 
     # ------------------------------------------------------------------ #

@@ -661,32 +661,42 @@ class Generalized_RCNN(nn.Module):
 
 
 @torch.no_grad()
-def prepare_fpn_body(fpn: FPNBody, epilogue: bool = True):
-    """Inference-time rewrite of an FPNBody: AffineChannel2d folded into the
-    convs (BN bodies) and the fused HIP epilogues switched on."""
-    body = fpn.conv_body
+def prepare_bottlenecks(blocks, epilogue: bool = True):
+    """Fold each BN Bottleneck's AffineChannel2d into its convs and switch on the
+    fused bias/residual/ReLU epilogue (GN blocks: the fused GroupNorm epilogue)."""
+    for blk in blocks:
+        if isinstance(blk, Bottleneck):
+            blk.f1 = _fold(blk.conv1, blk.bn1)
+            blk.f2 = _fold(blk.conv2, blk.bn2)
+            blk.f3 = _fold(blk.conv3, blk.bn3)
+            if blk.downsample is not None:
+                blk.fd = _fold(blk.downsample[0], blk.downsample[1])
+            blk.fused = True
+        blk.epilogue = epilogue
+
+
+@torch.no_grad()
+def prepare_resnet_body(body: ResNetBody, epilogue: bool = True):
+    """Inference-time rewrite of a ResNetBody (stem + every stage)."""
     stem = body.res1
     if body.use_gn:
         body.res1 = _StemGN(stem.conv1, stem.gn1, stem.maxpool) if epilogue else stem
-        for i in range(2, body.convX + 1):
-            for blk in getattr(body, "res%d" % i):
-                blk.epilogue = epilogue
+    elif epilogue:
+        body.res1 = _StemEpilogue(_fold(stem.conv1, stem.bn1), stem.maxpool)
     else:
-        if epilogue:
-            body.res1 = _StemEpilogue(_fold(stem.conv1, stem.bn1), stem.maxpool)
-        else:
-            body.res1 = nn.Sequential(OrderedDict([
-                ("conv1", _fold(stem.conv1, stem.bn1)), ("relu", nn.ReLU(inplace=True)),
-                ("maxpool", stem.maxpool)]))
-        for i in range(2, body.convX + 1):
-            for blk in getattr(body, "res%d" % i):
-                blk.f1 = _fold(blk.conv1, blk.bn1)
-                blk.f2 = _fold(blk.conv2, blk.bn2)
-                blk.f3 = _fold(blk.conv3, blk.bn3)
-                if blk.downsample is not None:
-                    blk.fd = _fold(blk.downsample[0], blk.downsample[1])
-                blk.fused = True
-                blk.epilogue = epilogue
+        body.res1 = nn.Sequential(OrderedDict([
+            ("conv1", _fold(stem.conv1, stem.bn1)), ("relu", nn.ReLU(inplace=True)),
+            ("maxpool", stem.maxpool)]))
+    for i in range(2, body.convX + 1):
+        prepare_bottlenecks(getattr(body, "res%d" % i), epilogue)
+    return body
+
+
+@torch.no_grad()
+def prepare_fpn_body(fpn: FPNBody, epilogue: bool = True):
+    """Inference-time rewrite of an FPNBody: AffineChannel2d folded into the
+    convs (BN bodies) and the fused HIP epilogues switched on."""
+    prepare_resnet_body(fpn.conv_body, epilogue)
     for m in fpn.topdown_lateral_modules:
         m.epilogue = epilogue
     fpn.epilogue = epilogue

@@ -77,6 +77,8 @@ def calibrate(model, frame_u8: np.ndarray, device):
             return (out - out.mean()) * g + target_mean
         return hook
 
+    if not model.cfg.FPN.FPN_ON:
+        return _calibrate_c4(model, blob[:, :, :H, :W], affine_pre, unit_out)
     for m in model.Conv_Body.conv_body.modules():
         if isinstance(m, AffineChannel2d):
             hooks.append(m.register_forward_pre_hook(affine_pre))
@@ -107,6 +109,34 @@ def calibrate(model, frame_u8: np.ndarray, device):
     return model
 
 
+@torch.no_grad()
+def _calibrate_c4(model, blob, affine_pre, unit_out):
+    """C4 family (no FPN): whiten the body's and the res5 head's AffineChannel2d
+    (the head on the whole res4 map, a stand-in for its RoI features), unit-scale
+    the RPN convs; same head gains as the FPN models."""
+    from .modeling import AffineChannel2d
+    hooks = []
+    for mod in (model.Conv_Body, model.Box_Head.res5):
+        for m in mod.modules():
+            if isinstance(m, AffineChannel2d):
+                hooks.append(m.register_forward_pre_hook(affine_pre))
+    rpn = model.RPN
+    hooks.append(rpn.RPN_conv.register_forward_hook(unit_out()))
+    hooks.append(rpn.RPN_cls_score.register_forward_hook(unit_out(1.5, -1.5)))
+    hooks.append(rpn.RPN_bbox_pred.register_forward_hook(unit_out(0.2)))
+    res4 = model.Conv_Body(blob)
+    rpn.outputs(res4)
+    model.Box_Head.res5(res4)
+    for h in hooks:
+        h.remove()
+    for m in model.modules():
+        if hasattr(m, "_calibrated"):
+            del m._calibrated
+    model.Box_Outs.cls_score.weight.mul_(6.0)
+    model.Mask_Outs.classify.weight.mul_(4.0)
+    return model
+
+
 def build_model(cfg, seed: int = 0, device="cuda", fold=True, channels_last=False,
                 calibrate_frame: np.ndarray | None = None):
     """Generalized_RCNN (Generalized_VOS_RCNN for the VOS configs, i.e. when
@@ -114,10 +144,12 @@ def build_model(cfg, seed: int = 0, device="cuda", fold=True, channels_last=Fals
     (calibrated) weights in eval mode.  Returns (model, state_dict) where
     state_dict has the reference's names and the unfolded AffineChannel
     parameters (what the oracle pipelines load)."""
+    from .c4 import Generalized_RCNN_C4
     from .modeling import Generalized_RCNN
     from .vos import Generalized_VOS_RCNN
     vos = bool(cfg.get("VOS", False))
-    m = (Generalized_VOS_RCNN if vos else Generalized_RCNN)(cfg)
+    c4 = not cfg.FPN.FPN_ON
+    m = (Generalized_VOS_RCNN if vos else Generalized_RCNN_C4 if c4 else Generalized_RCNN)(cfg)
     sd = synthetic_state_dict(m, seed)
     missing, unexpected = m.load_state_dict(sd, strict=False)
     assert not unexpected, unexpected
@@ -135,7 +167,11 @@ def build_model(cfg, seed: int = 0, device="cuda", fold=True, channels_last=Fals
     if channels_last:
         m.Conv_Body.to(memory_format=torch.channels_last)
         m.RPN.to(memory_format=torch.channels_last)
-        m.Mask_Head.conv_fcn.to(memory_format=torch.channels_last)
+        if c4:
+            m.Box_Head.to(memory_format=torch.channels_last)
+            m.Mask_Head.upconv5.to(memory_format=torch.channels_last)
+        else:
+            m.Mask_Head.conv_fcn.to(memory_format=torch.channels_last)
         if vos:
             m.ConvGRUs.to(memory_format=torch.channels_last)
     return m, sd
