@@ -291,6 +291,30 @@ int vd_convgru_update(const float *hh, const float *hx, const float *z, const fl
                       const float *gamma_h, const float *beta_h, int layout, float *out,
                       void *workspace, size_t ws_bytes, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * segm_results (lib/core/test.py:801-855; fork lib_vos/tools/vos_test.py:867-921)
+ * on the device, SURVEY.md section 8f row 3.
+ *
+ * vd_paste_masks: masks M x R x R fp32 (each detection's class-selected mask
+ * probabilities, i.e. masks[mask_ind, j]), boxes M x box_stride fp32
+ * (x1, y1, x2, y2 in image coordinates, the cls_boxes rows) -> out M x im_h x
+ * im_w u8 (row-major, every byte written): box_utils.expand_boxes by
+ * (R+2)/R (boxes.py:242-258) + astype(int32), cv2.resize(padded_mask, (w, h))
+ * INTER_LINEAR (OpenCV's scalar float path, restated), `> thresh`
+ * (MRCNN.THRESH_BINARIZE), pasted into the clipped box.  R <= 62.
+ *
+ * vd_mask_rle: pycocotools mask.encode counts of each M x H x W u8 plane in
+ * column-major (Fortran) order: counts[m][0..n) with n = ncounts[m], the
+ * first run counting zeros.  If a plane needs more than `cap` runs,
+ * ncounts[m] = -n and its counts are not written (call again with cap >= n).
+ * The run lengths -> ASCII string step (rleToString) is host formatting
+ * (vosdetectron_amd/segm.py).
+ * ------------------------------------------------------------------------- */
+int vd_paste_masks(const float *masks, int M, int R, const float *boxes, int box_stride,
+                   int im_h, int im_w, float thresh, uint8_t *out, void *stream);
+int vd_mask_rle(const uint8_t *masks, int M, int H, int W, uint32_t *counts, int cap,
+                int32_t *ncounts, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

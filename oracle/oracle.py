@@ -420,3 +420,94 @@ def get_image_blob(im, target_scale=800, max_size=1333, stride=32):
     blob = blob.transpose(0, 3, 1, 2)
     im_info = np.array([[H, W, scale]], np.float32)
     return blob, scale, im_info
+
+
+# --------------------------------------------------------------------------- #
+# segm_results (lib/core/test.py:801-855).  cv2 and pycocotools are absent
+# here, so the two third-party steps are restated from their published
+# algorithms -- "parity unpinned" against an executed cv2/pycocotools:
+#   * cv2.resize(src_f32, (w, h)) INTER_LINEAR, OpenCV's scalar float path
+#     (imgproc/src/resize.cpp: coefficient tables of cv::resize, HResizeLinear,
+#     VResizeLinear); IPP/SIMD builds may round differently;
+#   * pycocotools mask.encode (maskApi.c rleEncode + rleToString).
+# --------------------------------------------------------------------------- #
+def expand_boxes(boxes, scale):
+    """lib/utils/boxes.py:242-258 (float32 inputs stay float32 in numpy 2)."""
+    w_half = (boxes[:, 2] - boxes[:, 0]) * .5
+    h_half = (boxes[:, 3] - boxes[:, 1]) * .5
+    x_c = (boxes[:, 2] + boxes[:, 0]) * .5
+    y_c = (boxes[:, 3] + boxes[:, 1]) * .5
+    w_half *= scale
+    h_half *= scale
+    boxes_exp = np.zeros(boxes.shape)
+    boxes_exp[:, 0] = x_c - w_half
+    boxes_exp[:, 2] = x_c + w_half
+    boxes_exp[:, 1] = y_c - h_half
+    boxes_exp[:, 3] = y_c + h_half
+    return boxes_exp
+
+
+def cv2_resize_linear(src, w, h):
+    """cv2.resize(src, (w, h)) for a single-channel float32 image, INTER_LINEAR."""
+    src = np.asarray(src, np.float32)
+    sh, sw = src.shape
+    scale_x = 1. / (float(w) / sw)
+    scale_y = 1. / (float(h) / sh)
+    dx = np.arange(w)
+    fx = ((dx + 0.5) * scale_x - 0.5).astype(np.float32)
+    sx = np.floor(fx).astype(np.int64)
+    fx = (fx - sx.astype(np.float32)).astype(np.float32)
+    lo = sx < 0
+    fx[lo], sx[lo] = 0, 0
+    hi = sx >= sw - 1
+    fx[hi], sx[hi] = 0, sw - 1
+    a0, a1 = (np.float32(1) - fx).astype(np.float32), fx
+    sx1 = np.minimum(sx + 1, sw - 1)
+    D = src[:, sx] * a0 + src[:, sx1] * a1  # HResizeLinear, every source row
+    dy = np.arange(h)
+    fy = ((dy + 0.5) * scale_y - 0.5).astype(np.float32)
+    sy = np.floor(fy).astype(np.int64)
+    fy = (fy - sy.astype(np.float32)).astype(np.float32)
+    r0, r1 = np.clip(sy, 0, sh - 1), np.clip(sy + 1, 0, sh - 1)
+    b0, b1 = (np.float32(1) - fy).astype(np.float32), fy
+    return (D[r0] * b0[:, None] + D[r1] * b1[:, None]).astype(np.float32)  # VResizeLinear
+
+
+def paste_masks(masks, boxes, im_h, im_w, thresh=0.5):
+    """segm_results' per-detection loop (test.py:808-835) up to im_mask:
+    masks [M,R,R] class-selected, boxes [M,>=4] float32 -> [M,im_h,im_w] u8."""
+    M = masks.shape[-1]
+    scale = (M + 2.0) / M
+    ref_boxes = expand_boxes(np.asarray(boxes, np.float32)[:, :4], scale).astype(np.int32)
+    padded = np.zeros((M + 2, M + 2), dtype=np.float32)
+    out = np.zeros((len(masks), im_h, im_w), np.uint8)
+    for i in range(len(masks)):
+        padded[1:-1, 1:-1] = masks[i]
+        rb = ref_boxes[i]
+        w = max(rb[2] - rb[0] + 1, 1)
+        h = max(rb[3] - rb[1] + 1, 1)
+        mask = np.array(cv2_resize_linear(padded, w, h) > thresh, dtype=np.uint8)
+        x_0, x_1 = max(rb[0], 0), min(rb[2] + 1, im_w)
+        y_0, y_1 = max(rb[1], 0), min(rb[3] + 1, im_h)
+        out[i, y_0:y_1, x_0:x_1] = mask[(y_0 - rb[1]):(y_1 - rb[1]), (x_0 - rb[0]):(x_1 - rb[0])]
+    return out
+
+
+def rle_encode(im_mask):
+    """pycocotools mask.encode of one H x W u8 mask: {'size', 'counts' (str)}
+    plus the raw run lengths (maskApi.c rleEncode over Fortran order)."""
+    flat = np.asarray(im_mask, np.uint8).flatten(order="F")
+    change = np.flatnonzero(np.diff(np.concatenate([[0], flat])) != 0)
+    bounds = np.concatenate([[0], change, [flat.size]])
+    cnts = np.diff(bounds).astype(np.int64)
+    s = []
+    for i in range(len(cnts)):  # rleToString
+        x = int(cnts[i]) - (int(cnts[i - 2]) if i > 2 else 0)
+        while True:
+            c = x & 0x1f
+            x >>= 5
+            more = x != -1 if c & 0x10 else x != 0
+            s.append(chr((c | (0x20 if more else 0)) + 48))
+            if not more:
+                break
+    return {"size": [int(im_mask.shape[0]), int(im_mask.shape[1])], "counts": "".join(s)}, cnts

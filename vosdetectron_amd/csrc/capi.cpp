@@ -340,4 +340,22 @@ int vd_convgru_update(const float *hh, const float *hx, const float *z, const fl
     return launch_gn_apply(a, B, C, H, W, G, nhwc, s);
 }
 
+int vd_paste_masks(const float *masks, int M, int R, const float *boxes, int box_stride,
+                   int im_h, int im_w, float thresh, uint8_t *out, void *stream) {
+    if (M == 0) return VD_OK;
+    if (!masks || !boxes || !out || M < 0 || R < 1 || box_stride < 4 || im_h < 1 || im_w < 1)
+        return VD_ERR_ARG;
+    return launch_paste_masks(masks, M, R, boxes, box_stride, im_h, im_w, thresh, out,
+                              VD_STREAM(stream));
+}
+
+int vd_mask_rle(const uint8_t *masks, int M, int H, int W, uint32_t *counts, int cap,
+                int32_t *ncounts, void *stream) {
+    if (M == 0) return VD_OK;
+    if (!masks || !counts || !ncounts || M < 0 || H < 1 || W < 1 || cap < 1 ||
+        (int64_t)H * W > 0xffffffffll)
+        return VD_ERR_ARG;
+    return launch_mask_rle(masks, M, H, W, counts, cap, ncounts, VD_STREAM(stream));
+}
+
 }  // extern "C"

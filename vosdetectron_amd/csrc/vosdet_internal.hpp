@@ -103,4 +103,9 @@ int launch_gn_stats(const GnSets &sets, int nsets, int B, int C, int HW, int G, 
                     hipStream_t s);
 int launch_gn_apply(const GnApply &a, int B, int C, int H, int W, int G, int nhwc, hipStream_t s);
 
+int launch_paste_masks(const float *masks, int M, int R, const float *boxes, int box_stride,
+                       int im_h, int im_w, float thresh, uint8_t *out, hipStream_t s);
+int launch_mask_rle(const uint8_t *planes, int M, int H, int W, uint32_t *counts, int cap,
+                    int32_t *ncounts, hipStream_t s);
+
 }  // namespace vd

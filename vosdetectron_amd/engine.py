@@ -15,7 +15,8 @@ The reference crosses host<->device 5+5 times in proposals alone and twice per
 roi_feature_transform; here the only host read is the per-frame detection
 count that sizes the mask-head batch.  Outputs match the reference's
 `cls_boxes` rows (class-major, proposal order) and the class-selected masks
-that segm_results consumes (segm_results' paste/RLE is out of scope).
+that segm_results consumes; `frame_segms` runs segm_results' paste + RLE on
+the device (segm.py).
 """
 from __future__ import annotations
 
@@ -171,6 +172,20 @@ class FramePipeline:
         out["masks"] = self.model.Mask_Outs.selected(mh, mcls)
         out["mask_feat"] = mfeat
         return out
+
+
+def frame_segms(pipe: FramePipeline, out: dict, num_classes: int = 81):
+    """segm_results for every frame of a pipeline output (device paste + RLE,
+    vosdetectron_amd/segm.py): list over frames of cls_segms."""
+    from . import segm
+    res, start = [], 0
+    for f, k in enumerate(out["counts_host"]):
+        cls_segms, _ = segm.segm_results(
+            out["dets"][f, :k], out["classes"][f, :k], out["masks"][start:start + k],
+            pipe.H, pipe.W, num_classes, pipe.cfg.MRCNN.THRESH_BINARIZE)
+        res.append(cls_segms)
+        start += k
+    return res
 
 
 class VOSPipeline(FramePipeline):

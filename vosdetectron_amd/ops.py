@@ -460,6 +460,45 @@ def box_detections(rois, cls_prob, bbox_pred, roi_count, im_scale, im_hw, score_
 
 
 # --------------------------------------------------------------------------- #
+# segm_results: paste + binarize + RLE counts      #
+# --------------------------------------------------------------------------- #
+def paste_masks(masks: torch.Tensor, boxes: torch.Tensor, im_h: int, im_w: int,
+                thresh: float = 0.5, out=None) -> torch.Tensor:
+    """masks [M,R,R] fp32 (class-selected probabilities), boxes [M,>=4] fp32 image
+    coordinates -> [M,im_h,im_w] uint8 binary masks (segm_results' expand_boxes +
+    cv2.resize + `> THRESH_BINARIZE` + paste, lib/core/test.py:801-835)."""
+    m = _need(masks, "masks")
+    b = _need(boxes, "boxes")
+    M, R = m.shape[0], m.shape[-1]
+    if b.shape[0] != M or b.dim() != 2 or b.shape[1] < 4:
+        raise ValueError("boxes must be M x >=4, got %s" % (tuple(b.shape),))
+    if out is None:
+        out = torch.empty((M, im_h, im_w), dtype=torch.uint8, device=m.device)
+    check(lib().vd_paste_masks(m.data_ptr(), M, R, b.data_ptr(), b.shape[1], int(im_h),
+                               int(im_w), float(np.float32(thresh)), out.data_ptr(), _stream()),
+          "vd_paste_masks")
+    return out
+
+
+def mask_rle_counts(planes: torch.Tensor, cap: Optional[int] = None):
+    """pycocotools mask.encode run lengths (column-major, zeros first) of each
+    [H,W] uint8 plane: returns (counts int32 [M,cap'], n int32 [M]); runs are
+    < H*W <= 2^31, so int32 holds the kernel's uint32 counts."""
+    p = _need(planes, "planes", torch.uint8)
+    M, H, W = p.shape
+    cap = int(cap or (8 * W + 2))
+    while True:
+        counts = torch.empty((M, cap), dtype=torch.int32, device=p.device)
+        n = torch.empty((M,), dtype=torch.int32, device=p.device)
+        check(lib().vd_mask_rle(p.data_ptr(), M, H, W, counts.data_ptr(), cap, n.data_ptr(),
+                                _stream()), "vd_mask_rle")
+        need = int((-n).max().item()) if M else 0
+        if need <= cap:
+            return counts, n
+        cap = need
+
+
+# --------------------------------------------------------------------------- #
 # VOS temporal path: FlowAlign, GroupNorm epilogues, ConvGRU gates             #
 # --------------------------------------------------------------------------- #
 def _fmt(x: torch.Tensor, name: str) -> int:
