@@ -291,6 +291,17 @@ int vd_convgru_update(const float *hh, const float *hx, const float *z, const fl
                       const float *gamma_h, const float *beta_h, int layout, float *out,
                       void *workspace, size_t ws_bytes, void *stream);
 
+/* The fork's steps after the detections limit in box_results_with_nms_and_limit
+ * (lib_vos/tools/vos_test.py:805-833), in place on vd_box_detections' outputs:
+ * nms_cross_class > 0 -> one NMS (cython semantics) over all classes'
+ * detections, survivors regrouped by class in row order (TEST.NMS_CROSS_CLASS);
+ * num_det_per_class_pre > 0 -> per class the top-k by score, rows reordered by
+ * score (TEST.NUM_DET_PER_CLASS_PRE; ties by row order).  Both off -> no-op.
+ * det_cap <= 512. */
+int vd_detections_postfilter(float *dets, int32_t *classes, int32_t *counts, int num_images,
+                             int det_cap, float nms_cross_class, int num_det_per_class_pre,
+                             void *stream);
+
 /* ---------------------------------------------------------------------------
  * segm_results (lib/core/test.py:801-855; fork lib_vos/tools/vos_test.py:867-921)
  * on the device, SURVEY.md section 8f row 3.

@@ -380,9 +380,13 @@ def roi_feature_transform(blobs_in, rpn_ret, blob_rois, resolution, spatial_scal
 # Detection post-processing                                                    #
 # --------------------------------------------------------------------------- #
 def box_results_with_nms_and_limit(scores, boxes, num_classes=81, score_thresh=0.05,
-                                   nms_thresh=0.5, dets_per_im=100):
-    """lib/core/test.py:733-797 with the fork's NUM_DET_PER_CLASS fix
-    (lib_vos/tools/vos_test.py:748-865, NMS_CROSS_CLASS=0, *_PRE=0)."""
+                                   nms_thresh=0.5, dets_per_im=100, nms_cross_class=0.,
+                                   num_det_per_class_pre=0):
+    """lib/core/test.py:733-797 with the fork's NUM_DET_PER_CLASS fix and its
+    post-limit steps (lib_vos/tools/vos_test.py:748-865): TEST.NMS_CROSS_CLASS
+    (:810-827) and TEST.NUM_DET_PER_CLASS_PRE (:829-833; np.argsort(-s) read
+    stably, kind="stable").  NMS_SMALL_BOX_IOU needs the previous frame's boxes
+    and is off in every shipped config (out of scope)."""
     cls_boxes = [[] for _ in range(num_classes)]
     for j in range(1, num_classes):
         inds = np.where(scores[:, j] >= score_thresh)[0]
@@ -398,6 +402,18 @@ def box_results_with_nms_and_limit(scores, boxes, num_classes=81, score_thresh=0
             for j in range(1, num_classes):
                 keep = np.where(cls_boxes[j][:, -1] >= thr)[0]
                 cls_boxes[j] = cls_boxes[j][keep, :]
+    if nms_cross_class > 0.:
+        all_dets = np.vstack([cls_boxes[j] for j in range(1, num_classes)])
+        class_ids = np.vstack([np.ones(shape=(len(cls_boxes[j]), 1)) * j
+                               for j in range(1, num_classes)])
+        keep = nms(all_dets, nms_cross_class)
+        all_dets, class_ids = all_dets[keep, :], class_ids[keep, :]
+        for j in range(1, num_classes):
+            cls_boxes[j] = all_dets[np.where(class_ids == j)[0], :]
+    if num_det_per_class_pre > 0:
+        for j in range(1, num_classes):
+            keep = np.argsort(-cls_boxes[j][:, -1], kind="stable")[:num_det_per_class_pre]
+            cls_boxes[j] = cls_boxes[j][keep, :]
     im_results = np.vstack([cls_boxes[j] for j in range(1, num_classes)])
     return im_results[:, -1], im_results[:, :-1], cls_boxes
 

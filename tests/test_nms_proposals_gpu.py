@@ -210,3 +210,50 @@ def test_box_detections_vs_oracle(seed):
         assert np.array_equal(dets[i, :n, 4], sc)
         ref_cls = np.concatenate([[j] * len(cls_boxes[j]) for j in range(1, K)]).astype(np.int32)
         assert np.array_equal(dcls[i, :n], ref_cls)
+
+
+@pytest.mark.parametrize("seed,cross,pre,dets_per_im", [(0, 0.3, 0, 100), (1, 0., 2, 100),
+                                                        (2, 0.5, 1, 100), (3, 0.4, 50, 300),
+                                                        (4, 0.7, 3, 400)])
+def test_detections_postfilter_vs_oracle(seed, cross, pre, dets_per_im):
+    """The fork's post-limit steps (vos_test.py:805-833): cross-class NMS and the
+    per-class top-k (NUM_DET_PER_CLASS_PRE, e.g. 50 in
+    R-101-FPN_3x_gn_train_online.yaml), on vd_box_detections' outputs; seeds 1, 3
+    with tied scores."""
+    from vosdetectron_amd import ops
+    rng = np.random.default_rng(50 + seed)
+    N, R, K = 2, 600, 81
+    im_h, im_w = 480, 854
+    rois = np.zeros((N, R, 5), np.float32)
+    for i in range(N):
+        xy = rng.uniform(0, 800, (R, 2))
+        wh = rng.uniform(8, 200, (R, 2))
+        rois[i, :, 0] = i
+        rois[i, :, 1:3] = xy
+        rois[i, :, 3:5] = np.minimum(xy + wh, [863, 479])
+    logits = rng.normal(0, 2.5, (N, R, K)).astype(np.float32)
+    e = np.exp(logits - logits.max(-1, keepdims=True))
+    cls = (e / e.sum(-1, keepdims=True)).astype(np.float32)
+    if seed in (1, 3):
+        cls = (np.round(cls * 64) / 64).astype(np.float32)
+    pred = rng.normal(0, 1.0, (N, R, 4 * K)).astype(np.float32)
+    counts = np.array([R, R - 11], np.int32)
+    out = ops.box_detections(*[torch.from_numpy(x).to(DEV) for x in (rois, cls, pred, counts)],
+                             torch.tensor([1.0, 1.0], device=DEV),
+                             torch.tensor([[im_h, im_w]] * N, dtype=torch.int32, device=DEV),
+                             dets_per_im=dets_per_im, det_cap=512, nms_cross_class=cross,
+                             num_det_per_class_pre=pre)
+    dets, dcls, dcnt = [t.cpu().numpy() for t in out]
+    for i in range(N):
+        r = counts[i]
+        pb = orc.clip_tiled_boxes(orc.bbox_transform(rois[i, :r, 1:5], pred[i, :r],
+                                                     (10., 10., 5., 5.)), (im_h, im_w, 3))
+        sc, bx, cls_boxes = orc.box_results_with_nms_and_limit(
+            cls[i, :r], pb, dets_per_im=dets_per_im, nms_cross_class=cross,
+            num_det_per_class_pre=pre)
+        n = dcnt[i]
+        assert n == len(sc), (n, len(sc))
+        assert np.array_equal(dets[i, :n, :4], bx)
+        assert np.array_equal(dets[i, :n, 4], sc)
+        ref_cls = np.concatenate([[j] * len(cls_boxes[j]) for j in range(1, K)]).astype(np.int32)
+        assert np.array_equal(dcls[i, :n], ref_cls)

@@ -60,6 +60,7 @@ SIGNATURES = {
     "vd_image_to_blob": (_I, [_P, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
     "vd_nchw_to_nhwc": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "vd_bias_act": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
+    "vd_detections_postfilter": (_I, [_P, _P, _P, _I, _I, _F, _I, _P]),
     # segm_results (paste + binarize + RLE counts)
     "vd_paste_masks": (_I, [_P, _I, _I, _P, _I, _I, _I, _F, _P, _P]),
     "vd_mask_rle": (_I, [_P, _I, _I, _I, _P, _I, _P, _P]),

@@ -231,7 +231,8 @@ class C4FramePipeline(FramePipeline):
         dets, dcls, dcnt = ops.box_detections(
             rois, cls_prob.view(F_, post, K), bbox_pred.view(F_, post, 4 * K), rcnt,
             self.im_scale_t[:F_], self.im_hw[:F_], tst.SCORE_THRESH, tst.NMS,
-            tst.DETECTIONS_PER_IM, cfg.MODEL.BBOX_REG_WEIGHTS, self.det_cap)
+            tst.DETECTIONS_PER_IM, cfg.MODEL.BBOX_REG_WEIGHTS, self.det_cap,
+            nms_cross_class=tst.NMS_CROSS_CLASS, num_det_per_class_pre=tst.NUM_DET_PER_CLASS_PRE)
         counts = dcnt.cpu().tolist()
         if max(counts) > self.det_cap:
             raise RuntimeError("detections exceed det_cap=%d: %s" % (self.det_cap, counts))

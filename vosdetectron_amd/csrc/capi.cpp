@@ -358,4 +358,13 @@ int vd_mask_rle(const uint8_t *masks, int M, int H, int W, uint32_t *counts, int
     return launch_mask_rle(masks, M, H, W, counts, cap, ncounts, VD_STREAM(stream));
 }
 
+int vd_detections_postfilter(float *dets, int32_t *classes, int32_t *counts, int num_images,
+                             int det_cap, float nms_cross_class, int num_det_per_class_pre,
+                             void *stream) {
+    if (!dets || !classes || !counts) return VD_ERR_ARG;
+    return launch_detections_postfilter(dets, classes, counts, num_images, det_cap,
+                                        nms_cross_class, num_det_per_class_pre,
+                                        VD_STREAM(stream));
+}
+
 }  // extern "C"

@@ -12,6 +12,11 @@
 //   semantics), survivors ascending -> per-class slots in the workspace.
 // Kernel 2: one workgroup per image: the dets_per_im-th largest score over all
 //   classes (radix select), keep score >= it, emit in class-major order.
+// Kernel 3 (optional, vd_detections_postfilter): the fork's steps after the
+//   limit (lib_vos/tools/vos_test.py:805-833): TEST.NMS_CROSS_CLASS (one NMS
+//   over every class's detections, survivors regrouped by class) and
+//   TEST.NUM_DET_PER_CLASS_PRE (per class, the top-k by score, rows reordered
+//   by score -- np.argsort(-s) read stably: ties by row order).
 #include "nms_block.hpp"
 #include "vosdet_internal.hpp"
 
@@ -235,6 +240,124 @@ int launch_box_detections(const float *rois, const float *cls_prob, const float 
                        score_thresh, nms_thresh, bw, ws);
     hipLaunchKernelGGL(det_limit_kernel, dim3(num_images), dim3(1024), 0, s, R_cap, K,
                        dets_per_im, det_cap, ws, dets_out, det_cls_out, det_count_out);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+// --------------------------------------------------------------------------
+// Kernel 3: in-place post-filter of one image's detections (class-major rows).
+// --------------------------------------------------------------------------
+static constexpr int kPostMax = 512;
+
+struct PostLds {
+    float x1[kPostMax], y1[kPostMax], x2[kPostMax], y2[kPostMax], sc[kPostMax];
+    float ox1[kPostMax], oy1[kPostMax], ox2[kPostMax], oy2[kPostMax], oar[kPostMax];
+    int cl[kPostMax], rank[kPostMax], pos[kPostMax];
+    uint64_t keys[kPostMax];
+    uint64_t mask[kPostMax * (kPostMax / 64)];
+    uint8_t keep_rank[kPostMax], alive[kPostMax];
+    int scratch[32];
+};
+
+__global__ __launch_bounds__(512) void det_postfilter_kernel(float *__restrict__ dets,
+                                                              int32_t *__restrict__ cls,
+                                                              int32_t *__restrict__ counts,
+                                                              int det_cap, float cross_thresh,
+                                                              int per_class_pre) {
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    PostLds &L = *reinterpret_cast<PostLds *>(lds_raw);
+    const int img = blockIdx.x, t = threadIdx.x;
+    const int k = min((int)counts[img], det_cap);  // det_cap <= kPostMax (launcher)
+    float *d = dets + (size_t)img * det_cap * 5;
+    int32_t *c = cls + (size_t)img * det_cap;
+    for (int i = t; i < k; i += blockDim.x) {
+        L.x1[i] = d[i * 5 + 0];
+        L.y1[i] = d[i * 5 + 1];
+        L.x2[i] = d[i * 5 + 2];
+        L.y2[i] = d[i * 5 + 3];
+        L.sc[i] = d[i * 5 + 4];
+        L.cl[i] = c[i];
+        L.alive[i] = 1;
+    }
+    __syncthreads();
+    if (cross_thresh > 0.f && k > 1) {
+        // utils.boxes.nms(all_dets, NMS_CROSS_CLASS): processing order (score
+        // desc, higher row first), cython_nms semantics
+        const int np2 = next_pow2(k);
+        for (int i = t; i < np2; i += blockDim.x)
+            L.keys[i] = i < k ? ((uint64_t)float_key(L.sc[i]) << 32) | (uint32_t)i : 0ull;
+        __syncthreads();
+        bitonic_sort_desc(L.keys, np2);
+        for (int r = t; r < k; r += blockDim.x) {
+            const int i = (int)(uint32_t)L.keys[r];
+            L.ox1[r] = L.x1[i];
+            L.oy1[r] = L.y1[i];
+            L.ox2[r] = L.x2[i];
+            L.oy2[r] = L.y2[i];
+            L.oar[r] = (L.x2[i] - L.x1[i] + 1) * (L.y2[i] - L.y1[i] + 1);
+        }
+        __syncthreads();
+        nms_build_mask_rows(L.ox1, L.oy1, L.ox2, L.oy2, L.oar, k, cross_thresh, L.mask,
+                            wave_id(), num_waves());
+        __syncthreads();
+        if (wave_id() == 0) nms_resolve_wave(L.mask, k, L.keep_rank);
+        __syncthreads();
+        for (int r = t; r < k; r += blockDim.x) L.alive[(int)(uint32_t)L.keys[r]] = L.keep_rank[r];
+        __syncthreads();
+    }
+    // rank within the class: by (score desc, row asc) with the per-class top-k,
+    // else by row (the order is unchanged)
+    for (int i = t; i < k; i += blockDim.x) {
+        int rk = 0;
+        if (L.alive[i]) {
+            for (int j = 0; j < k; ++j) {
+                if (!L.alive[j] || L.cl[j] != L.cl[i]) continue;
+                if (per_class_pre > 0)
+                    rk += (L.sc[j] > L.sc[i]) || (L.sc[j] == L.sc[i] && j < i);
+                else
+                    rk += j < i;
+            }
+        }
+        L.rank[i] = rk;
+    }
+    __syncthreads();
+    if (per_class_pre > 0)
+        for (int i = t; i < k; i += blockDim.x)
+            if (L.rank[i] >= per_class_pre) L.alive[i] = 0;
+    __syncthreads();
+    for (int i = t; i < k; i += blockDim.x) {
+        int p = -1;
+        if (L.alive[i]) {
+            p = 0;
+            for (int j = 0; j < k; ++j)
+                p += L.alive[j] && (L.cl[j] < L.cl[i] || (L.cl[j] == L.cl[i] && L.rank[j] < L.rank[i]));
+        }
+        L.pos[i] = p;
+    }
+    __syncthreads();
+    int n = 0;
+    for (int i = t; i < k; i += blockDim.x) n += L.alive[i];
+    n = block_sum(n, L.scratch);
+    for (int i = t; i < k; i += blockDim.x) {
+        const int p = L.pos[i];
+        if (p < 0) continue;
+        d[p * 5 + 0] = L.x1[i];
+        d[p * 5 + 1] = L.y1[i];
+        d[p * 5 + 2] = L.x2[i];
+        d[p * 5 + 3] = L.y2[i];
+        d[p * 5 + 4] = L.sc[i];
+        c[p] = L.cl[i];
+    }
+    if (t == 0) counts[img] = n;
+}
+
+int launch_detections_postfilter(float *dets, int32_t *cls, int32_t *counts, int num_images,
+                                 int det_cap, float nms_cross_class, int num_det_per_class_pre,
+                                 hipStream_t s) {
+    if (num_images < 1 || det_cap < 1) return VD_ERR_ARG;
+    if (det_cap > kPostMax) return VD_ERR_SHAPE;
+    if (!(nms_cross_class > 0.f) && num_det_per_class_pre <= 0) return VD_OK;
+    hipLaunchKernelGGL(det_postfilter_kernel, dim3(num_images), dim3(512), sizeof(PostLds), s,
+                       dets, cls, counts, det_cap, nms_cross_class, num_det_per_class_pre);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 

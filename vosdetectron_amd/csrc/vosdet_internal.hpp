@@ -108,4 +108,8 @@ int launch_paste_masks(const float *masks, int M, int R, const float *boxes, int
 int launch_mask_rle(const uint8_t *planes, int M, int H, int W, uint32_t *counts, int cap,
                     int32_t *ncounts, hipStream_t s);
 
+int launch_detections_postfilter(float *dets, int32_t *cls, int32_t *counts, int num_images,
+                                 int det_cap, float nms_cross_class, int num_det_per_class_pre,
+                                 hipStream_t s);
+
 }  // namespace vd

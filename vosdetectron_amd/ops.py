@@ -430,7 +430,7 @@ def collect_distribute(level_rois, level_probs, level_counts, post_nms_topN: int
 
 def box_detections(rois, cls_prob, bbox_pred, roi_count, im_scale, im_hw, score_thresh=0.05,
                    nms_thresh=0.5, dets_per_im=100, bbox_reg_weights=(10., 10., 5., 5.),
-                   det_cap=256, out=None):
+                   det_cap=256, out=None, nms_cross_class=0., num_det_per_class_pre=0):
     """Decode + clip + per-class NMS + detections limit.  rois [N,R,5],
     cls_prob [N,R,K], bbox_pred [N,R,4K] -> (dets [N,cap,5], cls int32 [N,cap],
     counts int32 [N])."""
@@ -456,6 +456,11 @@ def box_detections(rois, cls_prob, bbox_pred, roi_count, im_scale, im_hw, score_
                                   ctypes.cast(w, ctypes.c_void_p), det_cap, dets.data_ptr(),
                                   cls.data_ptr(), cnt.data_ptr(), ws.data_ptr(), ws.numel(),
                                   _stream()), "vd_box_detections")
+    if nms_cross_class > 0 or num_det_per_class_pre > 0:  # the fork's vos_test.py:805-833
+        check(lib().vd_detections_postfilter(dets.data_ptr(), cls.data_ptr(), cnt.data_ptr(), N,
+                                             det_cap, float(np.float32(nms_cross_class)),
+                                             int(num_det_per_class_pre), _stream()),
+              "vd_detections_postfilter")
     return dets, cls, cnt
 
 
