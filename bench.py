@@ -208,6 +208,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=2)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--timers", action="store_true",
+                    help="after the timed steps, run --steps more with per-stage HIP-event "
+                         "timers and report stages_ms (not part of the timed region)")
     ap.add_argument("--seq-len", type=int, default=50,
                     help="VOS configs: frames per synthetic sequence (hidden states reset)")
     args = ap.parse_args()
@@ -287,6 +290,14 @@ def main():
         dt = float(t.item())
     dets_per_frame = float(np.mean(out["counts_host"]))
 
+    stages = None
+    if args.timers:
+        pipe.enable_timers()
+        for _ in range(args.steps):
+            step()
+        stages = {k: round(v * 1e3, 3) for k, v in pipe.timer_summary().items()}
+        pipe.enable_timers(False)
+
     roof = None
     if not args.no_roofline and rank == 0:
         roof = measure_roialign_roofline(dev)
@@ -316,6 +327,8 @@ def main():
                        "layout": args.layout, "dets_per_frame": dets_per_frame},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if stages:
+            line["stages_ms"] = stages
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -131,3 +131,17 @@ def test_end_to_end_vs_independent_cpu(setup):
             mask_err.append(np.abs(gm[same[j]] - masks[i]).max())
     assert matched >= 0.9 * len(sc), (matched, len(sc))
     assert np.median(mask_err) < 1e-3
+
+
+def test_stage_timers(setup):
+    """HIP-event stage timers (the reference's im_detect_all timers dict)."""
+    cfg, model, sd, pipe, frame, out = setup
+    pipe.enable_timers()
+    try:
+        for _ in range(2):
+            pipe.run(torch.from_numpy(frame[None]).to(DEV))
+        s = pipe.timer_summary()
+        assert set(s) == {"conv_body", "proposals", "box_head", "misc_bbox", "im_detect_mask"}
+        assert all(v > 0 for v in s.values()) and pipe.timers["conv_body"].calls == 2
+    finally:
+        pipe.enable_timers(False)

@@ -204,16 +204,17 @@ class C4FramePipeline(FramePipeline):
                                 roi_order=order, out_layout="nhwc")
         return out.permute(0, 3, 1, 2)  # NCHW view, channels_last memory
 
-    @torch.no_grad()
-    def run(self, frames: torch.Tensor, keep_intermediates: bool = False):
+    def _run(self, frames: torch.Tensor, keep_intermediates: bool = False):
         cfg, tst = self.cfg, self.cfg.TEST
         F_ = frames.shape[0]
         res4 = self.backbone(frames)
+        self._mark("conv_body")
         prob, delta = self.model.RPN.outputs(res4)
         lrois, lprobs, lcnt = ops.generate_proposals(
             [prob.contiguous()], [delta.contiguous()], self.anchors, [self.scale],
             self.im_info[:F_], tst.RPN_PRE_NMS_TOP_N, tst.RPN_POST_NMS_TOP_N,
             tst.RPN_NMS_THRESH, tst.RPN_MIN_SIZE)
+        self._mark("proposals")
         post = tst.RPN_POST_NMS_TOP_N
         rois, rcnt = lrois[:, 0].contiguous(), lcnt[:, 0].contiguous()
         res4_nhwc = res4.permute(0, 2, 3, 1)
@@ -226,6 +227,7 @@ class C4FramePipeline(FramePipeline):
         bf = self._roi_feat(res4_nhwc, flat, fr.ROI_XFORM_RESOLUTION, fr.ROI_XFORM_SAMPLING_RATIO)
         x = self.model.Box_Head.head(bf)
         cls_prob, bbox_pred = self.model.Box_Outs(x)
+        self._mark("box_head")
         K = cls_prob.shape[1]
         bbox_pred = self.model.Box_Outs.per_class_deltas(bbox_pred, K)
         dets, dcls, dcnt = ops.box_detections(
@@ -234,6 +236,7 @@ class C4FramePipeline(FramePipeline):
             tst.DETECTIONS_PER_IM, cfg.MODEL.BBOX_REG_WEIGHTS, self.det_cap,
             nms_cross_class=tst.NMS_CROSS_CLASS, num_det_per_class_pre=tst.NUM_DET_PER_CLASS_PRE)
         counts = dcnt.cpu().tolist()
+        self._mark("misc_bbox")
         if max(counts) > self.det_cap:
             raise RuntimeError("detections exceed det_cap=%d: %s" % (self.det_cap, counts))
         out = {"dets": dets, "classes": dcls, "counts": dcnt, "counts_host": counts,
@@ -260,4 +263,5 @@ class C4FramePipeline(FramePipeline):
         out["masks"] = self.model.Mask_Outs.selected(y, mcls)
         out["mask_rois"] = mrois
         out["mask_feat"] = mf
+        self._mark("im_detect_mask")
         return out

@@ -6,6 +6,7 @@ because the training/dataset keys are out of scope).
 """
 from __future__ import annotations
 
+import ast
 import copy
 import math
 
@@ -44,7 +45,7 @@ def default_cfg() -> AttrDict:
             TRANS_FUNC="bottleneck_transformation", STEM_FUNC="basic_bn_stem",
             SHORTCUT_FUNC="basic_bn_shortcut", RES5_DILATION=1, USE_GN=False),
         FPN=_d(  # config.py:680-726
-            FPN_ON=True, DIM=256, COARSEST_STRIDE=32, MULTILEVEL_ROIS=True, MULTILEVEL_RPN=True,
+            FPN_ON=False, DIM=256, COARSEST_STRIDE=32, MULTILEVEL_ROIS=False, MULTILEVEL_RPN=False,
             ROI_CANONICAL_SCALE=224, ROI_CANONICAL_LEVEL=4, ROI_MAX_LEVEL=5, ROI_MIN_LEVEL=2,
             RPN_MAX_LEVEL=6, RPN_MIN_LEVEL=2, RPN_ASPECT_RATIOS=(0.5, 1, 2),
             RPN_ANCHOR_START_SIZE=32, RPN_COLLECT_SCALE=1, EXTRA_CONV_LEVELS=False,
@@ -75,6 +76,17 @@ def default_cfg() -> AttrDict:
     )
 
 
+def _decode(v):
+    """config.py _decode_cfg_value: strings that are Python literals (e.g. the
+    YAML text "(32, 64, 128, 256, 512)") become values."""
+    if isinstance(v, str):
+        try:
+            return ast.literal_eval(v)
+        except (ValueError, SyntaxError):
+            return v
+    return v
+
+
 def _merge(a, b):
     for k, v in a.items():
         if k not in b:
@@ -82,6 +94,7 @@ def _merge(a, b):
         if isinstance(v, dict) and isinstance(b[k], dict):
             _merge(v, b[k])
         else:
+            v = _decode(v)
             if isinstance(b[k], tuple) and isinstance(v, (list, tuple)):
                 v = tuple(v)
             b[k] = v
@@ -106,6 +119,7 @@ def load_cfg(path: str | None = None, overrides: dict | None = None) -> AttrDict
 # (values from configs/baselines/*.yaml of the reference).
 def e2e_mask_rcnn_R_50_FPN_1x() -> AttrDict:
     return load_cfg(overrides={
+        "FPN.FPN_ON": True, "FPN.MULTILEVEL_ROIS": True, "FPN.MULTILEVEL_RPN": True,
         "MODEL.CONV_BODY": "FPN.fpn_ResNet50_conv5_body", "MODEL.FASTER_RCNN": True,
         "MODEL.MASK_ON": True, "FAST_RCNN.ROI_BOX_HEAD": "fast_rcnn_heads.roi_2mlp_head",
         "FAST_RCNN.ROI_XFORM_METHOD": "RoIAlign", "FAST_RCNN.ROI_XFORM_RESOLUTION": 7,
@@ -126,8 +140,7 @@ def e2e_mask_rcnn_R_50_C4_1x() -> AttrDict:
     (ROI_XFORM_SAMPLING_RATIO default 0), RPN pre/post 6000/1000."""
     return load_cfg(overrides={
         "MODEL.CONV_BODY": "ResNet.ResNet50_conv4_body", "MODEL.FASTER_RCNN": True,
-        "MODEL.MASK_ON": True, "FPN.FPN_ON": False, "FPN.MULTILEVEL_ROIS": False,
-        "FPN.MULTILEVEL_RPN": False, "RPN.SIZES": (32, 64, 128, 256, 512),
+        "MODEL.MASK_ON": True, "RPN.SIZES": (32, 64, 128, 256, 512),
         "FAST_RCNN.ROI_BOX_HEAD": "ResNet.ResNet_roi_conv5_head",
         "FAST_RCNN.ROI_XFORM_METHOD": "RoIAlign", "FAST_RCNN.ROI_XFORM_RESOLUTION": 14,
         "FAST_RCNN.ROI_XFORM_SAMPLING_RATIO": 0,
@@ -161,6 +174,7 @@ def vos_R_101_FPN_3x_gn_static_davis() -> AttrDict:
         "MODEL.CONV_BODY": "FPN.fpn_ResNet101_conv5_body", "MODEL.FASTER_RCNN": True,
         "MODEL.MASK_ON": True, "MODEL.CLS_AGNOSTIC_BBOX_REG": True,
         "MODEL.NUM_CLASSES": 145, "MODEL.IDENTITY_TRAINING": False,
+        "FPN.FPN_ON": True, "FPN.MULTILEVEL_ROIS": True, "FPN.MULTILEVEL_RPN": True,
         "FPN.USE_GN": True, "FPN.COARSEST_STRIDE": 64, "FPN.RPN_ANCHOR_START_SIZE": 32,
         "FPN.ROI_CANONICAL_SCALE": 224,
         "RESNETS.STRIDE_1X1": False, "RESNETS.TRANS_FUNC": "bottleneck_gn_transformation",

@@ -28,6 +28,22 @@ import torch
 from . import ops
 
 
+class StageTimer:
+    """utils/timer.Timer's accounting (total_time, calls, average_time) fed with
+    HIP-event stage times instead of time.time() tic/toc."""
+
+    def __init__(self, name: str):
+        self.name = name
+        self.total_time = 0.
+        self.calls = 0
+        self.average_time = 0.
+
+    def add(self, seconds: float):
+        self.total_time += seconds
+        self.calls += 1
+        self.average_time = self.total_time / self.calls
+
+
 class FramePipeline:
     def __init__(self, model, cfg, frame_hw=(800, 1333), batch=1, channels_last=False,
                  det_cap=256, device="cuda"):
@@ -65,9 +81,37 @@ class FramePipeline:
             self.rpn_scales = [1. / 2 ** l for l in self.rpn_levels]
             self.roi_levels = list(range(cfg.FPN.ROI_MIN_LEVEL, cfg.FPN.ROI_MAX_LEVEL + 1))
             self.roi_scales = [1. / 2 ** l for l in self.roi_levels]
-        self.timers = None
+        self.timers = None  # enable_timers(): per-stage HIP-event timing
+        self._marks = None
 
     # ------------------------------------------------------------------ #
+    # tracing: the reference threads a defaultdict(Timer) through im_detect_all
+    # (lib/core/test.py:62-107, utils/timer.py:11-35, wall clock); here each
+    # stage boundary records a HIP event on the launch stream, so the stage
+    # times are device times and timing never adds a synchronisation.
+    def enable_timers(self, on: bool = True):
+        self.timers = {} if on else None
+        return self
+
+    def _mark(self, name: str):
+        if self._marks is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self._marks.append((name, ev))
+
+    def _collect_marks(self):
+        marks, self._marks = self._marks, None
+        if not marks:
+            return
+        marks[-1][1].synchronize()
+        for (_, a), (name, b) in zip(marks[:-1], marks[1:]):
+            t = self.timers.setdefault(name, StageTimer(name))
+            t.add(a.elapsed_time(b) / 1e3)
+
+    def timer_summary(self):
+        """{stage: average seconds per call} (Timer.average_time of the reference)."""
+        return {k: v.average_time for k, v in (self.timers or {}).items()}
+
     def backbone(self, frames):
         nhwc = self.channels_last
         blob = ops.image_to_blob(frames, self.lut, self.Hp, self.Wp, nhwc=nhwc)
@@ -91,10 +135,23 @@ class FramePipeline:
         """frames: F x H x W x 3 uint8 BGR on the device.  Returns a dict of device
         tensors: dets [F,cap,5] (x1,y1,x2,y2,score), classes [F,cap], counts [F]
         (host list too), masks [M,28,28] for the M = sum(counts) detections in
-        (frame, class, proposal) order."""
+        (frame, class, proposal) order.  Stage marks (enable_timers): conv_body,
+        proposals, box_head (together the reference's im_detect_bbox), misc_bbox,
+        im_detect_mask."""
+        if self.timers is not None:
+            self._marks = []
+            self._mark("start")
+        try:
+            return self._run(frames, keep_intermediates)
+        finally:
+            if self.timers is not None:
+                self._collect_marks()
+
+    def _run(self, frames: torch.Tensor, keep_intermediates: bool = False):
         cfg = self.cfg
         F = frames.shape[0]
         feats = self.backbone(frames)
+        self._mark("conv_body")
         # RPN heads on P2..P6 (finest first for the proposal kernel)
         probs, deltas = [], []
         for lvl in self.rpn_levels:
@@ -109,6 +166,7 @@ class FramePipeline:
         post = int(tst.RPN_POST_NMS_TOP_N * cfg.FPN.RPN_COLLECT_SCALE + 0.5)
         rois, rlvl, rcnt = ops.collect_distribute(lrois, lprobs, lcnt, post,
                                                   cfg.FPN.ROI_MIN_LEVEL, cfg.FPN.ROI_MAX_LEVEL)
+        self._mark("proposals")
         pyr = self.nhwc_pyramid(feats)
         fr = cfg.FAST_RCNN
         flat_rois, flat_lvl = rois.view(-1, 5), rlvl.view(-1)
@@ -119,6 +177,7 @@ class FramePipeline:
                                      out_layout="nhwc" if fast else "nchw")
         x = self.model.Box_Head.mlp_nhwc(box_feat) if fast else self.model.Box_Head.mlp(box_feat)
         cls_prob, bbox_pred = self.model.Box_Outs(x)
+        self._mark("box_head")
         K = cls_prob.shape[1]
         bbox_pred = self.model.Box_Outs.per_class_deltas(bbox_pred, K)
         dets, dcls, dcnt = ops.box_detections(
@@ -127,6 +186,7 @@ class FramePipeline:
             tst.DETECTIONS_PER_IM, cfg.MODEL.BBOX_REG_WEIGHTS, self.det_cap,
             nms_cross_class=tst.NMS_CROSS_CLASS, num_det_per_class_pre=tst.NUM_DET_PER_CLASS_PRE)
         counts = dcnt.cpu().tolist()  # the one host read: sizes the mask batch
+        self._mark("misc_bbox")
         if max(counts) > self.det_cap:
             raise RuntimeError("detections exceed det_cap=%d: %s" % (self.det_cap, counts))
         out = {"dets": dets, "classes": dcls, "counts": dcnt, "counts_host": counts,
@@ -166,12 +226,14 @@ class FramePipeline:
             up = self.model.Mask_Head.head_nhwc(mfeat)
             out["masks"] = self.model.Mask_Outs.selected_from_up(up, mcls)[:M]
             out["mask_feat"] = mfeat[:M].permute(0, 3, 1, 2)
+            self._mark("im_detect_mask")
             return out
         mfeat = ops.roi_align_fpn(pyr, self.roi_scales, mrois, mlvl, mc.ROI_XFORM_RESOLUTION,
                                   mc.ROI_XFORM_SAMPLING_RATIO)
         mh = self.model.Mask_Head.head(mfeat)
         out["masks"] = self.model.Mask_Outs.selected(mh, mcls)
         out["mask_feat"] = mfeat
+        self._mark("im_detect_mask")
         return out
 
 
