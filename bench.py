@@ -202,7 +202,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=8, help="frames per GPU per step")
+    ap.add_argument("--batch", type=int, default=16, help="frames per GPU per step")
     ap.add_argument("--config", default="e2e_mask_rcnn_R-50-FPN_1x")
     ap.add_argument("--layout", default="nhwc", choices=["nchw", "nhwc"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -259,19 +259,30 @@ def main():
     from vosdetectron_amd.runner import ResultGatherer
     gatherer = ResultGatherer(F, pipe.det_cap, cfg.MRCNN.RESOLUTION, world, dev)
 
+    pending = [None]
+
+    def drain():  # the previous step's gather has landed (stream-ordered)
+        if pending[0] is not None:
+            pending[0].wait()
+            pending[0] = None
+
     def step():
         t = step_no[0]
         step_no[0] += 1
         if vos and t % args.seq_len == 0:
             pipe.reset()
         out = pipe.run(ring[t % len(ring)])
-        if world > 1:  # one all_gather per result tensor over RCCL (runner.py)
-            gatherer.gather(out["dets"], out["classes"], out["counts"], out["masks"],
-                            out["counts_host"])
+        if world > 1:
+            # ONE packed all_gather per step over RCCL (runner.py), left in flight
+            # on RCCL's stream while the next step computes; at most one in flight
+            drain()
+            pending[0] = gatherer.gather_async(out["dets"], out["classes"], out["counts"],
+                                               out["masks"], out["counts_host"])
         return out
 
     for _ in range(args.warmup):
         out = step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -279,6 +290,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = step()
+    drain()  # the last step's gather is inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -295,6 +307,7 @@ def main():
         pipe.enable_timers()
         for _ in range(args.steps):
             step()
+        drain()
         stages = {k: round(v * 1e3, 3) for k, v in pipe.timer_summary().items()}
         pipe.enable_timers(False)
 

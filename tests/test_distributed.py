@@ -41,9 +41,19 @@ def _worker(rank, world, port, outq):
     g = ResultGatherer(3, 16, 28, world, "cpu")
     out = g.gather(torch.from_numpy(dets), torch.from_numpy(cls), torch.from_numpy(counts),
                    torch.from_numpy(masks), counts.tolist())
+    # double-buffered async path: two gathers in flight order, second slot
+    p1 = g.gather_async(torch.from_numpy(dets), torch.from_numpy(cls), torch.from_numpy(counts),
+                        torch.from_numpy(masks), counts.tolist())
+    r1 = {k: v.clone() for k, v in p1.wait().items()}
+    p2 = g.gather_async(torch.from_numpy(dets) + 1, torch.from_numpy(cls),
+                        torch.from_numpy(counts), torch.from_numpy(masks), counts.tolist())
+    r2 = p2.wait()
+    same = all(torch.equal(r1[k], out[k]) for k in out)
+    shifted = torch.equal(r2["dets"], out["dets"] + 1) and torch.equal(r2["masks"], out["masks"])
     if rank == 0:
         outq.put({k: v.numpy().copy() for k, v in out.items()})
         outq.put(shard_frames(10, world, 1))
+        outq.put((same, shifted))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -58,6 +68,8 @@ def test_gather_world2_gloo():
         p.start()
     got = q.get(timeout=120)
     shard = q.get(timeout=60)
+    same, shifted = q.get(timeout=60)
+    assert same and shifted
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0

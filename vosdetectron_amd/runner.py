@@ -23,38 +23,74 @@ def shard_frames(n_frames: int, world: int, rank: int) -> Sequence[int]:
     return [int(i) for i in np.array_split(np.arange(n_frames), world)[rank]]
 
 
+class PendingGather:
+    """An in-flight all_gather (async_op) of one buffer slot."""
+
+    def __init__(self, work, gatherer, rbuf):
+        self.work, self.g, self.rbuf = work, gatherer, rbuf
+
+    def wait(self) -> Dict[str, torch.Tensor]:
+        """Orders the caller's stream after the collective; returns the gathered
+        results ([world*F, ...], rank-major)."""
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+        return self.g._views(self.rbuf)
+
+
 class ResultGatherer:
-    """Pads each rank's per-frame results to fixed shapes and all-gathers them."""
+    """Packs each rank's per-frame results -- dets [F,D,5], classes [F,D], counts
+    [F], class-selected masks padded to [F,D,R,R] -- into ONE flat fp32 buffer
+    (int32 fields bit-cast) and all-gathers it in a single collective.  Two
+    buffer slots alternate, so `gather_async` of step t can run on RCCL's stream
+    while step t+1 computes; `wait()` before the slot is reused (the caller
+    keeps at most one gather in flight)."""
 
     def __init__(self, frames_per_rank: int, det_cap: int, mask_res: int, world: int,
                  device, with_masks: bool = True):
-        F, D = frames_per_rank, det_cap
-        self.F, self.D, self.world, self.with_masks = F, D, world, with_masks
-        self.pad_masks = torch.zeros((F, D, mask_res, mask_res), device=device)
-        self.g_dets = torch.zeros((world * F, D, 5), device=device)
-        self.g_cls = torch.zeros((world * F, D), dtype=torch.int32, device=device)
-        self.g_cnt = torch.zeros((world * F,), dtype=torch.int32, device=device)
-        self.g_masks = torch.zeros((world * F, D, mask_res, mask_res), device=device)
+        F, D, R = frames_per_rank, det_cap, mask_res
+        self.F, self.D, self.R, self.world, self.with_masks = F, D, R, world, with_masks
+        self.o_cls = F * D * 5
+        self.o_cnt = self.o_cls + F * D
+        self.o_msk = self.o_cnt + F
+        self.L = self.o_msk + (F * D * R * R if with_masks else 0)
+        self.send = [torch.zeros((self.L,), device=device) for _ in range(2)]
+        self.recv = [torch.zeros((world, self.L), device=device) for _ in range(2)]
+        self.slot = 0
 
-    def pack_masks(self, masks: torch.Tensor, counts: List[int]) -> torch.Tensor:
-        self.pad_masks.zero_()
-        o = 0
-        for f, c in enumerate(counts):
-            if c:
-                self.pad_masks[f, :c] = masks[o:o + c]
-            o += c
-        return self.pad_masks
-
-    def gather(self, dets: torch.Tensor, classes: torch.Tensor, counts: torch.Tensor,
-               masks: torch.Tensor, counts_host: List[int]) -> Dict[str, torch.Tensor]:
-        """dets [F,D,5], classes [F,D] int32, counts [F] int32, masks [M,R,R]."""
-        if self.world == 1:
-            return {"dets": dets, "classes": classes, "counts": counts,
-                    "masks": self.pack_masks(masks, counts_host) if self.with_masks else None}
-        dist.all_gather_into_tensor(self.g_dets, dets.contiguous())
-        dist.all_gather_into_tensor(self.g_cls, classes.contiguous())
-        dist.all_gather_into_tensor(self.g_cnt, counts.contiguous())
+    def _pack(self, buf, dets, classes, counts, masks, counts_host):
+        F, D, R = self.F, self.D, self.R
+        buf[:self.o_cls].copy_(dets.reshape(-1))
+        buf[self.o_cls:self.o_cnt].view(torch.int32).copy_(classes.reshape(-1))
+        buf[self.o_cnt:self.o_msk].view(torch.int32).copy_(counts.reshape(-1))
         if self.with_masks:
-            dist.all_gather_into_tensor(self.g_masks, self.pack_masks(masks, counts_host))
-        return {"dets": self.g_dets, "classes": self.g_cls, "counts": self.g_cnt,
-                "masks": self.g_masks if self.with_masks else None}
+            pm = buf[self.o_msk:].view(F, D, R, R)
+            pm.zero_()
+            o = 0
+            for f, c in enumerate(counts_host):
+                if c:
+                    pm[f, :c] = masks[o:o + c]
+                o += c
+
+    def _views(self, rb):
+        W, F, D, R = rb.shape[0], self.F, self.D, self.R
+        v = {"dets": rb[:, :self.o_cls].reshape(W * F, D, 5),
+             "classes": rb[:, self.o_cls:self.o_cnt].contiguous().view(torch.int32)
+                        .reshape(W * F, D),
+             "counts": rb[:, self.o_cnt:self.o_msk].contiguous().view(torch.int32).reshape(W * F),
+             "masks": rb[:, self.o_msk:].reshape(W * F, D, R, R) if self.with_masks else None}
+        return v
+
+    def gather_async(self, dets: torch.Tensor, classes: torch.Tensor, counts: torch.Tensor,
+                     masks: torch.Tensor, counts_host: List[int]) -> PendingGather:
+        """dets [F,D,5], classes [F,D] int32, counts [F] int32, masks [M,R,R]."""
+        s = self.slot
+        self.slot ^= 1
+        self._pack(self.send[s], dets, classes, counts, masks, counts_host)
+        if self.world == 1:
+            return PendingGather(None, self, self.send[s].view(1, -1))
+        work = dist.all_gather_into_tensor(self.recv[s].view(-1), self.send[s], async_op=True)
+        return PendingGather(work, self, self.recv[s])
+
+    def gather(self, dets, classes, counts, masks, counts_host) -> Dict[str, torch.Tensor]:
+        return self.gather_async(dets, classes, counts, masks, counts_host).wait()
