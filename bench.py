@@ -93,15 +93,14 @@ def xcd_order(rois, lvls, n_xcd=8):
 
 
 ROIALIGN_KERNEL = {"3": "vd::roi_align_fpn_nhwc_kernel<7,2,2> (reference order)",
-                   "8": "vd::roi_align_fpn_nhwc_sep_kernel<2,false,false,true> (separable, nt stores)",
-                   "20": "vd::roi_align_fpn_nhwc_sep_kernel<2,false,false,false> (separable)"}
+                   "8": "vd::roi_align_fpn_nhwc_sep_kernel<2,true> (separable, nt stores)",
+                   "16": "vd::roi_align_fpn_nhwc_xslice2_kernel<2,32> (XCD channel slices)"}
 
 
 # rocprofv3 --pmc passes of this exact launch (tools/prof_roialign.sh, separate
 # passes per counter group; FETCH_SIZE doubled per the MI355X guide): L2<->fabric
 # bytes per launch, committed under profiles/ and reported as "traffic".
-ROIALIGN_PMC = {"8": "separable_v8nt_xcd.json", "20": "separable_v8_xcd.json",
-                "3": "rowkernel_v3_xcd.json"}
+ROIALIGN_PMC = {"8": "separable_v8nt_xcd.json", "3": "rowkernel_v3_xcd.json"}
 
 
 def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=None,

@@ -158,7 +158,7 @@ def test_roi_pool_backward_matches_scatter():
     assert np.array_equal(ft.grad.cpu().numpy().ravel(), ref)
 
 
-@pytest.mark.parametrize("variant", [None, "8", "9", "13", "14"])
+@pytest.mark.parametrize("variant", [None, "3", "16"])
 @pytest.mark.parametrize("P,C", [(7, 256), (14, 256), (7, 64), (14, 520)])
 def test_roi_align_fpn_separable_within_tolerance(P, C, variant, monkeypatch):
     """Separable NHWC kernel (variant 8): same sampling, summation re-associated

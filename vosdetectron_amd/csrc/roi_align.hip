@@ -333,10 +333,6 @@ __device__ __forceinline__ RowTaps<SR> row_taps(const RoiGeom &g, int ph) {
     return t;
 }
 
-__device__ __forceinline__ float4 fma4(float w, const float4 &a, const float4 &c) {
-    return make_float4(fmaf(w, a.x, c.x), fmaf(w, a.y, c.y), fmaf(w, a.z, c.z), fmaf(w, a.w, c.w));
-}
-
 template <int SR>
 struct TapCol {
     float4 f[2 * SR];
@@ -352,32 +348,26 @@ __device__ __forceinline__ TapCol<SR> load_column(const RowTaps<SR> &t, const fl
     return c;
 }
 
-template <int SR, bool FMA>
+template <int SR>
 __device__ __forceinline__ float4 combine_column(const RowTaps<SR> &t, const TapCol<SR> &c) {
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int k = 0; k < 2 * SR; ++k)
         if (t.alive[k]) {
-            if (FMA) {
-                v = fma4(t.w[k], c.f[k], v);
-            } else {
-                v.x += t.w[k] * c.f[k].x;
-                v.y += t.w[k] * c.f[k].y;
-                v.z += t.w[k] * c.f[k].z;
-                v.w += t.w[k] * c.f[k].w;
-            }
+            v.x += t.w[k] * c.f[k].x;
+            v.y += t.w[k] * c.f[k].y;
+            v.z += t.w[k] * c.f[k].z;
+            v.w += t.w[k] * c.f[k].w;
         }
     return v;
 }
 
-// PF: while the bins consume column x, the taps of column x+1 (the next one the
-// left-to-right sweep needs unless it skips) are already in flight.
 typedef float vf4 __attribute__((ext_vector_type(4)));
 
 // NT: output rows are written once and never re-read by this launch; storing
 // them non-temporal keeps them from evicting pyramid lines that overlapping
 // RoIs on the same XCD are about to re-read from L2.
-template <int SR, bool FMA, bool PF, bool NT = false>
+template <int SR, bool NT>
 __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
     FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
     const int *__restrict__ roi_order, int P, int out_nhwc, float *__restrict__ out) {
@@ -398,20 +388,11 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
         const bool active = c0 < C;
         const float *base = g.feat + (active ? c0 : 0);
         const RowTaps<SR> taps = row_taps<SR>(g, ph);
-        int cl = -1, ch = -1, pfc = -1;
+        int cl = -1, ch = -1;
         float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
-        TapCol<SR> pf;
         auto column = [&](int x) -> float4 {
-            if (PF) {
-                TapCol<SR> cur;
-                if (x == pfc) cur = pf;
-                else cur = load_column<SR>(taps, base, rowstride, (int64_t)x * C);
-                pfc = min(x + 1, W - 1);
-                pf = load_column<SR>(taps, base, rowstride, (int64_t)pfc * C);
-                return combine_column<SR, FMA>(taps, cur);
-            }
-            return combine_column<SR, FMA>(taps,
-                                           load_column<SR>(taps, base, rowstride, (int64_t)x * C));
+            return combine_column<SR>(taps,
+                                      load_column<SR>(taps, base, rowstride, (int64_t)x * C));
         };
         for (int pw = 0; pw < P; ++pw) {
             float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -430,15 +411,10 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
                     cl = xl;
                     ch = xh;
                 }
-                if (FMA) {
-                    acc = fma4(hx, va, acc);
-                    acc = fma4(lx, vb, acc);
-                } else {
-                    acc.x += hx * va.x + lx * vb.x;
-                    acc.y += hx * va.y + lx * vb.y;
-                    acc.z += hx * va.z + lx * vb.z;
-                    acc.w += hx * va.w + lx * vb.w;
-                }
+                acc.x += hx * va.x + lx * vb.x;
+                acc.y += hx * va.y + lx * vb.y;
+                acc.z += hx * va.z + lx * vb.z;
+                acc.w += hx * va.w + lx * vb.w;
             }
             acc = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
             if (!active) continue;
@@ -596,141 +572,6 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_xslice2_kernel(
     }
 }
 
-// Column-streamed separable row: the row's tap columns form the contiguous
-// range [xa, xb] (sample spacing bw/SR <= 1 px for every RoI the FPN level map
-// sends to P2-P5 at 7x7 / SR 2, except the largest on P5), so the wave walks it
-// left to right with the taps of the next DEPTH columns already in flight (a
-// static ring of raw loads: the memory-level parallelism the dependent
-// column-by-column fetch of roi_align_fpn_nhwc_sep_kernel lacks).  Samples are
-// consumed as soon as their right column has arrived; a bin is stored when its
-// last sample is done.
-template <int SR, int DEPTH>
-__global__ __launch_bounds__(512) void roi_align_fpn_nhwc_stream_kernel(
-    FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
-    const int *__restrict__ roi_order, int P, int out_nhwc, float *__restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) float tile[];  // [C][P][P] (NCHW out)
-    constexpr int T = 2 * SR;
-    const int r = roi_order ? roi_order[blockIdx.x] : (int)blockIdx.x;
-    int li = roi_level ? roi_level[r] : 0;
-    li = __builtin_amdgcn_readfirstlane(li);
-    const RoiGeom g = roi_geom(fa, C, rois + (int64_t)r * 5, li, P, P, SR);
-    const int chunks = (C + 255) / 256;
-    const int lane = lane_id();
-    const int W = g.W;
-    const int64_t rowstride = (int64_t)W * C;
-    const float inv = 1.f / g.count;
-    const int NS = P * SR;
-    // x geometry of sample j (identical for every row)
-    auto sample = [&](int j, int &xl, int &xh, float &lx) -> bool {
-        const int pw = j / SR, ix = j - pw * SR;
-        float x = g.sw + pw * g.bw + (ix + .5f) * g.bw / SR;
-        if (x < -1.0f || x > (float)W) return false;
-        if (x <= 0) x = 0;
-        xl = (int)x;
-        if (xl >= W - 1) { xh = xl = W - 1; x = (float)xl; } else xh = xl + 1;
-        lx = x - xl;
-        return true;
-    };
-    // valid samples are a contiguous index range [ja, jb); columns [xa, xb]
-    int ja = 0, jb = NS, xa = 0, xb = -1;
-    {
-        int xl, xh;
-        float lx;
-        while (ja < NS && !sample(ja, xl, xh, lx)) ++ja;
-        if (ja < NS) xa = xl;
-        while (jb > ja && !sample(jb - 1, xl, xh, lx)) --jb;
-        if (jb > ja) xb = xh;
-    }
-    const int ncols = xb - xa + 1;
-    for (int u = wave_id(); u < P * chunks; u += num_waves()) {
-        const int ph = u / chunks;
-        const int ck = u - ph * chunks;
-        const int c0 = ck * 256 + lane * 4;
-        const bool active = c0 < C;
-        const float *base = g.feat + (active ? c0 : 0);
-        const RowTaps<SR> taps = row_taps<SR>(g, ph);
-        const float *rp[T];
-#pragma unroll
-        for (int k = 0; k < T; ++k) rp[k] = base + taps.row[k] * rowstride;
-        auto store = [&](int pw, float4 a) {
-            if (!active) return;
-            a = make_float4(a.x * inv, a.y * inv, a.z * inv, a.w * inv);
-            if (out_nhwc) {
-                *reinterpret_cast<float4 *>(out + (((int64_t)r * P + ph) * P + pw) * C + c0) = a;
-            } else {
-                float *t = tile + (int64_t)c0 * P * P + ph * P + pw;
-                t[0] = a.x;
-                t[P * P] = a.y;
-                t[2 * P * P] = a.z;
-                t[3 * P * P] = a.w;
-            }
-        };
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        int j = 0;
-        // leading out-of-range samples (contribute 0)
-        for (; j < ja; ++j)
-            if (j % SR == SR - 1) { store(j / SR, acc); acc = make_float4(0.f, 0.f, 0.f, 0.f); }
-        float4 raw[DEPTH][T];
-        auto issue = [&](float4 (&dst)[T], int col) {
-            const int64_t off = (int64_t)min(col, xb) * C;
-#pragma unroll
-            for (int k = 0; k < T; ++k)
-                if (taps.alive[k]) dst[k] = ld4(rp[k] + off);
-        };
-#pragma unroll
-        for (int d = 0; d < DEPTH; ++d) issue(raw[d], xa + d);
-        float4 vprev = make_float4(0.f, 0.f, 0.f, 0.f);
-        // consume column xa + k from ring slot d, refill the slot with column + DEPTH
-        auto step = [&](int k, float4 (&slot)[T]) {
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int t = 0; t < T; ++t)
-                if (taps.alive[t]) {
-                    v.x += taps.w[t] * slot[t].x;
-                    v.y += taps.w[t] * slot[t].y;
-                    v.z += taps.w[t] * slot[t].z;
-                    v.w += taps.w[t] * slot[t].w;
-                }
-            if (k + DEPTH < ncols) issue(slot, xa + k + DEPTH);
-            const int x = xa + k;
-            int xl, xh;
-            float lx;
-            while (j < jb) {
-                sample(j, xl, xh, lx);
-                if (xh != x) break;
-                const float hx = 1.f - lx;
-                const float4 va = (xl == x) ? v : vprev;
-                acc.x += hx * va.x + lx * v.x;
-                acc.y += hx * va.y + lx * v.y;
-                acc.z += hx * va.z + lx * v.z;
-                acc.w += hx * va.w + lx * v.w;
-                if (j % SR == SR - 1) {
-                    store(j / SR, acc);
-                    acc = make_float4(0.f, 0.f, 0.f, 0.f);
-                }
-                ++j;
-            }
-            vprev = v;
-        };
-        for (int k = 0; k < ncols; k += DEPTH) {
-#pragma unroll
-            for (int d = 0; d < DEPTH; ++d)
-                if (k + d < ncols) step(k + d, raw[d]);
-        }
-        // trailing out-of-range samples
-        for (; j < NS; ++j)
-            if (j % SR == SR - 1) { store(j / SR, acc); acc = make_float4(0.f, 0.f, 0.f, 0.f); }
-    }
-    if (out_nhwc) return;
-    __syncthreads();
-    const int n4 = (C * P * P) / 4;
-    float4 *o4 = reinterpret_cast<float4 *>(out + (int64_t)r * C * P * P);
-    const float4 *t4 = reinterpret_cast<const float4 *>(tile);
-    for (int i = threadIdx.x; i < n4; i += blockDim.x) o4[i] = t4[i];
-    float *o = out + (int64_t)r * C * P * P;
-    for (int i = n4 * 4 + threadIdx.x; i < C * P * P; i += blockDim.x) o[i] = tile[i];
-}
-
 template <int P, int SR, int D>
 __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_kernel(
     FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
@@ -791,259 +632,6 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_kernel(
             o[(int64_t)c * P * P + rem] = tile[i];
         }
     }
-}
-
-// --------------------------------------------------------------------------
-// NHWC forward with the RoI footprint staged in LDS (C == 256, fixed P, SR).
-//
-// The P*SR x-samples of a RoI touch a sorted set of distinct columns D and the
-// P*SR y-samples a sorted set of distinct rows Y; every bilinear tap is a pixel
-// of the Y x D grid.  The grid is loaded into LDS once per RoI (one 1 KiB
-// global_load_lds per pixel = 256 fp32 channels), window by window when it is
-// larger than the LDS budget, and every one of the 4*P*P*SR*SR taps is then an
-// LDS read.  Each pixel crosses the L2/MALL once per RoI instead of once per
-// tap (4x-8x fewer fetches for the small RoIs that dominate P2).  Wave w owns
-// output column pw = w and accumulates acc[ph] in the reference's order.
-// --------------------------------------------------------------------------
-struct FootMeta {
-    int ncol, nrow;
-    int col[64], row[64];            // distinct tap columns / rows (pixel coords)
-    int xs_l[32], xs_h[32];          // per x-sample: slots in col[]
-    int ys_l[32], ys_h[32];          // per y-sample: slots in row[]
-    float lx[32], ly[32];
-    int vx[32], vy[32];
-};
-
-template <int NS>
-__device__ inline void build_axis(int n_lim, float start, float bin, int (&slots_l)[32],
-                                  int (&slots_h)[32], float (&frac)[32], int (&valid)[32],
-                                  int (&list)[64], int &count, int SRv) {
-    // serial, one lane: positions are non-decreasing, so the union of {lo, hi}
-    // over valid samples is built sorted by appending
-    int cnt = 0, last = -1;
-    for (int j = 0; j < NS; ++j) {
-        const int p = j / SRv, ix = j - p * SRv;
-        float v = start + p * bin + (ix + .5f) * bin / SRv;
-        const bool ok = !(v < -1.0f || v > (float)n_lim);
-        if (v <= 0) v = 0;
-        int lo = (int)v, hi;
-        if (lo >= n_lim - 1) { hi = lo = n_lim - 1; v = (float)lo; } else hi = lo + 1;
-        frac[j] = v - lo;
-        valid[j] = ok;
-        if (!ok) { slots_l[j] = slots_h[j] = 0; continue; }
-        if (lo > last) { list[cnt++] = lo; last = lo; }
-        slots_l[j] = (list[cnt - 1] == lo) ? cnt - 1 : cnt - 2;
-        if (hi > last) { list[cnt++] = hi; last = hi; }
-        slots_h[j] = (list[cnt - 1] == hi) ? cnt - 1 : cnt - 2;
-    }
-    count = cnt;
-}
-
-template <int P, int SR>
-__global__ __launch_bounds__(P * 64) void roi_align_fpn_nhwc_lds_kernel(
-    FpnLevels fa, const float *__restrict__ rois, const int *__restrict__ roi_level,
-    const int *__restrict__ roi_order, int budget_px, float *__restrict__ out) {
-    constexpr int C = 256;
-    constexpr int NS = P * SR;
-    extern __shared__ __attribute__((aligned(16))) float4 sm[];
-    __shared__ FootMeta meta;
-    const int r = roi_order ? roi_order[blockIdx.x] : (int)blockIdx.x;
-    int li = roi_level ? roi_level[r] : 0;
-    li = __builtin_amdgcn_readfirstlane(li);
-    const RoiGeom g = roi_geom(fa, C, rois + (int64_t)r * 5, li, P, P, SR);
-    const int wave = wave_id(), lane = lane_id();
-    if (threadIdx.x == 0)
-        build_axis<NS>(g.W, g.sw, g.bw, meta.xs_l, meta.xs_h, meta.lx, meta.vx, meta.col,
-                       meta.ncol, SR);
-    if (threadIdx.x == 64)
-        build_axis<NS>(g.H, g.sh, g.bh, meta.ys_l, meta.ys_h, meta.ly, meta.vy, meta.row,
-                       meta.nrow, SR);
-    __syncthreads();
-    const int ncol = meta.ncol, nrow = meta.nrow;
-    const int M = ncol > 0 ? budget_px / ncol : 0;  // rows per LDS window (>= 2)
-    const float *fbase = g.feat + lane * 4;
-    // this wave's column of bins: samples j = pw*SR + ix
-    const int pw = wave;
-    int xl[SR], xh[SR];
-    float lxv[SR];
-    bool vxv[SR];
-#pragma unroll
-    for (int ix = 0; ix < SR; ++ix) {
-        const int j = pw * SR + ix;
-        xl[ix] = meta.xs_l[j];
-        xh[ix] = meta.xs_h[j];
-        lxv[ix] = meta.lx[j];
-        vxv[ix] = meta.vx[j] != 0;
-    }
-    float4 acc[P];
-#pragma unroll
-    for (int ph = 0; ph < P; ++ph) acc[ph] = make_float4(0.f, 0.f, 0.f, 0.f);
-    int w0 = 0, w1 = 0;  // rows [w0, w1) of row[] are resident
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-        if (!meta.vy[i]) continue;  // whole sample row reads 0 (uniform)
-        const int yl = meta.ys_l[i], yh = meta.ys_h[i];
-        if (yh >= w1 || yl < w0) {  // slide the window (uniform across the block)
-            __syncthreads();
-            w0 = yl;
-            w1 = min(w0 + M, nrow);
-            const int npx = (w1 - w0) * ncol;
-            for (int p = wave; p < npx; p += P) {
-                const int ry = w0 + p / ncol, cx = p - (p / ncol) * ncol;
-                const float *src = fbase + ((int64_t)meta.row[ry] * g.W + meta.col[cx]) * C;
-                __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void *)src,
-                    (__attribute__((address_space(3))) void *)(sm + p * 64), 16, 0, 0);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-        }
-        const float ly = meta.ly[i], hy = 1.f - ly;
-        const float4 *top = sm + (yl - w0) * ncol * 64 + lane;
-        const float4 *bot = sm + (yh - w0) * ncol * 64 + lane;
-#pragma unroll
-        for (int ix = 0; ix < SR; ++ix) {
-            const float lx = lxv[ix], hx = 1.f - lx;
-            const float4 a = top[xl[ix] * 64], b = top[xh[ix] * 64];
-            const float4 c = bot[xl[ix] * 64], d = bot[xh[ix] * 64];
-            float4 t = acc[i / SR];
-            bilerp_acc(t, hy * hx, hy * lx, ly * hx, ly * lx, a, b, c, d);
-            if (vxv[ix]) acc[i / SR] = t;
-        }
-    }
-    __syncthreads();  // the window buffer becomes the [C][P][P] output tile
-    float *tile = reinterpret_cast<float *>(sm);
-#pragma unroll
-    for (int ph = 0; ph < P; ++ph) {
-        float *t = tile + (lane * 4) * (P * P) + ph * P + pw;
-        t[0] = acc[ph].x / g.count;
-        t[P * P] = acc[ph].y / g.count;
-        t[2 * P * P] = acc[ph].z / g.count;
-        t[3 * P * P] = acc[ph].w / g.count;
-    }
-    __syncthreads();
-    float4 *o4 = reinterpret_cast<float4 *>(out + (int64_t)r * C * P * P);
-    for (int i = threadIdx.x; i < C * P * P / 4; i += blockDim.x) o4[i] = sm[i];
-}
-
-// --------------------------------------------------------------------------
-// NHWC forward, channel-sliced per XCD (the product kernel for C % 32 == 0).
-//
-// Overlapping RoIs of one frame re-read the same pyramid pixels ~4.5x (sum of
-// per-RoI footprints / union), and a whole-pixel (1 KiB) working
-// set of the RoIs in flight does not fit a 4 MiB XCD L2, so those re-reads go
-// to the Infinity Cache.  Here block b pools channel slice s = b % S (32
-// channels = one 128-B line per pixel) of RoI order[b / S]: all blocks of a
-// slice land on one XCD (blocks b and b+8 share an XCD), so each XCD's L2 only
-// holds 1/8 of every pixel and the spatially sorted RoI stream re-reads it from
-// L2.  A lane group of 8 lanes (float4 each) owns one output bin; every tap is
-// one 128-B line, all 4*SR*SR taps of a bin are in flight together.  The bin
-// values are staged in LDS as [32][P*P] and written as one contiguous block.
-// --------------------------------------------------------------------------
-template <int SR>
-__device__ __forceinline__ float4 bin_value(const RoiGeom &g, int C, const float *base, int ph,
-                                            int pw, int gh, int gw) {
-    const int H = g.H, W = g.W;
-    const int64_t rowstride = (int64_t)W * C;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (SR > 0) {
-        constexpr int NK = SR > 0 ? SR * SR : 1;
-        float4 v[NK][4];
-        float wts[NK][4];
-        bool ok[NK];
-#pragma unroll
-        for (int iy = 0; iy < SR; ++iy) {
-            float y = g.sh + ph * g.bh + (iy + .5f) * g.bh / SR;
-            const bool vy = !(y < -1.0f || y > (float)H);
-            if (y <= 0) y = 0;
-            int yl = (int)y, yh;
-            if (yl >= H - 1) { yh = yl = H - 1; y = (float)yl; } else yh = yl + 1;
-            const float ly = y - yl, hy = 1.f - ly;
-#pragma unroll
-            for (int ix = 0; ix < SR; ++ix) {
-                float x = g.sw + pw * g.bw + (ix + .5f) * g.bw / SR;
-                const bool vx = !(x < -1.0f || x > (float)W);
-                if (x <= 0) x = 0;
-                int xl = (int)x, xh;
-                if (xl >= W - 1) { xh = xl = W - 1; x = (float)xl; } else xh = xl + 1;
-                const float lx = x - xl, hx = 1.f - lx;
-                const int k = iy * SR + ix;
-                v[k][0] = ld4(base + yl * rowstride + (int64_t)xl * C);
-                v[k][1] = ld4(base + yl * rowstride + (int64_t)xh * C);
-                v[k][2] = ld4(base + yh * rowstride + (int64_t)xl * C);
-                v[k][3] = ld4(base + yh * rowstride + (int64_t)xh * C);
-                wts[k][0] = hy * hx;
-                wts[k][1] = hy * lx;
-                wts[k][2] = ly * hx;
-                wts[k][3] = ly * lx;
-                ok[k] = vy && vx;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < SR * SR; ++k) {
-            float4 t = acc;
-            bilerp_acc(t, wts[k][0], wts[k][1], wts[k][2], wts[k][3], v[k][0], v[k][1], v[k][2],
-                       v[k][3]);
-            if (ok[k]) acc = t;
-        }
-        return acc;
-    }
-    for (int iy = 0; iy < gh; ++iy) {
-        float y = g.sh + ph * g.bh + (iy + .5f) * g.bh / gh;
-        for (int ix = 0; ix < gw; ++ix) {
-            float x = g.sw + pw * g.bw + (ix + .5f) * g.bw / gw;
-            float yy = y;
-            if (yy < -1.0f || yy > (float)H || x < -1.0f || x > (float)W) continue;
-            if (yy <= 0) yy = 0;
-            if (x <= 0) x = 0;
-            int yl = (int)yy, xl = (int)x, yh, xh;
-            if (yl >= H - 1) { yh = yl = H - 1; yy = (float)yl; } else yh = yl + 1;
-            if (xl >= W - 1) { xh = xl = W - 1; x = (float)xl; } else xh = xl + 1;
-            const float ly = yy - yl, lx = x - xl, hy = 1.f - ly, hx = 1.f - lx;
-            bilerp_acc(acc, hy * hx, hy * lx, ly * hx, ly * lx,
-                       ld4(base + yl * rowstride + (int64_t)xl * C),
-                       ld4(base + yl * rowstride + (int64_t)xh * C),
-                       ld4(base + yh * rowstride + (int64_t)xl * C),
-                       ld4(base + yh * rowstride + (int64_t)xh * C));
-        }
-    }
-    return acc;
-}
-
-template <int SR>
-__global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sliced_kernel(
-    FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
-    const int *__restrict__ roi_order, int PH, int PW, int sr, float *__restrict__ out) {
-    __shared__ __attribute__((aligned(16))) float tile[32 * 196];
-    const int S = C / 32;
-    const int slice = blockIdx.x % S;
-    const int ri = blockIdx.x / S;
-    const int r = roi_order ? roi_order[ri] : ri;
-    int li = roi_level ? roi_level[r] : 0;
-    li = __builtin_amdgcn_readfirstlane(li);
-    const RoiGeom g = roi_geom(fa, C, rois + (int64_t)r * 5, li, PH, PW, sr);
-    const int lane = lane_id();
-    const int grp = lane >> 3, q = lane & 7;
-    const int PP = PH * PW;
-    const float *base = g.feat + slice * 32 + q * 4;
-    for (int b0 = wave_id() * 8; b0 < PP; b0 += num_waves() * 8) {
-        const int bin = b0 + grp;
-        if (bin < PP) {
-            const int ph = bin / PW, pw = bin - (bin / PW) * PW;
-            const float4 a = bin_value<SR>(g, C, base, ph, pw, g.gh, g.gw);
-            float *t = tile + (q * 4) * PP + bin;
-            t[0] = a.x / g.count;
-            t[PP] = a.y / g.count;
-            t[2 * PP] = a.z / g.count;
-            t[3 * PP] = a.w / g.count;
-        }
-    }
-    __syncthreads();
-    float *o = out + ((int64_t)r * C + slice * 32) * PP;
-    const int n = 32 * PP;
-    // 32*PP floats: a multiple of 4, and o is 16-B aligned (C % 32 == 0)
-    for (int i = threadIdx.x; i < n / 4; i += blockDim.x)
-        reinterpret_cast<float4 *>(o)[i] = reinterpret_cast<const float4 *>(tile)[i];
 }
 
 // Any pooled size: one wave per (bin, 256-channel chunk), accumulator per bin.
@@ -1150,37 +738,15 @@ static int roialign_variant() {  // read per launch so tests can switch kernels
     return e ? atoi(e) : 8;
 }
 
-template <int SR, bool FMA, bool PF, bool NT = false>
-static void launch_sep_t(const FpnLevels &fa, int C, const float *rois, const int *lvl,
-                         const int *order, int R, int P, int out_nhwc, float *out, hipStream_t s,
-                         int waves, size_t lds) {
-    hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_kernel<SR, FMA, PF, NT>), dim3(R), dim3(64 * waves),
-                       lds, s, fa, C, rois, lvl, order, P, out_nhwc, out);
-}
-
 static int launch_sep(const FpnLevels &fa, int C, const float *rois, const int *lvl,
                       const int *order, int R, int P, int out_nhwc, float *out, hipStream_t s) {
     const size_t lds = out_nhwc ? 0 : (size_t)C * P * P * 4;
     if (lds > 160 * 1024) return VD_ERR_SHAPE;
     int waves = P * ((C + 255) / 256);
     if (waves > 8) waves = 8;
-    const int v = roialign_variant();
-    if (v == 9)
-        hipLaunchKernelGGL((roi_align_fpn_nhwc_stream_kernel<2, 2>), dim3(R), dim3(64 * waves), lds,
-                           s, fa, C, rois, lvl, order, P, out_nhwc, out);
-    else if (v == 13)
-        launch_sep_t<2, true, false>(fa, C, rois, lvl, order, R, P, out_nhwc, out, s, waves, lds);
-    else if (v == 14)
-        launch_sep_t<2, true, true>(fa, C, rois, lvl, order, R, P, out_nhwc, out, s, waves, lds);
-    else if (v == 20)  // plain (write-back) output stores: 306 us vs 297 us with NT
-        launch_sep_t<2, false, false>(fa, C, rois, lvl, order, R, P, out_nhwc, out, s, waves,
-                                      lds);
-    else if (v == 22)
-        launch_sep_t<2, true, false, true>(fa, C, rois, lvl, order, R, P, out_nhwc, out, s, waves,
-                                           lds);
-    else  // product default (variant 8): non-temporal output stores
-        launch_sep_t<2, false, false, true>(fa, C, rois, lvl, order, R, P, out_nhwc, out, s, waves,
-                                            lds);
+    // non-temporal output stores (297 us vs 306 us write-back on the 8-frame launch)
+    hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_kernel<2, true>), dim3(R), dim3(64 * waves), lds,
+                       s, fa, C, rois, lvl, order, P, out_nhwc, out);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
@@ -1217,36 +783,11 @@ int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, con
     }
     if (variant >= 8 && sr == 2 && PH == PW && (int64_t)C * PH * PW * 4 <= 160 * 1024)
         return launch_sep(fa, C, rois, lvl, order, R, PH, 0, out, s);
-    if (C % 32 == 0 && PH * PW <= 196 && (variant == 0 || variant == 7)) {
-        const int bins = PH * PW;
-        int waves = (bins + 7) / 8;
-        if (waves > 8) waves = 8;
-        const dim3 grid((unsigned)((int64_t)R * (C / 32)));
-        if (sr == 2)
-            hipLaunchKernelGGL((roi_align_fpn_nhwc_sliced_kernel<2>), grid, dim3(64 * waves), 0, s,
-                               fa, C, rois, lvl, order, PH, PW, sr, out);
-        else
-            hipLaunchKernelGGL((roi_align_fpn_nhwc_sliced_kernel<0>), grid, dim3(64 * waves), 0, s,
-                               fa, C, rois, lvl, order, PH, PW, sr, out);
-        return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
-    }
     if (PH == PW && (PH == 7 || PH == 14)) {
         const bool unrolled = sr == 2 && variant >= 2;
-        if (PH == 7 && sr == 2 && C == 256 && variant == 6) {
-            // LDS footprint staging: budget >= 2 rows x 28 columns and >= the output tile
-            const int budget_px = 72;
-            hipLaunchKernelGGL((roi_align_fpn_nhwc_lds_kernel<7, 2>), dim3(R), dim3(7 * 64),
-                               (size_t)budget_px * 1024, s, fa, rois, lvl, order, budget_px, out);
-            return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
-        }
-        if (PH == 7 && unrolled) {
-            switch (variant) {
-                case 3: return launch_rows<7, 2, 2>(fa, C, rois, lvl, order, R, sr, out, s);
-                case 4: return launch_rows<7, 2, 4>(fa, C, rois, lvl, order, R, sr, out, s);
-                case 5: return launch_rows<7, 2, 6>(fa, C, rois, lvl, order, R, sr, out, s);
-                default: return launch_rows<7, 2, 3>(fa, C, rois, lvl, order, R, sr, out, s);
-            }
-        }
+        if (PH == 7 && unrolled)
+            return variant == 3 ? launch_rows<7, 2, 2>(fa, C, rois, lvl, order, R, sr, out, s)
+                                : launch_rows<7, 2, 3>(fa, C, rois, lvl, order, R, sr, out, s);
         if (PH == 7) return launch_rows<7, 0>(fa, C, rois, lvl, order, R, sr, out, s);
         return unrolled ? launch_rows<14, 2>(fa, C, rois, lvl, order, R, sr, out, s)
                         : launch_rows<14, 0>(fa, C, rois, lvl, order, R, sr, out, s);
