@@ -1,8 +1,13 @@
 #!/usr/bin/env python3
 """Microbenchmark: conv + bias + relu (+ residual) variants on MI355X, channels_last fp32."""
 import json, sys, time
+import os
+
 import torch
 import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vosdetectron_amd import ops  # noqa: E402
 
 torch.backends.cudnn.benchmark = True
 dev = "cuda"
@@ -18,12 +23,14 @@ def timeit(fn, iters=20):
     return (time.perf_counter() - t) / iters * 1e3
 
 shapes = [  # (N, Cin, H, W, Cout, k, stride)
-    (4, 64, 200, 336, 64, 3, 1),
-    (4, 256, 200, 336, 64, 1, 1),
-    (4, 64, 200, 336, 256, 1, 1),
-    (4, 128, 100, 168, 128, 3, 1),
-    (4, 256, 50, 84, 256, 3, 1),
-    (4, 3, 800, 1344, 64, 7, 2),
+    (16, 64, 200, 336, 64, 3, 1),
+    (16, 256, 200, 336, 64, 1, 1),
+    (16, 64, 200, 336, 256, 1, 1),
+    (16, 128, 100, 168, 128, 3, 1),
+    (16, 256, 50, 84, 256, 3, 1),
+    (16, 256, 200, 336, 256, 3, 1),
+    (1600, 256, 14, 14, 256, 3, 1),
+    (16, 3, 800, 1344, 64, 7, 2),
 ]
 res = []
 for (N, Ci, H, W, Co, k, s) in shapes:
@@ -35,6 +42,8 @@ for (N, Ci, H, W, Co, k, s) in shapes:
     z = torch.randn(N, Co, Ho, Wo, device=dev).to(memory_format=torch.channels_last)
     r = {"shape": [N, Ci, H, W, Co, k, s]}
     r["conv_nobias"] = timeit(lambda: F.conv2d(x, w, None, s, p))
+    r["conv_vdepi"] = timeit(lambda: ops.bias_act_(F.conv2d(x, w, None, s, p), b, relu=True))
+    r["conv_vdepi_res"] = timeit(lambda: ops.bias_act_(F.conv2d(x, w, None, s, p), b, z, relu=True))
     r["conv_bias_relu"] = timeit(lambda: F.relu_(F.conv2d(x, w, b, s, p)))
     r["conv_bias_add_relu"] = timeit(lambda: F.relu_(F.conv2d(x, w, b, s, p).add_(z)))
     try:
