@@ -634,6 +634,42 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_kernel(
     }
 }
 
+// Speed-of-light probe (variant 30, measurement only -- NOT RoIAlign): the same
+// grid, block shape, RoI order and output writes as the separable kernel, but
+// each RoI reads its compulsory footprint (the SURVEY 8d rectangle of level
+// pixels) exactly once, one row per wave, with no sampling arithmetic.  Its time
+// is what any kernel that fetches per RoI pays for the memory traffic alone.
+__global__ __launch_bounds__(512) void roi_footprint_probe_kernel(
+    FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
+    const int *__restrict__ roi_order, int P, float *__restrict__ out) {
+    const int r = roi_order ? roi_order[blockIdx.x] : (int)blockIdx.x;
+    int li = roi_level ? roi_level[r] : 0;
+    li = __builtin_amdgcn_readfirstlane(li);
+    const float *roi = rois + (int64_t)r * 5;
+    const int H = fa.H[li], W = fa.W[li];
+    const float s = fa.scale[li];
+    const float *feat = fa.feat[li] + (int64_t)(int)roi[0] * H * W * C;
+    const float x1 = roi[1] * s, y1 = roi[2] * s, x2 = roi[3] * s, y2 = roi[4] * s;
+    const int xa = max((int)floorf(x1), 0), xb = min((int)floorf(fmaxf(x2, x1 + 1.f)) + 1, W - 1);
+    const int ya = max((int)floorf(y1), 0), yb = min((int)floorf(fmaxf(y2, y1 + 1.f)) + 1, H - 1);
+    const int lane = lane_id();
+    for (int c0 = 0; c0 < C; c0 += 256) {
+        const int c = c0 + lane * 4;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int y = ya + wave_id(); y <= yb; y += num_waves())
+            for (int x = xa; x <= xb; ++x) {
+                const float4 v = ld4(feat + ((int64_t)y * W + x) * C + c);
+                acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+            }
+        for (int ph = wave_id(); ph < P; ph += num_waves())
+            for (int pw = 0; pw < P; ++pw) {
+                vf4 v = {acc.x, acc.y, acc.z, acc.w};
+                __builtin_nontemporal_store(
+                    v, reinterpret_cast<vf4 *>(out + (((int64_t)r * P + ph) * P + pw) * C + c));
+            }
+    }
+}
+
 // Any pooled size: one wave per (bin, 256-channel chunk), accumulator per bin.
 __global__ __launch_bounds__(256) void roi_align_fpn_nhwc_generic_kernel(
     FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
@@ -758,6 +794,11 @@ int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, con
     if (C % 4 != 0) return VD_ERR_SHAPE;
     const int variant = roialign_variant();
     if (out_nhwc) {  // product path: [R][P][P][C] written straight from registers
+        if (variant == 30 && PH == PW && C % 256 == 0) {  // speed-of-light probe (not RoIAlign)
+            hipLaunchKernelGGL(roi_footprint_probe_kernel, dim3(R), dim3(64 * (PH < 8 ? PH : 8)),
+                               0, s, fa, C, rois, lvl, order, PH, out);
+            return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+        }
         if (variant == 16 && sr == 2 && PH == PW && C % 32 == 0 && PH <= 16) {
             const int64_t blocks = (int64_t)R * (C / 32);
             const int waves = PH < 8 ? PH : 8;
