@@ -94,7 +94,8 @@ def xcd_order(rois, lvls, n_xcd=8):
 
 ROIALIGN_KERNEL = {"3": "vd::roi_align_fpn_nhwc_kernel<7,2,2> (reference order)",
                    "8": "vd::roi_align_fpn_nhwc_sep_kernel<2,true> (separable, nt stores)",
-                   "16": "vd::roi_align_fpn_nhwc_xslice2_kernel<2,32> (XCD channel slices)"}
+                   "16": "vd::roi_align_fpn_nhwc_xslice2_kernel<2,32> (XCD channel slices)",
+                   "30": "vd::roi_footprint_probe_kernel (speed-of-light probe, NOT RoIAlign)"}
 
 
 # rocprofv3 --pmc passes of this exact launch (tools/prof_roialign.sh, separate
