@@ -46,6 +46,9 @@ static inline size_t rpn_mask_bytes(int pre) {
 }
 
 static inline size_t rpn_box_bytes(int pre) { return a256(sizeof(float) * 10 * (size_t)pre); }
+// large variant: NMS processing-order keys + the candidate count m, handed from the
+// select/decode kernel to the mask-build and resolve kernels
+static inline size_t rpn_key_bytes(int pre) { return a256(sizeof(uint64_t) * (size_t)pre) + 256; }
 
 // pre_nms_topN actually used per level and whether the large variant is needed
 static bool rpn_plan(const VdRpnLevel *levels, int num_levels, int pre_nms_topN, int *max_pre,
@@ -65,7 +68,7 @@ static bool rpn_plan(const VdRpnLevel *levels, int num_levels, int pre_nms_topN,
 
 static inline size_t rpn_slot_bytes(int max_pre, bool large) {
     const int p = max_pre < 64 ? 64 : max_pre;
-    return large ? rpn_mask_bytes(p) + rpn_box_bytes(p) : rpn_mask_bytes(p);
+    return large ? rpn_mask_bytes(p) + rpn_box_bytes(p) + rpn_key_bytes(p) : rpn_mask_bytes(p);
 }
 
 size_t rpn_workspace_bytes(const VdRpnLevel *levels, int num_levels, int num_images,
@@ -134,7 +137,7 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
     RpnArgs args, int num_levels, const float *__restrict__ im_info, int pre_nms_topN,
     int post_nms_topN, float nms_thresh, float min_size, float *__restrict__ rois_out,
     float *__restrict__ probs_out, int32_t *__restrict__ counts_out, char *__restrict__ ws,
-    size_t slot_bytes, size_t mask_bytes) {
+    size_t slot_bytes, size_t mask_bytes, size_t box_bytes) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     auto &L = *reinterpret_cast<RpnLds<SelCap, PreMax, GB> *>(lds_raw);
     const int l = blockIdx.x, img = blockIdx.y;
@@ -148,7 +151,10 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
     float *boxes = GB ? reinterpret_cast<float *>(ws + (size_t)slot * slot_bytes + mask_bytes)
                       : &L.box[0][0];
     // box-array stride: the slot's box region holds >= max_pre entries (rpn_box_bytes)
-    const int bstride = GB ? (int)((slot_bytes - mask_bytes) / (10 * sizeof(float))) : PreMax;
+    const int bstride = GB ? (int)(box_bytes / (10 * sizeof(float))) : PreMax;
+    uint64_t *gkeys = reinterpret_cast<uint64_t *>(ws + (size_t)slot * slot_bytes + mask_bytes +
+                                                   box_bytes);
+    int32_t *gm = reinterpret_cast<int32_t *>(gkeys + bstride);
     float *const px1 = boxes, *const py1 = boxes + bstride, *const px2 = boxes + 2 * bstride;
     float *const py2 = boxes + 3 * bstride, *const psc = boxes + 4 * bstride;
     float *const ox1 = boxes + 5 * bstride, *const oy1 = boxes + 6 * bstride;
@@ -199,7 +205,10 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
             rank = (lo + hi) >> 1;
         }
         if (ncand < 0) {  // cannot bracket: signal and bail out (host reports)
-            if (threadIdx.x == 0) counts_out[slot] = -1;
+            if (threadIdx.x == 0) {
+                counts_out[slot] = -1;
+                if (GB) *gm = -1;
+            }
             return;
         }
         block_compact(
@@ -269,7 +278,10 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
             ro[p * 5 + 4] = py2[p];
             po[p] = psc[p];
         }
-        if (threadIdx.x == 0) counts_out[slot] = n_out;
+        if (threadIdx.x == 0) {
+            counts_out[slot] = n_out;
+            if (GB) *gm = -1;
+        }
         return;
     }
 
@@ -289,6 +301,11 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
         ox2[r] = c;
         oy2[r] = e;
         oar[r] = (c - a + 1) * (e - b + 1);
+        if (GB) gkeys[r] = L.keys[r];
+    }
+    if (GB) {  // mask rows and resolve run as rpn_nms_mask_kernel / rpn_nms_finish_kernel
+        if (threadIdx.x == 0) *gm = m;
+        return;
     }
     __syncthreads();
     nms_build_mask_rows(ox1, oy1, ox2, oy2, oar, m, nms_thresh, mask, wave_id(),
@@ -300,6 +317,77 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
     for (int r = threadIdx.x; r < m; r += blockDim.x)
         L.keep_pos[(int)(uint32_t)L.keys[r]] = L.keep_rank[r];
     __syncthreads();
+    const int kept = block_compact(
+        m, [&](int p) { return L.keep_pos[p] != 0; },
+        [&](int pos, int p) {
+            if (pos < cap) {
+                ro[pos * 5 + 0] = (float)img;
+                ro[pos * 5 + 1] = px1[p];
+                ro[pos * 5 + 2] = py1[p];
+                ro[pos * 5 + 3] = px2[p];
+                ro[pos * 5 + 4] = py2[p];
+                po[pos] = psc[p];
+            }
+        },
+        L.scratch);
+    if (threadIdx.x == 0) counts_out[slot] = min(kept, cap);
+}
+
+// Large variant, phase 2: the suppression mask of every slot built by many
+// workgroups (one wave per row, as the standalone vd_nms) instead of the 16
+// waves of the slot's own workgroup.
+__global__ __launch_bounds__(1024) void rpn_nms_mask_kernel(char *__restrict__ ws,
+                                                             size_t slot_bytes, size_t mask_bytes,
+                                                             size_t box_bytes, float nms_thresh) {
+    const int slot = blockIdx.y;
+    char *base = ws + (size_t)slot * slot_bytes;
+    const int bstride = (int)(box_bytes / (10 * sizeof(float)));
+    const float *boxes = reinterpret_cast<const float *>(base + mask_bytes);
+    const int32_t m = *reinterpret_cast<const int32_t *>(
+        reinterpret_cast<const uint64_t *>(base + mask_bytes + box_bytes) + bstride);
+    if (m < 1) return;
+    const int wpb = blockDim.x / 64;
+    nms_build_mask_rows(boxes + 5 * bstride, boxes + 6 * bstride, boxes + 7 * bstride,
+                        boxes + 8 * bstride, boxes + 9 * bstride, m, nms_thresh,
+                        reinterpret_cast<uint64_t *>(base), blockIdx.x * wpb + wave_id(),
+                        gridDim.x * wpb);
+}
+
+// Large variant, phase 3: greedy resolve (one wave) + ascending compaction.
+struct RpnFinishLds {
+    uint64_t keys[kPreMaxL];
+    uint8_t keep_rank[kPreMaxL];
+    uint8_t keep_pos[kPreMaxL];
+    int scratch[32];
+};
+
+__global__ __launch_bounds__(1024) void rpn_nms_finish_kernel(
+    int num_levels, int post_nms_topN, float *__restrict__ rois_out,
+    float *__restrict__ probs_out, int32_t *__restrict__ counts_out, char *__restrict__ ws,
+    size_t slot_bytes, size_t mask_bytes, size_t box_bytes) {
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    RpnFinishLds &L = *reinterpret_cast<RpnFinishLds *>(lds_raw);
+    const int l = blockIdx.x, img = blockIdx.y;
+    const int slot = img * num_levels + l;
+    char *base = ws + (size_t)slot * slot_bytes;
+    const int bstride = (int)(box_bytes / (10 * sizeof(float)));
+    const float *boxes = reinterpret_cast<const float *>(base + mask_bytes);
+    const uint64_t *gkeys = reinterpret_cast<const uint64_t *>(base + mask_bytes + box_bytes);
+    const int32_t m = *reinterpret_cast<const int32_t *>(gkeys + bstride);
+    if (m < 0) return;  // finished in phase 1 (no NMS, or could not bracket)
+    const float *px1 = boxes, *py1 = boxes + bstride, *px2 = boxes + 2 * bstride;
+    const float *py2 = boxes + 3 * bstride, *psc = boxes + 4 * bstride;
+    for (int r = threadIdx.x; r < m; r += blockDim.x) L.keys[r] = gkeys[r];
+    __syncthreads();
+    if (wave_id() == 0 && m > 0)
+        nms_resolve_wave(reinterpret_cast<const uint64_t *>(base), m, L.keep_rank);
+    __syncthreads();
+    for (int r = threadIdx.x; r < m; r += blockDim.x)
+        L.keep_pos[(int)(uint32_t)L.keys[r]] = L.keep_rank[r];
+    __syncthreads();
+    const int cap = post_nms_topN;
+    float *ro = rois_out + (size_t)slot * cap * 5;
+    float *po = probs_out + (size_t)slot * cap;
     const int kept = block_compact(
         m, [&](int p) { return L.keep_pos[p] != 0; },
         [&](int pos, int p) {
@@ -329,6 +417,7 @@ int launch_rpn_proposals(const VdRpnLevel *levels, int num_levels, int num_image
     if (!rpn_plan(levels, num_levels, pre_nms_topN, &max_pre, &large)) return VD_ERR_SHAPE;
     const int p = max_pre < 64 ? 64 : max_pre;
     const size_t mb = rpn_mask_bytes(p);
+    const size_t bb = large ? rpn_box_bytes(p) : 0;
     const size_t sb = rpn_slot_bytes(max_pre, large);
     if (!workspace || ws_bytes < sb * (size_t)num_levels * (size_t)num_images)
         return VD_ERR_WORKSPACE;
@@ -338,13 +427,22 @@ int launch_rpn_proposals(const VdRpnLevel *levels, int num_levels, int num_image
         hipLaunchKernelGGL((rpn_proposals_kernel<kSelCapL, kPreMaxL, true>), grid, dim3(1024),
                            sizeof(Lds), s, args, num_levels, im_info,
                            pre_nms_topN, post_nms_topN, nms_thresh, min_size, rois_out,
-                           probs_out, counts_out, (char *)workspace, sb, mb);
+                           probs_out, counts_out, (char *)workspace, sb, mb, bb);
+        if (nms_thresh > 0.f) {
+            const int rows_per_block = 16;  // 16 waves, one row each per pass
+            const dim3 mgrid((p + rows_per_block - 1) / rows_per_block, num_levels * num_images);
+            hipLaunchKernelGGL(rpn_nms_mask_kernel, mgrid, dim3(64 * rows_per_block), 0, s,
+                               (char *)workspace, sb, mb, bb, nms_thresh);
+            hipLaunchKernelGGL(rpn_nms_finish_kernel, grid, dim3(1024), sizeof(RpnFinishLds), s,
+                               num_levels, post_nms_topN, rois_out, probs_out, counts_out,
+                               (char *)workspace, sb, mb, bb);
+        }
     } else {
         using Lds = RpnLds<kSelCap, kPreMax, false>;
         hipLaunchKernelGGL((rpn_proposals_kernel<kSelCap, kPreMax, false>), grid, dim3(1024),
                            sizeof(Lds), s, args, num_levels, im_info, pre_nms_topN,
                            post_nms_topN, nms_thresh, min_size, rois_out, probs_out, counts_out,
-                           (char *)workspace, sb, mb);
+                           (char *)workspace, sb, mb, bb);
     }
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
