@@ -264,7 +264,7 @@ def main():
 
     def drain():  # the previous step's gather has landed (stream-ordered)
         if pending[0] is not None:
-            pending[0].wait()
+            pending[0].wait(views=False)
             pending[0] = None
 
     def step():

@@ -29,13 +29,13 @@ class PendingGather:
     def __init__(self, work, gatherer, rbuf):
         self.work, self.g, self.rbuf = work, gatherer, rbuf
 
-    def wait(self) -> Dict[str, torch.Tensor]:
+    def wait(self, views: bool = True) -> Dict[str, torch.Tensor]:
         """Orders the caller's stream after the collective; returns the gathered
-        results ([world*F, ...], rank-major)."""
+        results ([world*F, ...], rank-major) unless views=False."""
         if self.work is not None:
             self.work.wait()
             self.work = None
-        return self.g._views(self.rbuf)
+        return self.g._views(self.rbuf) if views else {}
 
 
 class ResultGatherer:
