@@ -257,3 +257,30 @@ def test_detections_postfilter_vs_oracle(seed, cross, pre, dets_per_im):
         assert np.array_equal(dets[i, :n, 4], sc)
         ref_cls = np.concatenate([[j] * len(cls_boxes[j]) for j in range(1, K)]).astype(np.int32)
         assert np.array_equal(dcls[i, :n], ref_cls)
+
+
+def test_detections_postfilter_golden(golden):
+    """vd_detections_postfilter on the stock limit's output reproduces the
+    reference-executed fork steps (detections_postfilter.npz)."""
+    import ctypes
+    from vosdetectron_amd._lib import check, lib
+    g = golden("detections_postfilter")
+    sc, bx, cls_boxes = orc.box_results_with_nms_and_limit(g["scores"], g["boxes"])
+    cls = np.concatenate([[j] * len(cls_boxes[j]) for j in range(1, 81)]).astype(np.int32)
+    cap = 256
+    for tag, cross, pre in (("cross04_pre2", 0.4, 2), ("cross0_pre50", 0., 50),
+                            ("cross06_pre0", 0.6, 0)):
+        dets = torch.zeros((1, cap, 5), device=DEV)
+        dets[0, :len(sc), :4] = torch.from_numpy(bx).to(DEV)
+        dets[0, :len(sc), 4] = torch.from_numpy(sc).to(DEV)
+        dcls = torch.zeros((1, cap), dtype=torch.int32, device=DEV)
+        dcls[0, :len(sc)] = torch.from_numpy(cls).to(DEV)
+        cnt = torch.tensor([len(sc)], dtype=torch.int32, device=DEV)
+        check(lib().vd_detections_postfilter(dets.data_ptr(), dcls.data_ptr(), cnt.data_ptr(), 1,
+                                             cap, ctypes.c_float(cross), pre,
+                                             torch.cuda.current_stream().cuda_stream),
+              "vd_detections_postfilter")
+        n = int(cnt.item())
+        assert n == len(g[tag + "_dets"]), tag
+        assert np.array_equal(dets[0, :n].cpu().numpy(), g[tag + "_dets"]), tag
+        assert np.array_equal(dcls[0, :n].cpu().numpy(), g[tag + "_cls"]), tag

@@ -73,3 +73,16 @@ def test_multilevel_mask_rois(golden):
     for lvl in range(2, 6):
         assert np.array_equal(d["mask_rois_fpn%d" % lvl], g["mask_rois_fpn%d" % lvl])
     assert np.array_equal(d["mask_rois_idx_restore_int32"], g["mask_rois_idx_restore_int32"])
+
+
+def test_detections_postfilter_golden(golden):
+    """The fork's NMS_CROSS_CLASS / NUM_DET_PER_CLASS_PRE steps executed by the
+    reference's own vos_test.box_results_with_nms_and_limit (detections_postfilter.npz)."""
+    g = golden("detections_postfilter")
+    for tag, cross, pre in (("cross04_pre2", 0.4, 2), ("cross0_pre50", 0., 50),
+                            ("cross06_pre0", 0.6, 0)):
+        sc, bx, cls_boxes = orc.box_results_with_nms_and_limit(
+            g["scores"], g["boxes"], nms_cross_class=cross, num_det_per_class_pre=pre)
+        assert np.array_equal(np.hstack([bx, sc[:, None]]), g[tag + "_dets"]), tag
+        cls = np.concatenate([[j] * len(cls_boxes[j]) for j in range(1, 81)]).astype(np.int32)
+        assert np.array_equal(cls, g[tag + "_cls"]), tag

@@ -205,6 +205,36 @@ def main():
              rois=rois, roi_probs=rprobs, im_info=im_info, pre_nms=6000, post_nms=1000)
     cfg.TEST.RPN_PRE_NMS_TOP_N = 1000
 
+    # ---- the fork's box_results_with_nms_and_limit post-limit steps
+    # (lib_vos/tools/vos_test.py:748-865): TEST.NMS_CROSS_CLASS and
+    # TEST.NUM_DET_PER_CLASS_PRE, executed by the reference module itself
+    sys.path.insert(0, os.path.join(REF, "lib_vos", "tools"))
+    import vos_test
+    rng5 = np.random.default_rng(20241017)
+    R, K = 400, 81
+    xy = rng5.uniform(0, 700, (R, 2))
+    wh = rng5.uniform(8, 200, (R, 2))
+    base = np.hstack([xy, xy + wh])
+    jitter = rng5.normal(0, 6, (R, 4 * K))
+    boxes_cls = (np.tile(base, K) + jitter).astype(np.float32)
+    logits = rng5.normal(0, 2.5, (R, K))
+    e = np.exp(logits - logits.max(1, keepdims=True))
+    scores = (e / e.sum(1, keepdims=True)).astype(np.float32)  # continuous: tie-free
+    cfg.MODEL.NUM_CLASSES = K  # reference default -1
+    cfg.TEST.SCORE_THRESH, cfg.TEST.NMS, cfg.TEST.DETECTIONS_PER_IM = 0.05, 0.5, 100
+    cfg.TEST.SOFT_NMS.ENABLED, cfg.TEST.BBOX_VOTE.ENABLED = False, False
+    cfg.TEST.NMS_SMALL_BOX_IOU = 0.
+    post = {"scores": scores, "boxes": boxes_cls}
+    for tag, cross, pre in (("cross04_pre2", 0.4, 2), ("cross0_pre50", 0., 50),
+                            ("cross06_pre0", 0.6, 0)):
+        cfg.TEST.NMS_CROSS_CLASS, cfg.TEST.NUM_DET_PER_CLASS_PRE = cross, pre
+        _, _, cls_b = vos_test.box_results_with_nms_and_limit(scores, boxes_cls)
+        post[tag + "_dets"] = np.vstack([cls_b[j] for j in range(1, K)]).astype(np.float32)
+        post[tag + "_cls"] = np.concatenate(
+            [[j] * len(cls_b[j]) for j in range(1, K)]).astype(np.int32)
+    cfg.TEST.NMS_CROSS_CLASS, cfg.TEST.NUM_DET_PER_CLASS_PRE = 0., 0
+    np.savez(os.path.join(OUT, "detections_postfilter.npz"), **post)
+
     print("wrote", sorted(os.listdir(OUT)))
 
 
