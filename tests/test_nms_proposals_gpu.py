@@ -269,7 +269,7 @@ def test_detections_postfilter_golden(golden):
     cls = np.concatenate([[j] * len(cls_boxes[j]) for j in range(1, 81)]).astype(np.int32)
     cap = 256
     for tag, cross, pre in (("cross04_pre2", 0.4, 2), ("cross0_pre50", 0., 50),
-                            ("cross06_pre0", 0.6, 0)):
+                            ("cross06_pre0", 0.6, 0), ("cross0_pre0", 0., 0)):
         dets = torch.zeros((1, cap, 5), device=DEV)
         dets[0, :len(sc), :4] = torch.from_numpy(bx).to(DEV)
         dets[0, :len(sc), 4] = torch.from_numpy(sc).to(DEV)

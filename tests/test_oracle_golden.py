@@ -80,7 +80,7 @@ def test_detections_postfilter_golden(golden):
     reference's own vos_test.box_results_with_nms_and_limit (detections_postfilter.npz)."""
     g = golden("detections_postfilter")
     for tag, cross, pre in (("cross04_pre2", 0.4, 2), ("cross0_pre50", 0., 50),
-                            ("cross06_pre0", 0.6, 0)):
+                            ("cross06_pre0", 0.6, 0), ("cross0_pre0", 0., 0)):
         sc, bx, cls_boxes = orc.box_results_with_nms_and_limit(
             g["scores"], g["boxes"], nms_cross_class=cross, num_det_per_class_pre=pre)
         assert np.array_equal(np.hstack([bx, sc[:, None]]), g[tag + "_dets"]), tag

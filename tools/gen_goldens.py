@@ -226,7 +226,7 @@ def main():
     cfg.TEST.NMS_SMALL_BOX_IOU = 0.
     post = {"scores": scores, "boxes": boxes_cls}
     for tag, cross, pre in (("cross04_pre2", 0.4, 2), ("cross0_pre50", 0., 50),
-                            ("cross06_pre0", 0.6, 0)):
+                            ("cross06_pre0", 0.6, 0), ("cross0_pre0", 0., 0)):
         cfg.TEST.NMS_CROSS_CLASS, cfg.TEST.NUM_DET_PER_CLASS_PRE = cross, pre
         _, _, cls_b = vos_test.box_results_with_nms_and_limit(scores, boxes_cls)
         post[tag + "_dets"] = np.vstack([cls_b[j] for j in range(1, K)]).astype(np.float32)
