@@ -110,3 +110,27 @@ def test_pipeline_with_no_detections():
     out = pipe.run(torch.from_numpy(fr).to(DEV))
     assert out["counts_host"] == [0, 0] and out["masks"].shape == (0, 28, 28)
     assert all(not any(s) for s in frame_segms(pipe, out))
+
+
+def test_proposals_size_limits():
+    """pre_nms_topN up to 8192 (the large-candidate kernel's limit, incl. take-all at
+    exactly 8192 anchors) matches the oracle; 8193 is rejected."""
+    from vosdetectron_amd import ops
+    from vosdetectron_amd._lib import VosdetError
+    rng = np.random.default_rng(11)
+    an = orc.generate_anchors(16, (32, 64, 128, 256, 512), (0.5, 1, 2))
+    for (H, W, pre) in [(16, 34, 0), (40, 60, 8192)]:  # 16*34*15 = 8160 take-all; pre cap
+        p = rng.uniform(0, 1, (1, 15, H, W)).astype(np.float32)
+        d = rng.normal(0, 0.3, (1, 60, H, W)).astype(np.float32)
+        info = np.array([[H * 16, W * 16, 1.0]], np.float32)
+        rois, _, cnt = [t.cpu().numpy() for t in ops.generate_proposals(
+            [torch.from_numpy(p).to(DEV)], [torch.from_numpy(d).to(DEV)],
+            [torch.from_numpy(an).to(DEV)], [1. / 16], torch.from_numpy(info).to(DEV), pre,
+            1000, 0.7, 0)]
+        ref, _ = orc.generate_proposals(an, 1. / 16, p, d, info, pre, 1000, 0.7, 0)
+        assert cnt[0, 0] == len(ref) and np.array_equal(rois[0, 0, :cnt[0, 0]], ref)
+    with pytest.raises(VosdetError):
+        z = torch.zeros((1, 15, 40, 60), device=DEV)
+        ops.generate_proposals([z], [torch.zeros((1, 60, 40, 60), device=DEV)],
+                               [torch.from_numpy(an).to(DEV)], [1. / 16],
+                               torch.tensor([[640., 960., 1.]], device=DEV), 8193, 1000, 0.7, 0)
