@@ -19,7 +19,6 @@ proposal level through the large-candidate vd_generate_proposals
 """
 from __future__ import annotations
 
-import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F

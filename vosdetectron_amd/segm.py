@@ -8,7 +8,6 @@ from __future__ import annotations
 
 from typing import List, Sequence
 
-import numpy as np
 import torch
 
 from . import ops
