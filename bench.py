@@ -159,6 +159,32 @@ def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=Non
             "algorithmic_bytes_per_launch": int(nbytes), "avg_launch_us": round(t * 1e6, 2)}
 
 
+def cpu_roialign_1thread(C=256, P=7, sr=2, seed=0):
+    """The reference's RoIAlign semantics on the host, single thread (oracle/roi_ops.c,
+    the per-level roi_feature_transform loop): one frame of the roofline launch's
+    synthetic RoIs (1000, P=7) -- SURVEY.md 8(d) asks for this number beside the
+    multi-thread e2e baseline."""
+    from oracle import oracle as orc
+    sizes = [(200, 336), (100, 168), (50, 84), (25, 42)]
+    rng = np.random.default_rng(seed + 1)
+    feats = [rng.standard_normal((1, C, h, w), dtype=np.float32) for h, w in sizes]
+    rois = synthetic_rois(seed, 1000)
+    lv = fpn_levels_np(rois)
+    d = {}
+    order = []
+    for k in range(2, 6):
+        idx = np.where(lv == k)[0]
+        d["rois_fpn%d" % k] = rois[idx]
+        order.append(idx)
+    d["rois_idx_restore_int32"] = np.argsort(np.concatenate(order), kind="stable").astype(np.int32)
+    nbytes = roi_align_algorithmic_bytes(rois, lv - 2, sizes, C, P)
+    t0 = time.perf_counter()
+    orc.roi_feature_transform(feats[::-1], d, "rois", P, [1. / 32, 1. / 16, 1. / 8, 1. / 4], sr)
+    dt = time.perf_counter() - t0
+    return {"ms_per_frame": round(dt * 1e3, 1), "GBs_algorithmic": round(nbytes / dt / 1e9, 3),
+            "threads": 1, "sample": "1 frame, 1000 synthetic RoIs (seed 0), C=256, P=7, sr=2"}
+
+
 def cpu_baseline(cfg_name, sd, n_frames=2, threads=None, cfg=None):
     """The reference's CPU path (oracle/pipeline.py, oracle/vos_pipeline.py) on a
     bounded sample."""
@@ -190,8 +216,10 @@ def cpu_baseline(cfg_name, sd, n_frames=2, threads=None, cfg=None):
     for i in range(n_frames):
         ref(fr[i + 1])
     dt = time.perf_counter() - t0
+    ra = None if (cfg is not None and (cfg.get("VOS", False) or not cfg.FPN.FPN_ON)) \
+        else cpu_roialign_1thread()
     return {"value": round(n_frames / dt, 4), "unit": "frames/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "roialign_1thread": ra,
             "sample": "%d synthetic %s, full im_detect_all path (torch-CPU convs, "
                       "oracle C RoIAlign/NMS, numpy proposals), %.1f s, cpu=%s" % (
                           n_frames, what, dt, platform.processor() or platform.machine())}
