@@ -185,9 +185,10 @@ def cpu_roialign_1thread(C=256, P=7, sr=2, seed=0):
             "threads": 1, "sample": "1 frame, 1000 synthetic RoIs (seed 0), C=256, P=7, sr=2"}
 
 
-def cpu_baseline(cfg_name, sd, n_frames=2, threads=None, cfg=None):
+def cpu_baseline(cfg_name, sd, n_frames=16, threads=None, cfg=None, min_seconds=10.0):
     """The reference's CPU path (oracle/pipeline.py, oracle/vos_pipeline.py) on a
-    bounded sample."""
+    bounded sample: frames are run until ``min_seconds`` of CPU work (at least 2 frames,
+    at most ``n_frames``), so the sample is ~10-30 s whatever the host."""
     from oracle.pipeline import RefCPUPipeline
     threads = threads or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
@@ -213,9 +214,12 @@ def cpu_baseline(cfg_name, sd, n_frames=2, threads=None, cfg=None):
         what = "800x1333 frames"
     ref(fr[0])  # warm-up
     t0 = time.perf_counter()
-    for i in range(n_frames):
-        ref(fr[i + 1])
+    done = 0
+    while done < n_frames and (done < 2 or time.perf_counter() - t0 < min_seconds):
+        ref(fr[done + 1])
+        done += 1
     dt = time.perf_counter() - t0
+    n_frames = done
     ra = None if (cfg is not None and (cfg.get("VOS", False) or not cfg.FPN.FPN_ON)) \
         else cpu_roialign_1thread()
     return {"value": round(n_frames / dt, 4), "unit": "frames/s", "cores": threads,
@@ -234,7 +238,8 @@ def main():
     ap.add_argument("--config", default="e2e_mask_rcnn_R-50-FPN_1x")
     ap.add_argument("--layout", default="nhwc", choices=["nchw", "nhwc"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=2)
+    ap.add_argument("--cpu-frames", type=int, default=16,
+                    help="max frames in the CPU-baseline sample (run until 10 s, >= 2 frames)")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-timers", dest="timers", action="store_false",
                     help="skip the per-stage breakdown: by default, after the timed steps, "
