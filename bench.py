@@ -314,9 +314,27 @@ def main():
                                                out["masks"], out["counts_host"])
         return out
 
-    for _ in range(args.warmup):
+    # MIOpen's first-shape search (cudnn.benchmark) keeps the first warm-up step
+    # silent for a minute or more: a heartbeat on stderr shows the run is alive.
+    import threading
+    warm_done = threading.Event()
+
+    def heartbeat():
+        t_hb = time.perf_counter()
+        while not warm_done.wait(30.0):
+            print("bench: warm-up in progress (%.0f s)" % (time.perf_counter() - t_hb),
+                  file=sys.stderr, flush=True)
+
+    if rank == 0:
+        threading.Thread(target=heartbeat, daemon=True).start()
+    for i in range(args.warmup):
         out = step()
+        if rank == 0:
+            print("bench: warm-up step %d/%d issued" % (i + 1, args.warmup),
+                  file=sys.stderr, flush=True)
     drain()
+    torch.cuda.synchronize()
+    warm_done.set()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
