@@ -94,8 +94,7 @@ def xcd_order(rois, lvls, n_xcd=8):
 
 ROIALIGN_KERNEL = {"3": "vd::roi_align_fpn_nhwc_kernel<7,2,2> (reference order)",
                    "8": "vd::roi_align_fpn_nhwc_sep_kernel<2,true> (separable, nt stores)",
-                   "16": "vd::roi_align_fpn_nhwc_xslice2_kernel<2,32> (XCD channel slices)",
-                   "30": "vd::roi_footprint_probe_kernel (speed-of-light probe, NOT RoIAlign)"}
+                   "40": "vd::roi_align_fpn_nhwc_xcd_kernel<2> (XCD channel slices)"}
 
 
 # rocprofv3 --pmc passes of this exact launch (tools/prof_roialign.sh, separate
@@ -105,7 +104,7 @@ ROIALIGN_PMC = {"8": "separable_v8nt_xcd.json", "3": "rowkernel_v3_xcd.json"}
 
 
 def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=None,
-                              use_order=True, out_layout="nhwc", deal=8):
+                              use_order=True, out_layout="nhwc", deal=None, window=None):
     """RoIAlign (FPN NHWC, one launch over 4 levels x `frames` images) timed with HIP
     events on the launch stream; >= 8 distinct frames so the working set (>700 MB)
     exceeds the 256 MB Infinity Cache."""
@@ -125,7 +124,10 @@ def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=Non
     rois_np, lv_np = np.concatenate(rois), np.concatenate(lvls)
     rois_t = torch.from_numpy(rois_np).to(dev)
     lv_t = torch.from_numpy(lv_np).to(dev)
-    order = ops.xcd_roi_order(rois_t, lv_t, n_xcd=deal) if use_order else None
+    variant = os.environ.get("VOSDET_ROIALIGN_VARIANT", "8")
+    if deal is None:  # the XCD-sliced kernel runs every RoI on every XCD: plain sort
+        deal = 1 if variant == "40" else 8
+    order = ops.xcd_roi_order(rois_t, lv_t, n_xcd=deal, window=window) if use_order else None
     shape = (frames * R, P, P, C) if out_layout == "nhwc" else (frames * R, C, P, P)
     out = torch.empty(shape, device=dev)
     s = torch.cuda.current_stream()
@@ -141,7 +143,6 @@ def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=Non
     e1.synchronize()
     t = e0.elapsed_time(e1) / 1e3 / iters
     achieved = nbytes / t / 1e9
-    variant = os.environ.get("VOSDET_ROIALIGN_VARIANT", "8")
     traffic, tsrc = None, None
     pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01_roialign_pmc",
                        ROIALIGN_PMC.get(variant, "-"))
@@ -185,12 +186,43 @@ def cpu_roialign_1thread(C=256, P=7, sr=2, seed=0):
             "threads": 1, "sample": "1 frame, 1000 synthetic RoIs (seed 0), C=256, P=7, sr=2"}
 
 
+def cpu_share():
+    """(threads, how) for the CPU baseline: the host CPUs this process may use --
+    its affinity set, capped by a cgroup quota and by OMP_NUM_THREADS when the
+    launcher sets one (the GPU box exports 16 while nproc shows the whole
+    machine, and threads beyond the share only time-slice)."""
+    n_aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    caps = {"affinity": n_aff}
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            caps["cgroup_quota"] = max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        caps["OMP_NUM_THREADS"] = int(omp)
+    threads = min(caps.values())
+    return threads, caps
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
 def cpu_baseline(cfg_name, sd, n_frames=16, threads=None, cfg=None, min_seconds=10.0):
     """The reference's CPU path (oracle/pipeline.py, oracle/vos_pipeline.py) on a
     bounded sample: frames are run until ``min_seconds`` of CPU work (at least 2 frames,
     at most ``n_frames``), so the sample is ~10-30 s whatever the host."""
     from oracle.pipeline import RefCPUPipeline
-    threads = threads or min(16, os.cpu_count() or 1)
+    share, caps = cpu_share()
+    threads = threads or share
     torch.set_num_threads(threads)
     if cfg is not None and cfg.get("VOS", False):
         from oracle.vos_pipeline import RefCPUVOSPipeline
@@ -223,18 +255,146 @@ def cpu_baseline(cfg_name, sd, n_frames=16, threads=None, cfg=None, min_seconds=
     ra = None if (cfg is not None and (cfg.get("VOS", False) or not cfg.FPN.FPN_ON)) \
         else cpu_roialign_1thread()
     return {"value": round(n_frames / dt, 4), "unit": "frames/s", "cores": threads,
-            "kind": "port", "roialign_1thread": ra,
-            "sample": "%d synthetic %s, full im_detect_all path (torch-CPU convs, "
-                      "oracle C RoIAlign/NMS, numpy proposals), %.1f s, cpu=%s" % (
-                          n_frames, what, dt, platform.processor() or platform.machine())}
+            "kind": "port", "roialign_1thread": ra, "cpu_model": cpu_model(),
+            "nproc": os.cpu_count(), "cpu_share": caps,
+            "sample": "%d synthetic %s, im_detect_all path (torch-CPU convs on %d threads, "
+                      "oracle C RoIAlign/NMS, numpy proposals; segm_results excluded as in "
+                      "the GPU line), %.1f s" % (n_frames, what, threads, dt)}
+
+
+def measure_pipeline_roialign(pipe, frames_dev, reps=20):
+    """Roofline of the engine's OWN box RoIAlign launch: the real proposals and
+    pyramid of one batch (keep_intermediates), algorithmic bytes from those
+    RoIs (§8d formula), time = HIP events around `reps` launches on the stream
+    the engine launches on."""
+    from vosdetectron_amd import ops
+    cfg = pipe.cfg
+    out = pipe.run(frames_dev, keep_intermediates=True)
+    pyr = out["pyramid"]
+    F = frames_dev.shape[0]
+    rois_all, lv_all, nbytes = [], [], 0
+    counts = out["roi_counts"].cpu().tolist()
+    sizes = [tuple(p.shape[1:3]) for p in pyr]
+    C = pyr[0].shape[3]
+    P = cfg.FAST_RCNN.ROI_XFORM_RESOLUTION
+    for f in range(F):
+        r = out["rois"][f, :counts[f]].cpu().numpy()
+        lv = fpn_levels_np(r) - 2
+        nbytes += roi_align_algorithmic_bytes(r, lv, sizes, C, P)
+        rois_all.append(r)
+        lv_all.append(lv)
+    rois_t = torch.from_numpy(np.concatenate(rois_all)).to(frames_dev.device)
+    lv_t = torch.from_numpy(np.concatenate(lv_all).astype(np.int32)).to(frames_dev.device)
+    order = ops.xcd_roi_order(rois_t, lv_t)
+    res = torch.empty((rois_t.shape[0], P, P, C), device=frames_dev.device)
+    sr = cfg.FAST_RCNN.ROI_XFORM_SAMPLING_RATIO
+    for _ in range(3):
+        ops.roi_align_fpn(pyr, pipe.roi_scales, rois_t, lv_t, P, sr, roi_order=order, out=res,
+                          out_layout="nhwc")
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        ops.roi_align_fpn(pyr, pipe.roi_scales, rois_t, lv_t, P, sr, roi_order=order, out=res,
+                          out_layout="nhwc")
+    e1.record(s)
+    e1.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / reps
+    return {"bound": "hbm", "achieved": round(nbytes / t / 1e9, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(nbytes / t / 1e9 / HBM_PEAK_GBS, 4),
+            "launch": "engine box RoIAlign, %d frames x %d real proposals, C=%d, P=%d, sr=%d"
+                      % (F, rois_t.shape[0] // max(F, 1), C, P, sr),
+            "algorithmic_bytes_per_launch": int(nbytes), "avg_launch_us": round(t * 1e6, 2)}
+
+
+def measure_segm(pipe, out, frames=4):
+    """segm_results (device paste + RLE + host rleToString) per frame -- outside
+    the FPS by SURVEY §8d's definition, reported beside it."""
+    from vosdetectron_amd.engine import frame_segms
+    sub = dict(out)
+    k = min(frames, len(out["counts_host"]))
+    sub["counts_host"] = out["counts_host"][:k]
+    frame_segms(pipe, sub)  # warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    frame_segms(pipe, sub)
+    torch.cuda.synchronize()
+    return round((time.perf_counter() - t0) / k * 1e3, 3)
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without a launcher: start N ranks through
+    torch.distributed.run (one process per GPU, like the reference's per-GPU
+    subprocesses, lib/utils/subprocess.py:41-115) and return its exit code.  Runs
+    before anything touches the GPU; the ranks are children, not an exec."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, world, rank):
+    """--dry-run: the N-rank plumbing on CPU (gloo): forms the world, runs K steps
+    of the packed result all-gather on synthetic per-rank results, checks every
+    gathered row, and prints the bench line shape with n_gpus from the live world."""
+    import torch.distributed as dist
+    from vosdetectron_amd.runner import ResultGatherer, frame_masks
+    F, D, R = args.batch or 3, 16, 28
+    g = ResultGatherer(F, D, R, world, "cpu", mask_rows=F * D)
+
+    def results(r, t):
+        rng = np.random.default_rng(1000 * t + r)
+        counts = rng.integers(0, D + 1, F).astype(np.int32)
+        dets = rng.uniform(0, 100, (F, D, 5)).astype(np.float32)
+        cls = rng.integers(1, 81, (F, D)).astype(np.int32)
+        masks = rng.uniform(0, 1, (int(counts.sum()), R, R)).astype(np.float32)
+        return dets, cls, counts, masks
+
+    t0 = time.perf_counter()
+    ok = True
+    for t in range(args.steps):
+        d, c, n, m = results(rank, t)
+        v = g.gather(torch.from_numpy(d), torch.from_numpy(c), torch.from_numpy(n),
+                     torch.from_numpy(m))
+        for r in range(world):
+            d2, c2, n2, m2 = results(r, t)
+            ok &= bool(np.array_equal(v["dets"][r * F:(r + 1) * F].numpy(), d2))
+            ok &= bool(np.array_equal(v["counts"][r * F:(r + 1) * F].numpy(), n2))
+            o = 0
+            for f in range(F):
+                ok &= bool(np.array_equal(frame_masks(v, F, r * F + f).numpy(),
+                                          m2[o:o + n2[f]]))
+                o += n2[f]
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    okt = torch.tensor([int(ok)])
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run (gloo, CPU): frame-sharded result all_gather",
+                          "value": round(world * F * args.steps / float(t), 3),
+                          "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": 0, "dry_run": True, "gather_ok": bool(okt.item()),
+                          "bytes_per_rank": g.bytes_per_rank}), flush=True)
+    dist.destroy_process_group()
+    return 0 if okt.item() else 1
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of one node; default: the launcher's WORLD_SIZE or 1. "
+                         "Without a launcher, N > 1 spawns N ranks via torch.distributed.run")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16, help="frames per GPU per step")
+    ap.add_argument("--batch", type=int, default=None, help="frames per GPU per step (16)")
     ap.add_argument("--config", default="e2e_mask_rcnn_R-50-FPN_1x")
     ap.add_argument("--layout", default="nhwc", choices=["nchw", "nhwc"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -245,29 +405,51 @@ def main():
                     help="skip the per-stage breakdown: by default, after the timed steps, "
                          "min(--steps, 3) more steps run with HIP-event stage timers and "
                          "stages_ms is reported (not part of the timed region)")
+    ap.add_argument("--resident", action="store_true",
+                    help="frames uploaded once before timing (round-1 definition); default: "
+                         "every step uploads its u8 frames from pinned host memory inside the "
+                         "timed region (SURVEY §8d)")
     ap.add_argument("--seq-len", type=int, default=50,
                     help="VOS configs: frames per synthetic sequence (hidden states reset)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU/gloo rehearsal of the N-rank launch and gather (no GPU)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0:  # no launcher
+        if args.gpus and args.gpus > 1:
+            return spawn_ranks(args.gpus)
+        world = 1
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit("bench: --gpus %d but the launcher formed a world of %d ranks"
+                         % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29512")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        return dry_run(args, dist.get_world_size(), rank)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()  # n_gpus from the live world
     dev = torch.device("cuda", local)
     torch.backends.cudnn.benchmark = True
 
     from vosdetectron_amd import config as vcfg
     from vosdetectron_amd.engine import FramePipeline
+    from vosdetectron_amd.runner import FrameUploader, ResultGatherer
     from vosdetectron_amd.weights import build_model
 
     cfg = vcfg.get(args.config)
     vos = bool(cfg.get("VOS", False))
     model, sd = build_model(cfg, seed=0, device=dev, channels_last=args.layout == "nhwc")
-    F = args.batch
+    F = args.batch or 16
+    n_host = 4  # distinct pinned host batches cycled through
     if vos:
         # configs[3]: DAVIS-shaped 480p sequences; batch row b = sequence b of
         # this rank (sequences shard across ranks), a step = the
@@ -276,22 +458,25 @@ def main():
         fh, fw = 480, 854
         pipe = VOSPipeline(model, cfg, frame_hw=(fh, fw), batch=F,
                            channels_last=args.layout == "nhwc", device=dev)
-        ring = [torch.from_numpy(synthetic_frames(F, 1 + rank * F + 7919 * t, fh, fw)).to(dev)
-                for t in range(4)]
     elif not cfg.FPN.FPN_ON:  # configs[0]: the C4 single-scale family
         from vosdetectron_amd.c4 import C4FramePipeline
+        fh, fw = 800, 1333
         pipe = C4FramePipeline(model, cfg, batch=F, channels_last=args.layout == "nhwc",
                                device=dev)
-        ring = [torch.from_numpy(synthetic_frames(F, 1 + rank * F)).to(dev)]
     else:
+        fh, fw = 800, 1333
         pipe = FramePipeline(model, cfg, batch=F, channels_last=args.layout == "nhwc",
                              device=dev)
-        ring = [torch.from_numpy(synthetic_frames(F, 1 + rank * F)).to(dev)]
-    frames = ring[0]
+    host = [synthetic_frames(F, 1 + rank * F * n_host + i * F + (7919 if vos else 0), fh, fw)
+            for i in range(n_host)]
+    uploader = FrameUploader(host, dev)
+    if args.resident:
+        resident = [torch.from_numpy(h).to(dev) for h in host]
+    any_frames = resident[0] if args.resident else uploader.dev[0]  # post-run measurements
     step_no = [0]
 
-    from vosdetectron_amd.runner import ResultGatherer
-    gatherer = ResultGatherer(F, pipe.det_cap, cfg.MRCNN.RESOLUTION, world, dev)
+    gatherer = ResultGatherer(F, pipe.det_cap, cfg.MRCNN.RESOLUTION, world, dev,
+                              mask_rows=F * max(100, int(cfg.TEST.DETECTIONS_PER_IM)) + 64)
 
     pending = [None]
 
@@ -300,18 +485,21 @@ def main():
             pending[0].wait(views=False)
             pending[0] = None
 
-    def step():
+    def step(prefetch):
         t = step_no[0]
         step_no[0] += 1
         if vos and t % args.seq_len == 0:
             pipe.reset()
-        out = pipe.run(ring[t % len(ring)])
+        frames = resident[t % n_host] if args.resident else uploader.get(t, prefetch)
+        out = pipe.run(frames)
+        if not args.resident:
+            uploader.release(t)
         if world > 1:
             # ONE packed all_gather per step over RCCL (runner.py), left in flight
             # on RCCL's stream while the next step computes; at most one in flight
             drain()
             pending[0] = gatherer.gather_async(out["dets"], out["classes"], out["counts"],
-                                               out["masks"], out["counts_host"])
+                                               out["masks"])
         return out
 
     # MIOpen's first-shape search (cudnn.benchmark) keeps the first warm-up step
@@ -328,20 +516,19 @@ def main():
     if rank == 0:
         threading.Thread(target=heartbeat, daemon=True).start()
     for i in range(args.warmup):
-        out = step()
+        out = step(prefetch=i < args.warmup - 1)
         if rank == 0:
             print("bench: warm-up step %d/%d issued" % (i + 1, args.warmup),
                   file=sys.stderr, flush=True)
     drain()
     torch.cuda.synchronize()
     warm_done.set()
-    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
+    for i in range(args.steps):
+        out = step(prefetch=i < args.steps - 1)
     drain()  # the last step's gather is inside the timed region
     torch.cuda.synchronize()
     if world > 1:
@@ -355,22 +542,30 @@ def main():
     dets_per_frame = float(np.mean(out["counts_host"]))
 
     stages = None
+    extra = {}
     if args.timers and rank == 0:  # local steps only: no collective on one rank
         pipe.enable_timers()
         for i in range(min(args.steps, 3)):
-            pipe.run(ring[i % len(ring)])
+            pipe.run(any_frames)
         stages = {k: round(v * 1e3, 3) for k, v in pipe.timer_summary().items()}
         pipe.enable_timers(False)
+        if not vos and cfg.FPN.FPN_ON:
+            extra["segm_results_ms_per_frame"] = measure_segm(pipe, out)
 
     roof = None
     if not args.no_roofline and rank == 0:
         roof = measure_roialign_roofline(dev)
+        if not vos and cfg.FPN.FPN_ON:
+            roof["engine_launch"] = measure_pipeline_roialign(pipe, any_frames)
     cpu = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:
         cpu = cpu_baseline(args.config, sd, args.cpu_frames, cfg=cfg)
 
     if rank == 0:
         fps = world * F * args.steps / dt
+        h2d = "resident in HBM before timing" if args.resident else (
+            "u8 frames uploaded every step inside the timed region (pinned host, side "
+            "stream, %.1f MB/step/GPU)" % (uploader.nbytes / 1e6))
         line = {
             "metric": "frames/sec @1333x800 e2e_mask_rcnn_R-50-FPN, 1/2/4/8 MI355X; "
                       "RoIAlign HBM GB/s",
@@ -383,20 +578,23 @@ def main():
                 "%s inference, %d DAVIS-shaped 480x854 synthetic sequences per GPU (one frame "
                 "of each per step, ConvGRU hidden states carried, reset every %d frames), full "
                 "vos im_detect_all path" % (args.config, F, args.seq_len)) if vos else (
-                "%s inference, %d synthetic 800x1333 frames per GPU per step, full "
-                "im_detect_all path (proposals, box head, class NMS, mask head)"
-                % (args.config, F)),
+                "%s inference, %d synthetic %dx%d frames per GPU per step: blob, body, RPN, "
+                "proposals, box head, class NMS, mask head -> class-selected masks "
+                "(segm_results paste/RLE excluded, SURVEY 8d)" % (args.config, F, fh, fw)),
                        "frames_per_gpu_step": F, "global_batch": world * F,
                        "parallelism": "frame-sharded dp%d + RCCL all_gather" % world,
-                       "layout": args.layout, "dets_per_frame": dets_per_frame},
+                       "layout": args.layout, "dets_per_frame": dets_per_frame, "h2d": h2d,
+                       "gather_bytes_per_rank": gatherer.bytes_per_rank if world > 1 else 0},
             "roofline": roof, "cpu_baseline": cpu,
         }
         if stages:
             line["stages_ms"] = stages
+        line.update(extra)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

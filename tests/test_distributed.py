@@ -20,6 +20,7 @@ def _free_port():
 
 
 def _rank_outputs(rank, F=3, D=16, R=28):
+    """Per-rank engine outputs; the masks are frame-major like the engine's."""
     rng = np.random.default_rng(100 + rank)
     counts = rng.integers(0, D + 1, F).astype(np.int32)
     dets = np.zeros((F, D, 5), np.float32)
@@ -36,24 +37,44 @@ def _worker(rank, world, port, outq):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from vosdetectron_amd.runner import ResultGatherer, shard_frames
+    from vosdetectron_amd.runner import ResultGatherer, frame_masks, shard_frames
     dets, cls, counts, masks = _rank_outputs(rank)
-    g = ResultGatherer(3, 16, 28, world, "cpu")
+    g = ResultGatherer(3, 16, 28, world, "cpu", mask_rows=48)
     out = g.gather(torch.from_numpy(dets), torch.from_numpy(cls), torch.from_numpy(counts),
-                   torch.from_numpy(masks), counts.tolist())
+                   torch.from_numpy(masks))
+    out = {k: v.clone() for k, v in out.items()}
+    per_frame = [frame_masks(out, 3, i).numpy().copy() for i in range(world * 3)]
     # double-buffered async path: two gathers in flight order, second slot
     p1 = g.gather_async(torch.from_numpy(dets), torch.from_numpy(cls), torch.from_numpy(counts),
-                        torch.from_numpy(masks), counts.tolist())
-    r1 = {k: v.clone() for k, v in p1.wait().items()}
+                        torch.from_numpy(masks))
+    r1 = p1.wait(clone=True)
     p2 = g.gather_async(torch.from_numpy(dets) + 1, torch.from_numpy(cls),
-                        torch.from_numpy(counts), torch.from_numpy(masks), counts.tolist())
+                        torch.from_numpy(counts), torch.from_numpy(masks))
     r2 = p2.wait()
     same = all(torch.equal(r1[k], out[k]) for k in out)
     shifted = torch.equal(r2["dets"], out["dets"] + 1) and torch.equal(r2["masks"], out["masks"])
+    # a view of a reused slot raises instead of showing a later step's rows
+    for _ in range(2):  # the gather after next reuses p2's slot
+        g.gather_async(torch.from_numpy(dets), torch.from_numpy(cls), torch.from_numpy(counts),
+                       torch.from_numpy(masks)).wait(views=False)
+    try:
+        p2.wait()
+        stale_raises = False
+    except RuntimeError:
+        stale_raises = True
+    # more masks than mask rows raises (never truncates)
+    try:
+        g.gather_async(torch.from_numpy(dets), torch.from_numpy(cls), torch.from_numpy(counts),
+                       torch.zeros((49, 28, 28)))
+        overflow_raises = False
+    except RuntimeError:
+        overflow_raises = True
     if rank == 0:
-        outq.put({k: v.numpy().copy() for k, v in out.items()})
+        got = {k: v.numpy().copy() for k, v in out.items()}
+        got["per_frame"] = per_frame
+        outq.put(got)
         outq.put(shard_frames(10, world, 1))
-        outq.put((same, shifted))
+        outq.put((same, shifted, stale_raises, overflow_raises))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -68,8 +89,8 @@ def test_gather_world2_gloo():
         p.start()
     got = q.get(timeout=120)
     shard = q.get(timeout=60)
-    same, shifted = q.get(timeout=60)
-    assert same and shifted
+    same, shifted, stale_raises, overflow_raises = q.get(timeout=60)
+    assert same and shifted and stale_raises and overflow_raises
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -81,7 +102,31 @@ def test_gather_world2_gloo():
         o = 0
         for f in range(3):
             k = n[f]
-            assert np.array_equal(got["masks"][r * 3 + f, :k], m[o:o + k])
-            assert not got["masks"][r * 3 + f, k:].any()
+            assert np.array_equal(got["per_frame"][r * 3 + f], m[o:o + k])
+            assert got["mask_offsets"][r, f] == o
             o += k
     assert shard == [5, 6, 7, 8, 9]
+
+
+def test_bench_launch_world2_dry_run():
+    """`bench.py --gpus 2` without a launcher spawns 2 ranks (torch.distributed.run)
+    and the bench line reports n_gpus from the live world; --dry-run runs the
+    packed all-gather on gloo and checks every gathered row."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--steps", "3", "--dry-run"], capture_output=True, text=True,
+                       timeout=300, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["dry_run"] and line["gather_ok"]
+    # a launcher world that disagrees with --gpus is refused
+    env2 = dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p2 = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                         "--dry-run"], capture_output=True, text=True, timeout=120, env=env2,
+                        cwd=root)
+    assert p2.returncode != 0 and "formed a world of 1" in p2.stderr

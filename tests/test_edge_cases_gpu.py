@@ -134,3 +134,69 @@ def test_proposals_size_limits():
         ops.generate_proposals([z], [torch.zeros((1, 60, 40, 60), device=DEV)],
                                [torch.from_numpy(an).to(DEV)], [1. / 16],
                                torch.tensor([[640., 960., 1.]], device=DEV), 8193, 1000, 0.7, 0)
+
+
+def test_proposals_unbracketable_topk_fails_loudly():
+    """a score map on which the top-k threshold search cannot bracket
+    pre_nms_topN within its candidate capacity (the sampled anchors score 0 but
+    four, every other anchor 0.5: 197k candidates tie between two adjacent
+    sample keys) must not drop the level silently -- its count is -1, which
+    collect_distribute and box_detections pass on and the engine raises on."""
+    from vosdetectron_amd import ops
+    from vosdetectron_amd._lib import VosdetError
+    H, W, A = 200, 336, 3
+    n_all, S = H * W * A, 2048  # kSampleMax
+    flat = np.full(n_all, 0.5, np.float32)  # element order e = (h*W + w)*A + a
+    samp = (np.arange(S, dtype=np.int64) * n_all) // S
+    flat[samp] = 0.0
+    flat[samp[:4]] = 1.0
+    p = flat.reshape(H * W, A).T.reshape(1, A, H, W).copy()
+    d = np.zeros((1, 4 * A, H, W), np.float32)
+    an = orc.fpn_level_anchors(2)
+    info = torch.tensor([[800., 1344., 1.]], device=DEV)
+    rois, pr, cnt = ops.generate_proposals(
+        [torch.from_numpy(p).to(DEV)], [torch.from_numpy(d).to(DEV)],
+        [torch.from_numpy(an).to(DEV)], [1. / 4], info, 1000, 1000, 0.7, 0)
+    assert cnt.cpu().tolist() == [[-1]]
+    cr, clv, ccnt = ops.collect_distribute(rois, pr, cnt, 1000, 2, 5)
+    assert ccnt.cpu().tolist() == [-1]
+    K = 81
+    dets, dcls, dcnt = ops.box_detections(
+        cr, torch.full((1, 1000, K), 0.5, device=DEV), torch.zeros((1, 1000, 4 * K), device=DEV),
+        ccnt, torch.ones(1, device=DEV), torch.tensor([[800, 1333]], dtype=torch.int32,
+                                                      device=DEV))
+    assert dcnt.cpu().tolist() == [-1]
+    with pytest.raises(VosdetError):
+        ops.raise_on_failed_counts(dcnt.cpu().tolist())
+
+
+def test_roi_align_fpn_malformed_indices_pool_to_zero():
+    """out-of-range level / batch indices from a caller of the public C
+    ABI pool to exactly zero (no out-of-bounds read); well-formed RoIs of the
+    same launch are unaffected; mismatched level shapes are rejected on the host."""
+    from vosdetectron_amd import ops
+    C = 256
+    lv0 = torch.randn(2, 20, 30, C, device=DEV)
+    lv1 = torch.randn(2, 10, 15, C, device=DEV)
+    rois = torch.tensor([[0, 4, 4, 60, 50], [5, 4, 4, 60, 50], [-1, 4, 4, 60, 50],
+                         [1, 10, 8, 70, 60], [0, 4, 4, 60, 50]], dtype=torch.float32,
+                        device=DEV)
+    lvl = torch.tensor([0, 0, 1, 1, 7], dtype=torch.int32, device=DEV)
+    for variant in ("8", "3"):
+        import os
+        os.environ["VOSDET_ROIALIGN_VARIANT"] = variant
+        try:
+            out = ops.roi_align_fpn([lv0, lv1], [0.25, 0.125], rois, lvl, 7, 2, out_layout="nhwc")
+        finally:
+            del os.environ["VOSDET_ROIALIGN_VARIANT"]
+        o = out.cpu().numpy()
+        assert not o[1].any() and not o[2].any() and not o[4].any()
+        good = ops.roi_align_fpn([lv0, lv1], [0.25, 0.125], rois[[0, 3]], lvl[[0, 3]], 7, 2,
+                                 out_layout="nhwc").cpu().numpy()
+        np.testing.assert_allclose(o[[0, 3]], good, rtol=1e-5, atol=1e-6)
+    f = torch.randn(2, 8, 10, 12, device=DEV)
+    got = ops.roi_align_forward(f, torch.tensor([[3., 0, 0, 20, 20]], device=DEV), 7, 7, 0.5, 2)
+    assert not got.cpu().numpy().any()
+    with pytest.raises(ValueError):
+        ops.roi_align_fpn([lv0, torch.randn(1, 10, 15, C, device=DEV)], [0.25, 0.125], rois,
+                          lvl, 7, 2)

@@ -18,7 +18,10 @@ if __name__ == "__main__":
     frames = int(os.environ.get("FRAMES", "8"))
     r = measure_roialign_roofline(torch.device("cuda"), frames=frames, R=R, P=P, use_order=order,
                                   out_layout=os.environ.get("OUT", "nhwc"),
-                                  deal=int(os.environ.get("XCD_DEAL", "8")))
+                                  deal=int(os.environ["XCD_DEAL"]) if "XCD_DEAL" in os.environ
+                                  else None,
+                                  window=int(os.environ["XCD_WINDOW"]) if "XCD_WINDOW" in os.environ
+                                  else None)
     r["variant"] = os.environ.get("VOSDET_ROIALIGN_VARIANT", "default")
     r["xcd_order"] = order
     print(json.dumps(r), flush=True)

@@ -215,3 +215,39 @@ CONFIGS = {
 
 def get(name: str) -> AttrDict:
     return copy.deepcopy(CONFIGS[name]())
+
+
+# The reference's module-global ``cfg`` (lib/core/config.py:25) that its
+# operators read (GenerateProposalsOp, collect/distribute): the package's op
+# mirrors read this one unless given a cfg explicitly.
+cfg = e2e_mask_rcnn_R_50_FPN_1x()
+
+
+def merge_cfg_from_file(path: str) -> None:
+    """config.py:1107-1111: merge a reference YAML into the global cfg in place."""
+    with open(path) as f:
+        _merge(yaml.safe_load(f) or {}, cfg)
+
+
+cfg_from_file = merge_cfg_from_file  # config.py:1113
+
+
+def merge_cfg_from_list(cfg_list) -> None:
+    """config.py:1121-1144: ['TEST.NMS', '0.4', ...] key/value pairs."""
+    if len(cfg_list) % 2:
+        raise ValueError("cfg_list must hold key/value pairs")
+    for key, val in zip(cfg_list[0::2], cfg_list[1::2]):
+        d = cfg
+        parts = key.split(".")
+        for p in parts[:-1]:
+            d = d[p]
+        if parts[-1] not in d:
+            raise KeyError("Non-existent config key: %s" % key)
+        d[parts[-1]] = _decode(val)
+
+
+def use(name: str) -> AttrDict:
+    """Replace the global cfg's contents with a named BASELINE configuration."""
+    cfg.clear()
+    cfg.update(get(name))
+    return cfg

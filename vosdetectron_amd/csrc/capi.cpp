@@ -67,6 +67,9 @@ int vd_roi_align_fpn_forward(const VdFeatLevel *levels, int num_levels, int B, i
         fa.W[l] = levels[l].W;
         fa.scale[l] = levels[l].spatial_scale;
     }
+    fa.L = num_levels;
+    fa.B = B;
+    fa.R = num_rois;
     if (output_layout != VD_LAYOUT_NCHW && output_layout != VD_LAYOUT_NHWC) return VD_ERR_ARG;
     if (layout == VD_LAYOUT_NHWC)
         return launch_roi_align_fpn_nhwc(fa, C, rois, roi_level, roi_order, num_rois, ah, aw,

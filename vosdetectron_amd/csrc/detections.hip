@@ -161,7 +161,8 @@ __global__ __launch_bounds__(1024) void class_nms_kernel(
     if (threadIdx.x == 0) ws.cls_count[slot] = kept;
 }
 
-__global__ __launch_bounds__(1024) void det_limit_kernel(int R_cap, int K, int dets_per_im,
+__global__ __launch_bounds__(1024) void det_limit_kernel(const int32_t *__restrict__ roi_count,
+                                                          int R_cap, int K, int dets_per_im,
                                                           int det_cap, DetWs ws,
                                                           float *__restrict__ dets_out,
                                                           int32_t *__restrict__ det_cls_out,
@@ -170,6 +171,10 @@ __global__ __launch_bounds__(1024) void det_limit_kernel(int R_cap, int K, int d
     __shared__ uint32_t hist[256];
     __shared__ int scratch[32];
     const int img = blockIdx.x;
+    if (roi_count[img] < 0) {  // proposal selection failed upstream: propagate, never hide
+        if (threadIdx.x == 0) det_count_out[img] = -1;
+        return;
+    }
     // prefix over classes 1..K-1 (K <= 1024)
     if (threadIdx.x == 0) {
         int o = 0;
@@ -238,7 +243,7 @@ int launch_box_detections(const float *rois, const float *cls_prob, const float 
     hipLaunchKernelGGL(class_nms_kernel, dim3(K - 1, num_images), dim3(1024), sizeof(ClsLds), s,
                        rois, cls_prob, bbox_pred, roi_count, R_cap, K, im_scale, im_hw,
                        score_thresh, nms_thresh, bw, ws);
-    hipLaunchKernelGGL(det_limit_kernel, dim3(num_images), dim3(1024), 0, s, R_cap, K,
+    hipLaunchKernelGGL(det_limit_kernel, dim3(num_images), dim3(1024), 0, s, roi_count, R_cap, K,
                        dets_per_im, det_cap, ws, dets_out, det_cls_out, det_count_out);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
@@ -266,6 +271,7 @@ __global__ __launch_bounds__(512) void det_postfilter_kernel(float *__restrict__
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     PostLds &L = *reinterpret_cast<PostLds *>(lds_raw);
     const int img = blockIdx.x, t = threadIdx.x;
+    if (counts[img] < 0) return;  // upstream failure stays visible (-1)
     const int k = min((int)counts[img], det_cap);  // det_cap <= kPostMax (launcher)
     float *d = dets + (size_t)img * det_cap * 5;
     int32_t *c = cls + (size_t)img * det_cap;

@@ -204,7 +204,8 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
             if (lo > hi) break;
             rank = (lo + hi) >> 1;
         }
-        if (ncand < 0) {  // cannot bracket: signal and bail out (host reports)
+        if (ncand < 0) {  // cannot bracket: count -1, which collect_distribute and the
+                          // detections propagate to the engine's host read (raises)
             if (threadIdx.x == 0) {
                 counts_out[slot] = -1;
                 if (GB) *gm = -1;
@@ -457,17 +458,22 @@ __global__ __launch_bounds__(1024) void collect_distribute_kernel(
     int32_t *__restrict__ count_out) {
     __shared__ uint64_t keys[kSelCap];
     __shared__ int offs[VD_MAX_LEVELS + 1];
+    __shared__ int failed;
     const int img = blockIdx.x;
     if (threadIdx.x == 0) {
         int o = 0;
+        failed = 0;
         for (int l = 0; l < num_levels; ++l) {
             offs[l] = o;
             const int c = level_counts[img * num_levels + l];
+            failed |= c < 0;  // a level's selection could not bracket its top-k
             o += c > 0 ? c : 0;
         }
         offs[num_levels] = o;
+        if (failed) count_out[img] = -1;
     }
     __syncthreads();
+    if (failed) return;
     const int n = offs[num_levels];
     const int np2 = next_pow2(n < 1 ? 1 : n);
     for (int q = threadIdx.x; q < np2; q += blockDim.x) {

@@ -45,7 +45,7 @@ __device__ __forceinline__ float bilinear_nchw(const float *__restrict__ plane, 
 }
 
 __global__ __launch_bounds__(256) void roi_align_fwd_nchw_kernel(
-    int64_t nthreads, const float *__restrict__ feat, float scale, int H, int W, int C,
+    int64_t nthreads, const float *__restrict__ feat, float scale, int B, int H, int W, int C,
     int PH, int PW, int sr, const float *__restrict__ rois, float *__restrict__ out) {
     for (int64_t index = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; index < nthreads;
          index += (int64_t)blockDim.x * gridDim.x) {
@@ -55,6 +55,10 @@ __global__ __launch_bounds__(256) void roi_align_fwd_nchw_kernel(
         int64_t n = index / PW / PH / C;
         const float *r = rois + n * 5;
         int b = (int)r[0];
+        if (b < 0 || b >= B) {  // out-of-range batch index: zero, never an OOB read
+            out[index] = 0.f;
+            continue;
+        }
         float sw = r[1] * scale, sh = r[2] * scale, ew = r[3] * scale, eh = r[4] * scale;
         float rw = fmaxf(ew - sw, 1.f), rh = fmaxf(eh - sh, 1.f);
         float bh = rh / PH, bw = rw / PW;
@@ -132,17 +136,23 @@ struct RoiGeom {
     float count;
 };
 
+// A RoI whose level index or batch index is out of range (a malformed caller of
+// the public C ABI) pools to exactly zero instead of reading out of bounds: its
+// box is moved far off the map, where every sample is out of range (y < -1).
 __device__ __forceinline__ RoiGeom roi_geom(const FpnLevels &fa, int C, const float *roi,
                                             int li, int PH, int PW, int sr) {
     RoiGeom g;
+    const int b = (int)roi[0];
+    const bool ok = li >= 0 && li < fa.L && b >= 0 && b < fa.B;
+    if (!ok) li = 0;
     g.H = fa.H[li];
     g.W = fa.W[li];
     const float scale = fa.scale[li];
-    const int b = (int)roi[0];
-    g.feat = fa.feat[li] + (int64_t)b * g.H * g.W * C;
-    g.sw = roi[1] * scale;
-    g.sh = roi[2] * scale;
-    float ew = roi[3] * scale, eh = roi[4] * scale;
+    g.feat = fa.feat[li] + (ok ? (int64_t)b * g.H * g.W * C : 0);
+    const float kOff = -1e30f;
+    g.sw = ok ? roi[1] * scale : kOff;
+    g.sh = ok ? roi[2] * scale : kOff;
+    float ew = ok ? roi[3] * scale : kOff, eh = ok ? roi[4] * scale : kOff;
     float rw = fmaxf(ew - g.sw, 1.f), rh = fmaxf(eh - g.sh, 1.f);
     g.bh = rh / PH;
     g.bw = rw / PW;
@@ -373,6 +383,7 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
     const int *__restrict__ roi_order, int P, int out_nhwc, float *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float tile[];  // [C][P][P] (NCHW out)
     const int r = roi_order ? roi_order[blockIdx.x] : (int)blockIdx.x;
+    if (r < 0 || r >= fa.R) return;  // malformed schedule entry: write nothing
     int li = roi_level ? roi_level[r] : 0;
     li = __builtin_amdgcn_readfirstlane(li);
     const RoiGeom g = roi_geom(fa, C, rois + (int64_t)r * 5, li, P, P, SR);
@@ -445,130 +456,118 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
     for (int i = n4 * 4 + threadIdx.x; i < C * P * P; i += blockDim.x) o[i] = tile[i];
 }
 
-// --------------------------------------------------------------------------
-// XCD channel-sliced separable forward, one workgroup per (RoI, slice) with
-// one wave per output row.  Keeping ~P waves per RoI keeps the number of RoIs
-// an XCD has in flight at what the full-pixel kernel has (~128), while the
-// bytes each RoI pulls into that XCD's L2 shrink 8x: the in-flight footprint
-// window (~3 MB of 128-B pixel slices) fits the 4 MiB L2, so overlapping RoIs
-// re-read from L2 instead of the fabric.  Per output row the wave
-//   1. loads its tap columns 8 at a time (lane group g = column slot, lane
-//      q = channel quad): one 1 KiB instruction = 8 pixel slices of one tap
-//      row; the vertical combine V(x) = sum_k w_k F(row_k, x) is lane-local;
-//   2. parks V in LDS (wave-private), then lane group g computes bin pw = g
-//      (g + 8 ...) from V(xl), V(xh) of its samples and stores 128 B.
-// Column slots: the contiguous range [xmin, xmax] of tap columns when it fits
-// NS slots (every RoI with sample spacing <= 1 px), else one slot per tap
-// (2 P SR <= NS).  Arithmetic order as roi_align_fpn_nhwc_sep_kernel.
-// Measured (variant 16, profiles/r01_roialign_pmc/xslice_v16.txt): fabric reads
-// drop to 642 MB per launch (= the compulsory 0.66 GB; variant 8 reads 1.17 GB)
-// and the L2 hit rate rises 0.54 -> 0.69, but the kernel runs 8x the waves
-// with the per-RoI prologue replicated per slice: 2.7x the VALU instructions
-// of variant 8, VALU-issue bound at ~510 us vs 306 us.  Kept as the record of
-// the locality experiment (and its persistent / slice-per-row-group cousins,
-// both slower); variant 8 stays the product kernel.
-// --------------------------------------------------------------------------
-struct SampleX {
-    int xl, xh;
-    float lx;
-    bool ok;
-};
 
+// --------------------------------------------------------------------------
+// XCD-sliced separable forward (variant 40).  Channel slice s (32 channels =
+// 128 B of every pyramid pixel) of every RoI runs on XCD s: block b takes slice
+// b % 8, which the round-robin dispatch places on XCD b % 8, so an XCD's 4 MiB
+// L2 only ever caches 1/8 of each pixel and the footprints of the RoIs it has
+// in flight (spatially sorted by xcd_roi_order) fit in it -- the 4.5x
+// inter-RoI footprint overlap is then served from L2 instead of the fabric.
+// One wave owns one (RoI, slice) and walks the P output rows; lane group
+// g = lane / 8 owns output bin pw = g (+8, +16 ...), lane q = lane % 8 owns 4
+// channels.  Per row the wave loads each bin's distinct tap columns (2 samples
+// x (xl, xh): usually 3 distinct) for every live tap row -- one 1 KiB wave load
+// fetches 8 bins' 128 B slices -- and combines them in exactly the order of
+// roi_align_fpn_nhwc_sep_kernel (V(x) = sum_k w_k F(row_k, x), then
+// acc += hx V(xl) + lx V(xh) per sample), so its output is bit-identical to the
+// separable kernel's.  The per-RoI geometry is computed once per (RoI, slice)
+// wave instead of once per (RoI, slice, row) as in the round-1 slice kernel.
+// --------------------------------------------------------------------------
 template <int SR>
-__device__ __forceinline__ SampleX sample_x(const RoiGeom &g, int j) {
-    const int pw = j / SR, ix = j - (j / SR) * SR;
-    float x = g.sw + pw * g.bw + (ix + .5f) * g.bw / SR;
-    SampleX sx;
-    sx.ok = !(x < -1.0f || x > (float)g.W);
-    if (x <= 0) x = 0;
-    int xl = (int)x, xh;
-    if (xl >= g.W - 1) { xh = xl = g.W - 1; x = (float)xl; } else xh = xl + 1;
-    sx.xl = xl;
-    sx.xh = xh;
-    sx.lx = x - xl;
-    return sx;
-}
-
-template <int SR, int NS>
-__global__ __launch_bounds__(512) void roi_align_fpn_nhwc_xslice2_kernel(
+__global__ __launch_bounds__(256) void roi_align_fpn_nhwc_xcd_kernel(
     FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
-    const int *__restrict__ roi_order, int P, float *__restrict__ out) {
-    __shared__ float4 vcol[8][NS][8];  // [wave][column slot][channel quad]
-    const int S = C >> 5;
-    const int s = blockIdx.x % S;
-    const int i = blockIdx.x / S;
+    const int *__restrict__ roi_order, int P, int nslice, float *__restrict__ out) {
+    const int s = blockIdx.x % nslice;
+    const int i = (blockIdx.x / nslice) * num_waves() + wave_id();
+    if (i >= fa.R) return;
     int r = roi_order ? roi_order[i] : i;
     r = __builtin_amdgcn_readfirstlane(r);
+    if (r < 0 || r >= fa.R) return;
     int li = roi_level ? roi_level[r] : 0;
     li = __builtin_amdgcn_readfirstlane(li);
     const RoiGeom g = roi_geom(fa, C, rois + (int64_t)r * 5, li, P, P, SR);
-    const int lane = lane_id(), wv = wave_id();
+    const int lane = lane_id();
     const int grp = lane >> 3, q = lane & 7;
     const int c0 = s * 32 + q * 4;
     const float *base = g.feat + c0;
-    const int64_t rowstride = (int64_t)g.W * C;
+    const int W = g.W;
+    const int64_t rowstride = (int64_t)W * C;
     const float inv = 1.f / g.count;
-    const int nsamp = P * SR;
-    // valid samples are a contiguous run [j0, j1] (x increases with j)
-    int j0 = 0, j1 = nsamp - 1;
-    while (j0 < nsamp && !sample_x<SR>(g, j0).ok) ++j0;
-    while (j1 >= j0 && !sample_x<SR>(g, j1).ok) --j1;
-    int xmin = 0, nslot = 0;
-    bool contiguous = true;
-    if (j0 <= j1) {
-        xmin = sample_x<SR>(g, j0).xl;
-        const int span = sample_x<SR>(g, j1).xh - xmin + 1;
-        contiguous = span <= NS;
-        nslot = contiguous ? span : 2 * nsamp;
-    }
-    float4 *vw = &vcol[wv][0][0];
-    for (int ph = wv; ph < P; ph += num_waves()) {
-        const RowTaps<SR> taps = row_taps<SR>(g, ph);
-        for (int c8 = 0; c8 < nslot; c8 += 8) {
-            const int slot = c8 + grp;
-            int col;
-            if (contiguous) {
-                col = xmin + slot;
-            } else {
-                const SampleX sx = sample_x<SR>(g, min(slot >> 1, nsamp - 1));
-                col = (slot & 1) ? sx.xh : sx.xl;
-            }
-            col = min(col, g.W - 1);
-            const bool ok = slot < nslot;
-            const float *p = base + (int64_t)col * C;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int pw = grp; pw < P; pw += 8) {
+        // the bin's SR sample columns (same for every output row)
+        int xl[SR], xh[SR];
+        float lx[SR];
+        bool vx[SR];
 #pragma unroll
-            for (int k = 0; k < 2 * SR; ++k)
-                if (taps.alive[k] && ok) {
-                    const float4 f = ld4(p + taps.row[k] * rowstride);
-                    v.x += taps.w[k] * f.x;
-                    v.y += taps.w[k] * f.y;
-                    v.z += taps.w[k] * f.z;
-                    v.w += taps.w[k] * f.w;
-                }
-            vw[slot * 8 + q] = v;
+        for (int ix = 0; ix < SR; ++ix) {
+            float x = g.sw + pw * g.bw + (ix + .5f) * g.bw / SR;
+            vx[ix] = !(x < -1.0f || x > (float)W);
+            if (x <= 0) x = 0;
+            int a = (int)x, b;
+            if (a >= W - 1) { b = a = W - 1; x = (float)a; } else b = a + 1;
+            xl[ix] = a;
+            xh[ix] = b;
+            lx[ix] = x - a;
         }
-        __builtin_amdgcn_wave_barrier();
-        for (int pw = grp; pw < P; pw += 8) {
+        // distinct tap columns: slot j = (sample j/2, xl|xh); dup[j] = earlier slot
+        // holding the same column (-1: load it), dead[j]: sample out of range
+        int col[2 * SR], dup[2 * SR];
+        bool need[2 * SR];
+#pragma unroll
+        for (int j = 0; j < 2 * SR; ++j) {
+            col[j] = (j & 1) ? xh[j >> 1] : xl[j >> 1];
+            need[j] = vx[j >> 1];
+            dup[j] = -1;
+#pragma unroll
+            for (int k = 0; k < j; ++k)
+                if (dup[j] < 0 && need[k] && dup[k] < 0 && col[k] == col[j]) dup[j] = k;
+        }
+        for (int ph = 0; ph < P; ++ph) {
+            const RowTaps<SR> taps = row_taps<SR>(g, ph);
+            float4 F[2 * SR][2 * SR];  // [tap row k][column slot j]
+#pragma unroll
+            for (int k = 0; k < 2 * SR; ++k) {
+                if (!taps.alive[k]) continue;  // wave-uniform
+                const float *rp = base + taps.row[k] * rowstride;
+#pragma unroll
+                for (int j = 0; j < 2 * SR; ++j)
+                    if (need[j] && dup[j] < 0) F[k][j] = ld4(rp + (int64_t)col[j] * C);
+            }
+            float4 V[2 * SR];
+#pragma unroll
+            for (int j = 0; j < 2 * SR; ++j) {
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int k = 0; k < 2 * SR; ++k)
+                    if (taps.alive[k]) {
+                        v.x += taps.w[k] * F[k][j].x;
+                        v.y += taps.w[k] * F[k][j].y;
+                        v.z += taps.w[k] * F[k][j].z;
+                        v.w += taps.w[k] * F[k][j].w;
+                    }
+                V[j] = v;
+            }
+#pragma unroll
+            for (int j = 1; j < 2 * SR; ++j)
+#pragma unroll
+                for (int k = 0; k < j; ++k)
+                    if (dup[j] == k) V[j] = V[k];
             float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int ix = 0; ix < SR; ++ix) {
-                const int j = pw * SR + ix;
-                const SampleX sx = sample_x<SR>(g, j);
-                if (!sx.ok) continue;
-                const int sa = contiguous ? sx.xl - xmin : 2 * j;
-                const int sb = contiguous ? sx.xh - xmin : 2 * j + 1;
-                const float4 va = vw[sa * 8 + q], vb = vw[sb * 8 + q];
-                const float lx = sx.lx, hx = 1.f - lx;
-                acc.x += hx * va.x + lx * vb.x;
-                acc.y += hx * va.y + lx * vb.y;
-                acc.z += hx * va.z + lx * vb.z;
-                acc.w += hx * va.w + lx * vb.w;
+                if (!vx[ix]) continue;
+                const float4 va = V[2 * ix], vb = V[2 * ix + 1];
+                const float hx = 1.f - lx[ix];
+                acc.x += hx * va.x + lx[ix] * vb.x;
+                acc.y += hx * va.y + lx[ix] * vb.y;
+                acc.z += hx * va.z + lx[ix] * vb.z;
+                acc.w += hx * va.w + lx[ix] * vb.w;
             }
-            *reinterpret_cast<float4 *>(out + (((int64_t)r * P + ph) * P + pw) * C + c0) =
-                make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+            vf4 o = {acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv};
+            __builtin_nontemporal_store(
+                o, reinterpret_cast<vf4 *>(out + (((int64_t)r * P + ph) * P + pw) * C + c0));
         }
-        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -579,6 +578,7 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_kernel(
     float *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float tile[];
     const int r = roi_order ? roi_order[blockIdx.x] : (int)blockIdx.x;
+    if (r < 0 || r >= fa.R) return;  // malformed schedule entry: write nothing
     const int row0 = blockIdx.y * rows_per_block;
     const int rows = min(rows_per_block, P - row0);
     int li = roi_level ? roi_level[r] : 0;
@@ -631,42 +631,6 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_kernel(
             const int c = i / seg, rem = i - c * seg;
             o[(int64_t)c * P * P + rem] = tile[i];
         }
-    }
-}
-
-// Speed-of-light probe (variant 30, measurement only -- NOT RoIAlign): the same
-// grid, block shape, RoI order and output writes as the separable kernel, but
-// each RoI reads its compulsory footprint (the SURVEY 8d rectangle of level
-// pixels) exactly once, one row per wave, with no sampling arithmetic.  Its time
-// is what any kernel that fetches per RoI pays for the memory traffic alone.
-__global__ __launch_bounds__(512) void roi_footprint_probe_kernel(
-    FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
-    const int *__restrict__ roi_order, int P, float *__restrict__ out) {
-    const int r = roi_order ? roi_order[blockIdx.x] : (int)blockIdx.x;
-    int li = roi_level ? roi_level[r] : 0;
-    li = __builtin_amdgcn_readfirstlane(li);
-    const float *roi = rois + (int64_t)r * 5;
-    const int H = fa.H[li], W = fa.W[li];
-    const float s = fa.scale[li];
-    const float *feat = fa.feat[li] + (int64_t)(int)roi[0] * H * W * C;
-    const float x1 = roi[1] * s, y1 = roi[2] * s, x2 = roi[3] * s, y2 = roi[4] * s;
-    const int xa = max((int)floorf(x1), 0), xb = min((int)floorf(fmaxf(x2, x1 + 1.f)) + 1, W - 1);
-    const int ya = max((int)floorf(y1), 0), yb = min((int)floorf(fmaxf(y2, y1 + 1.f)) + 1, H - 1);
-    const int lane = lane_id();
-    for (int c0 = 0; c0 < C; c0 += 256) {
-        const int c = c0 + lane * 4;
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int y = ya + wave_id(); y <= yb; y += num_waves())
-            for (int x = xa; x <= xb; ++x) {
-                const float4 v = ld4(feat + ((int64_t)y * W + x) * C + c);
-                acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-            }
-        for (int ph = wave_id(); ph < P; ph += num_waves())
-            for (int pw = 0; pw < P; ++pw) {
-                vf4 v = {acc.x, acc.y, acc.z, acc.w};
-                __builtin_nontemporal_store(
-                    v, reinterpret_cast<vf4 *>(out + (((int64_t)r * P + ph) * P + pw) * C + c));
-            }
     }
 }
 
@@ -727,11 +691,10 @@ static int grid_1d(int64_t n, int block) {
 int launch_roi_align_fwd_nchw(const float *feat, int B, int C, int H, int W, const float *rois,
                               int R, int PH, int PW, float scale, int sr, float *out,
                               hipStream_t s) {
-    (void)B;
     int64_t n = (int64_t)R * C * PH * PW;
     if (n == 0) return VD_OK;
     hipLaunchKernelGGL(roi_align_fwd_nchw_kernel, dim3(grid_1d(n, 256)), dim3(256), 0, s, n, feat,
-                       scale, H, W, C, PH, PW, sr, rois, out);
+                       scale, B, H, W, C, PH, PW, sr, rois, out);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
@@ -794,22 +757,11 @@ int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, con
     if (C % 4 != 0) return VD_ERR_SHAPE;
     const int variant = roialign_variant();
     if (out_nhwc) {  // product path: [R][P][P][C] written straight from registers
-        if (variant == 30 && PH == PW && C % 256 == 0) {  // speed-of-light probe (not RoIAlign)
-            hipLaunchKernelGGL(roi_footprint_probe_kernel, dim3(R), dim3(64 * (PH < 8 ? PH : 8)),
-                               0, s, fa, C, rois, lvl, order, PH, out);
-            return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
-        }
-        if (variant == 16 && sr == 2 && PH == PW && C % 32 == 0 && PH <= 16) {
-            const int64_t blocks = (int64_t)R * (C / 32);
-            const int waves = PH < 8 ? PH : 8;
-            if (PH <= 8)
-                hipLaunchKernelGGL((roi_align_fpn_nhwc_xslice2_kernel<2, 32>),
-                                   dim3((unsigned)blocks), dim3(64 * waves), 0, s, fa, C, rois,
-                                   lvl, order, PH, out);
-            else
-                hipLaunchKernelGGL((roi_align_fpn_nhwc_xslice2_kernel<2, 64>),
-                                   dim3((unsigned)blocks), dim3(64 * waves), 0, s, fa, C, rois,
-                                   lvl, order, PH, out);
+        if (variant == 40 && sr == 2 && PH == PW && C == 256) {
+            const int waves = 4, nslice = C / 32;
+            const int64_t blocks = (int64_t)((R + waves - 1) / waves) * nslice;
+            hipLaunchKernelGGL((roi_align_fpn_nhwc_xcd_kernel<2>), dim3((unsigned)blocks),
+                               dim3(64 * waves), 0, s, fa, C, rois, lvl, order, PH, nslice, out);
             return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
         }
         if (variant >= 8 && sr == 2 && PH == PW)

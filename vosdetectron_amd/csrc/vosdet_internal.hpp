@@ -14,6 +14,9 @@ struct FpnLevels {
     int H[VD_MAX_LEVELS];
     int W[VD_MAX_LEVELS];
     float scale[VD_MAX_LEVELS];
+    int L;  // levels in use
+    int B;  // images per level
+    int R;  // RoIs of the launch (bounds roi_order entries)
 };
 
 int launch_roi_align_fwd_nchw(const float *feat, int B, int C, int H, int W, const float *rois,

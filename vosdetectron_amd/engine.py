@@ -186,6 +186,7 @@ class FramePipeline:
             tst.DETECTIONS_PER_IM, cfg.MODEL.BBOX_REG_WEIGHTS, self.det_cap,
             nms_cross_class=tst.NMS_CROSS_CLASS, num_det_per_class_pre=tst.NUM_DET_PER_CLASS_PRE)
         counts = dcnt.cpu().tolist()  # the one host read: sizes the mask batch
+        ops.raise_on_failed_counts(counts)
         self._mark("misc_bbox")
         if max(counts) > self.det_cap:
             raise RuntimeError("detections exceed det_cap=%d: %s" % (self.det_cap, counts))

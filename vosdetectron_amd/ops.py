@@ -134,23 +134,39 @@ def roi_align_fpn(levels: Sequence[torch.Tensor], spatial_scales: Sequence[float
         raise ValueError("1..%d levels" % _lib.VD_MAX_LEVELS)
     r = _need(rois, "rois")
     nhwc = layout == "nhwc"
+    if r.dim() != 2 or r.shape[1] != 5:
+        raise ValueError("rois must be R x 5, got %s" % (tuple(r.shape),))
     descs = (_lib.VdFeatLevel * len(levels))()
     keep = []
+    BC = None
     for i, (t, sc) in enumerate(zip(levels, spatial_scales)):
         t = _need(t, "levels[%d]" % i)
+        if t.dim() != 4:
+            raise ValueError("levels[%d] must be 4-D" % i)
         keep.append(t)
         if nhwc:
             B, H, W, C = t.shape
         else:
             B, C, H, W = t.shape
+        if BC is not None and (B, C) != BC:
+            raise ValueError("levels[%d] has B, C = %s; levels[0] has %s" % (i, (B, C), BC))
+        BC = (B, C)
         descs[i] = _lib.VdFeatLevel(t.data_ptr(), H, W, float(sc))
     R = r.shape[0]
     onhwc = out_layout == "nhwc"
+    shape = (R, resolution, resolution, C) if onhwc else (R, C, resolution, resolution)
     if out is None:
-        shape = (R, resolution, resolution, C) if onhwc else (R, C, resolution, resolution)
         out = torch.empty(shape, dtype=torch.float32, device=r.device)
+    elif (tuple(out.shape) != shape or out.dtype != torch.float32 or not out.is_contiguous()
+          or out.device != r.device):
+        raise ValueError("out must be a contiguous float32 %s tensor on %s, got %s %s"
+                         % (shape, r.device, tuple(out.shape), out.dtype))
     if R == 0:
         return out
+    if roi_level is not None and tuple(roi_level.shape) != (R,):
+        raise ValueError("roi_level must have R = %d entries" % R)
+    if roi_order is not None and tuple(roi_order.shape) != (R,):
+        raise ValueError("roi_order must have R = %d entries" % R)
     lv = _need(roi_level, "roi_level", torch.int32) if roi_level is not None else None
     od = _need(roi_order, "roi_order", torch.int32) if roi_order is not None else None
     check(lib().vd_roi_align_fpn_forward(
@@ -165,12 +181,34 @@ def roi_align_fpn(levels: Sequence[torch.Tensor], spatial_scales: Sequence[float
 _ORDER_CACHE = {}
 
 
+def _deal(n: int, n_xcd: int, window: Optional[int]) -> np.ndarray:
+    """Block b -> position in the sorted order: inside each window of `window`
+    consecutive positions (the whole order by default), XCD k (b % n_xcd == k)
+    takes the k-th contiguous slice."""
+    p = np.empty(n, np.int64)
+    w = n if not window else int(window)
+    for start in range(0, n, w):
+        m = min(w, n - start)
+        per = -(-m // n_xcd)
+        b = np.arange(m)
+        slot = (b % n_xcd) * per + b // n_xcd
+        ok = slot < m
+        q = np.empty(m, np.int64)
+        q[ok] = slot[ok]
+        q[~ok] = np.setdiff1d(np.arange(m), slot[ok])
+        p[start:start + m] = q + start
+    return p
+
+
 def xcd_roi_order(rois: torch.Tensor, roi_level: torch.Tensor, n_xcd: int = 8,
-                  band: int = 8) -> torch.Tensor:
+                  band: int = 8, window: Optional[int] = None) -> torch.Tensor:
     """Scheduling permutation for roi_align_fpn (never changes results): RoIs
     sorted by (image, level, y-band of 8 level pixels, x) and dealt so that the
     blocks of one XCD (b % 8 equal) walk one contiguous slice of that order --
-    spatial neighbours, whose footprints overlap, run on the same L2."""
+    spatial neighbours, whose footprints overlap, run on the same L2.  With
+    `window` the dealing restarts every `window` positions (e.g. one frame's
+    RoIs), so all XCDs work on the same frame at a time; n_xcd=1 is the plain
+    spatial sort (the XCD-sliced kernel runs every RoI on every XCD)."""
     r = rois
     lv = roi_level.to(torch.int64)
     scale = torch.pow(2.0, -(lv + 2).to(torch.float32))
@@ -180,17 +218,12 @@ def xcd_roi_order(rois: torch.Tensor, roi_level: torch.Tensor, n_xcd: int = 8,
            + cx.clamp(0, 65535).to(torch.int64))
     srt = torch.argsort(key)
     n = r.shape[0]
-    perm = _ORDER_CACHE.get((n, n_xcd, r.device))
+    if n_xcd <= 1:
+        return srt.to(torch.int32).contiguous()
+    perm = _ORDER_CACHE.get((n, n_xcd, window, r.device))
     if perm is None:
-        per = -(-n // n_xcd)
-        b = np.arange(n)
-        slot = (b % n_xcd) * per + b // n_xcd
-        ok = slot < n
-        p = np.empty(n, np.int64)
-        p[ok] = slot[ok]
-        p[~ok] = np.setdiff1d(np.arange(n), slot[ok])
-        perm = torch.from_numpy(p).to(r.device)
-        _ORDER_CACHE[(n, n_xcd, r.device)] = perm
+        perm = torch.from_numpy(_deal(n, n_xcd, window)).to(r.device)
+        _ORDER_CACHE[(n, n_xcd, window, r.device)] = perm
     return srt[perm].to(torch.int32).contiguous()
 
 
@@ -405,6 +438,18 @@ def generate_proposals(cls_probs: Sequence[torch.Tensor], bbox_preds: Sequence[t
                                       counts.data_ptr(), ws.data_ptr(), ws.numel(), _stream()),
           "vd_generate_proposals")
     return rois, probs, counts
+
+
+def raise_on_failed_counts(counts, what: str = "frame"):
+    """-1 in a per-image count means a device kernel could not complete that
+    image (generate_proposals' top-k threshold search could not bracket
+    pre_nms_topN within its candidate capacity; collect_distribute and
+    box_detections pass the -1 on).  Raise instead of dropping proposals."""
+    bad = [i for i, c in enumerate(counts) if c < 0]
+    if bad:
+        raise _lib.VosdetError(
+            "proposal selection failed for %s(s) %s: the pre_nms_topN threshold search "
+            "could not bracket its candidates (count -1)" % (what, bad))
 
 
 def collect_distribute(level_rois, level_probs, level_counts, post_nms_topN: int, k_min: int = 2,

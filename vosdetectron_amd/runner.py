@@ -4,14 +4,18 @@ The reference range-shards a dataset over per-GPU subprocesses and collates
 pickled `all_boxes` / `all_segms` in the parent (lib/core/test_engine.py:168-213,
 lib/utils/subprocess.py:41-115).  Here every rank (one process per GPU,
 torch.distributed over RCCL/xGMI) runs the device-resident engine on its own
-frames, and ONE collective per step -- all_gather of fixed-size padded tensors --
-gives every rank all results (no reduction, so the gathered rows are bit-identical
-to the per-rank rows).  The same code runs on the gloo backend with CPU tensors,
-which is how the N>1 path is tested in a CPU container.
+frames, and ONE collective per step -- all_gather of a fixed-size packed buffer
+-- gives every rank all results (no reduction, so the gathered rows are
+bit-identical to the per-rank rows).  The same code runs on the gloo backend
+with CPU tensors, which is how the N>1 path is tested in a CPU container.
+
+Also here: `FrameUploader`, the per-step host->device frame upload that the
+§8d FPS definition puts inside the timed region (pinned host batches, copied on
+a side stream one step ahead of the compute that consumes them).
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -24,73 +28,176 @@ def shard_frames(n_frames: int, world: int, rank: int) -> Sequence[int]:
 
 
 class PendingGather:
-    """An in-flight all_gather (async_op) of one buffer slot."""
+    """An in-flight all_gather (async_op) of one buffer slot.
 
-    def __init__(self, work, gatherer, rbuf):
-        self.work, self.g, self.rbuf = work, gatherer, rbuf
+    The views `wait()` returns alias the gatherer's receive slot (the send slot
+    when world == 1).  Slots alternate, so a view stays valid until the
+    gather_async call after next; `wait(clone=True)` returns private copies for
+    callers that keep results longer.  A view read after its slot was reused
+    raises (generation check) instead of silently showing a later step's rows."""
 
-    def wait(self, views: bool = True) -> Dict[str, torch.Tensor]:
+    def __init__(self, work, gatherer, rbuf, slot, gen):
+        self.work, self.g, self.rbuf, self.slot, self.gen = work, gatherer, rbuf, slot, gen
+
+    def wait(self, views: bool = True, clone: bool = False) -> Dict[str, torch.Tensor]:
         """Orders the caller's stream after the collective; returns the gathered
-        results ([world*F, ...], rank-major) unless views=False."""
+        results (rank-major) unless views=False."""
         if self.work is not None:
             self.work.wait()
             self.work = None
-        return self.g._views(self.rbuf) if views else {}
+        if not views:
+            return {}
+        if self.g.gen[self.slot] != self.gen:
+            raise RuntimeError("gathered results of slot %d were overwritten by a later "
+                               "gather_async; wait(clone=True) keeps a private copy" % self.slot)
+        v = self.g._views(self.rbuf)
+        return {k: t.clone() for k, t in v.items()} if clone else v
 
 
 class ResultGatherer:
-    """Packs each rank's per-frame results -- dets [F,D,5], classes [F,D], counts
-    [F], class-selected masks padded to [F,D,R,R] -- into ONE flat fp32 buffer
-    (int32 fields bit-cast) and all-gathers it in a single collective.  Two
-    buffer slots alternate, so `gather_async` of step t can run on RCCL's stream
-    while step t+1 computes; `wait()` before the slot is reused (the caller
-    keeps at most one gather in flight)."""
+    """Packs each rank's per-step results into ONE flat fp32 buffer and
+    all-gathers it in a single collective:
+
+      dets [F, D, 5] | classes [F, D] (int32 bit-cast) | counts [F] (int32) |
+      masks [mask_rows, R, R]  (the class-selected fp32 masks of the step's
+                                M = sum(counts) detections, frame-major, as the
+                                engine produces them; rows >= M are padding)
+
+    Packing is three device copies (no host loop, no per-frame work): the
+    engine's masks are already frame-contiguous, so a frame's rows start at the
+    exclusive prefix sum of the counts, which receivers recompute on the device
+    (`frame_offsets`).  mask_rows defaults to F x DETECTIONS_PER_IM (100), the
+    most box_results_with_nms_and_limit keeps per frame barring exact score ties
+    at the 100th place; a step whose M exceeds it raises (never truncates).
+    With F = 16 that is 5.0 MB per rank per step (vs 12.8 MB for masks padded to
+    the engine's det_cap of 256 rows per frame), still exact fp32 -- the
+    reference's segm_results resizes the probabilities before thresholding, so a
+    pre-binarised mask would change its output.
+
+    Two buffer slots alternate, so `gather_async` of step t can run on RCCL's
+    stream while step t+1 computes; the caller keeps at most one gather in
+    flight (`wait()` before issuing the next)."""
 
     def __init__(self, frames_per_rank: int, det_cap: int, mask_res: int, world: int,
-                 device, with_masks: bool = True):
+                 device, with_masks: bool = True, mask_rows: Optional[int] = None):
         F, D, R = frames_per_rank, det_cap, mask_res
         self.F, self.D, self.R, self.world, self.with_masks = F, D, R, world, with_masks
+        self.mask_rows = int(mask_rows if mask_rows is not None else F * 100) if with_masks else 0
         self.o_cls = F * D * 5
         self.o_cnt = self.o_cls + F * D
         self.o_msk = self.o_cnt + F
-        self.L = self.o_msk + (F * D * R * R if with_masks else 0)
+        self.L = self.o_msk + self.mask_rows * R * R
         self.send = [torch.zeros((self.L,), device=device) for _ in range(2)]
         self.recv = [torch.zeros((world, self.L), device=device) for _ in range(2)]
         self.slot = 0
+        self.gen = [0, 0]
 
-    def _pack(self, buf, dets, classes, counts, masks, counts_host):
-        F, D, R = self.F, self.D, self.R
+    @property
+    def bytes_per_rank(self) -> int:
+        return 4 * self.L
+
+    def _pack(self, buf, dets, classes, counts, masks):
         buf[:self.o_cls].copy_(dets.reshape(-1))
         buf[self.o_cls:self.o_cnt].view(torch.int32).copy_(classes.reshape(-1))
         buf[self.o_cnt:self.o_msk].view(torch.int32).copy_(counts.reshape(-1))
         if self.with_masks:
-            pm = buf[self.o_msk:].view(F, D, R, R)
-            pm.zero_()
-            o = 0
-            for f, c in enumerate(counts_host):
-                if c:
-                    pm[f, :c] = masks[o:o + c]
-                o += c
+            M = masks.shape[0]
+            if M > self.mask_rows:
+                raise RuntimeError("%d masks in one step exceed the gather's %d mask rows "
+                                   "(build ResultGatherer with a larger mask_rows)"
+                                   % (M, self.mask_rows))
+            if M:
+                buf[self.o_msk:self.o_msk + M * self.R * self.R].copy_(masks.reshape(-1))
 
     def _views(self, rb):
         W, F, D, R = rb.shape[0], self.F, self.D, self.R
+        counts = rb[:, self.o_cnt:self.o_msk].contiguous().view(torch.int32)
         v = {"dets": rb[:, :self.o_cls].reshape(W * F, D, 5),
              "classes": rb[:, self.o_cls:self.o_cnt].contiguous().view(torch.int32)
                         .reshape(W * F, D),
-             "counts": rb[:, self.o_cnt:self.o_msk].contiguous().view(torch.int32).reshape(W * F),
-             "masks": rb[:, self.o_msk:].reshape(W * F, D, R, R) if self.with_masks else None}
+             "counts": counts.reshape(W * F)}
+        if self.with_masks:
+            v["masks"] = rb[:, self.o_msk:].reshape(W, self.mask_rows, R, R)
+            v["mask_offsets"] = self.frame_offsets(counts)
         return v
 
+    @staticmethod
+    def frame_offsets(counts: torch.Tensor) -> torch.Tensor:
+        """counts [W, F] int32 -> first mask row of every frame within its rank's
+        mask rows ([W, F] int64, exclusive prefix sum, on the counts' device)."""
+        c = counts.to(torch.int64)
+        return torch.cumsum(c, 1) - c
+
     def gather_async(self, dets: torch.Tensor, classes: torch.Tensor, counts: torch.Tensor,
-                     masks: torch.Tensor, counts_host: List[int]) -> PendingGather:
-        """dets [F,D,5], classes [F,D] int32, counts [F] int32, masks [M,R,R]."""
+                     masks: torch.Tensor, counts_host: Optional[List[int]] = None
+                     ) -> PendingGather:
+        """dets [F,D,5], classes [F,D] int32, counts [F] int32, masks [M,R,R] (the
+        engine's class-selected masks, frame-major).  counts_host is unused (kept
+        for callers of the round-1 signature)."""
         s = self.slot
         self.slot ^= 1
-        self._pack(self.send[s], dets, classes, counts, masks, counts_host)
+        self.gen[s] += 1
+        self._pack(self.send[s], dets, classes, counts, masks)
         if self.world == 1:
-            return PendingGather(None, self, self.send[s].view(1, -1))
+            return PendingGather(None, self, self.send[s].view(1, -1), s, self.gen[s])
         work = dist.all_gather_into_tensor(self.recv[s].view(-1), self.send[s], async_op=True)
-        return PendingGather(work, self, self.recv[s])
+        return PendingGather(work, self, self.recv[s], s, self.gen[s])
 
-    def gather(self, dets, classes, counts, masks, counts_host) -> Dict[str, torch.Tensor]:
-        return self.gather_async(dets, classes, counts, masks, counts_host).wait()
+    def gather(self, dets, classes, counts, masks, counts_host=None) -> Dict[str, torch.Tensor]:
+        return self.gather_async(dets, classes, counts, masks).wait()
+
+
+def frame_masks(views: Dict[str, torch.Tensor], frames_per_rank: int, frame: int
+                ) -> torch.Tensor:
+    """The gathered masks of global frame index `frame` (rank-major order)."""
+    r, f = divmod(frame, frames_per_rank)
+    o = int(views["mask_offsets"][r, f])
+    k = int(views["counts"][frame])
+    return views["masks"][r, o:o + k]
+
+
+class FrameUploader:
+    """Per-step H2D of the u8 frames (SURVEY.md §8d puts "H2D of the u8 frame"
+    inside the timed region).  Host batches live in pinned memory; `get(t)`
+    returns batch t's device copy with the current stream ordered after it, and
+    issues batch t+1's copy on a side stream so PCIe overlaps step t's compute.
+    Two device slots alternate; the copy into a slot waits for the compute
+    stream's event recorded after the step that last read it (`release`)."""
+
+    def __init__(self, host_batches: Sequence[np.ndarray], device):
+        self.device = torch.device(device)
+        self.host = [torch.from_numpy(np.ascontiguousarray(b)).pin_memory() for b in host_batches]
+        shape = self.host[0].shape
+        self.dev = [torch.empty(shape, dtype=torch.uint8, device=self.device) for _ in range(2)]
+        self.stream = torch.cuda.Stream(device=self.device)
+        self.ready = [torch.cuda.Event() for _ in range(2)]
+        self.free = [None, None]
+        self.issued = -1
+        self.nbytes = int(self.host[0].numel())
+
+    def _issue(self, t: int):
+        s = t % 2
+        with torch.cuda.stream(self.stream):
+            if self.free[s] is not None:
+                self.stream.wait_event(self.free[s])
+            self.dev[s].copy_(self.host[t % len(self.host)], non_blocking=True)
+            self.ready[s].record(self.stream)
+        self.issued = t
+
+    def get(self, t: int, prefetch: bool = True) -> torch.Tensor:
+        """prefetch=False on a timed region's last step (and a warm-up's): the
+        next region's first upload is then issued, and timed, inside it."""
+        if self.issued < t:
+            self._issue(t)
+        s = t % 2
+        torch.cuda.current_stream().wait_event(self.ready[s])
+        if prefetch:
+            self._issue(t + 1)  # overlaps this step's compute
+        return self.dev[s]
+
+    def release(self, t: int):
+        """Call after step t's work is queued: its slot may be overwritten once
+        the compute stream passes this point."""
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self.free[t % 2] = ev
