@@ -93,8 +93,7 @@ def xcd_order(rois, lvls, n_xcd=8):
 
 
 ROIALIGN_KERNEL = {"3": "vd::roi_align_fpn_nhwc_kernel<7,2,2> (reference order)",
-                   "8": "vd::roi_align_fpn_nhwc_sep_kernel<2,true> (separable, nt stores)",
-                   "40": "vd::roi_align_fpn_nhwc_xcd_kernel<2> (XCD channel slices)"}
+                   "8": "vd::roi_align_fpn_nhwc_sep_kernel<2,true> (separable, nt stores)"}
 
 
 # rocprofv3 --pmc passes of this exact launch (tools/prof_roialign.sh, separate
@@ -125,8 +124,8 @@ def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=Non
     rois_t = torch.from_numpy(rois_np).to(dev)
     lv_t = torch.from_numpy(lv_np).to(dev)
     variant = os.environ.get("VOSDET_ROIALIGN_VARIANT", "8")
-    if deal is None:  # the XCD-sliced kernel runs every RoI on every XCD: plain sort
-        deal = 1 if variant == "40" else 8
+    if deal is None:
+        deal = 8
     order = ops.xcd_roi_order(rois_t, lv_t, n_xcd=deal, window=window) if use_order else None
     shape = (frames * R, P, P, C) if out_layout == "nhwc" else (frames * R, C, P, P)
     out = torch.empty(shape, device=dev)
@@ -153,7 +152,7 @@ def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=Non
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "traffic_source": tsrc,
-            "kernel": ROIALIGN_KERNEL.get(os.environ.get("VOSDET_ROIALIGN_VARIANT", "8"),
+            "kernel": ROIALIGN_KERNEL.get(variant,
                                           "vd::roi_align_fpn_nhwc_kernel")
                       + (" (XCD-ordered)" if use_order else "") + ", out " + out_layout,
             "launch": "%d frames x %d RoIs, C=%d, P=%d, sr=%d" % (frames, R, C, P, sr),

@@ -189,3 +189,157 @@ __global__ __launch_bounds__(512) void roi_footprint_probe_kernel(
     }
 }
 
+
+
+// ==========================================================================
+// Round 2, variant 40b (profiles/r02_roialign/README.md): XCD channel slices,
+// lane group = tap column, LDS row exchange.  436 us vs 300 us for variant 8.
+// Launched as: blocks = ceil(R / 4) * (C / 32), 256 threads, roi_order =
+// xcd_roi_order(n_xcd=1).
+// ==========================================================================
+// --------------------------------------------------------------------------
+// XCD-sliced separable forward (variant 40).  Channel slice s (32 channels =
+// 128 B of every pyramid pixel) of every RoI runs on XCD s: block b takes slice
+// b % 8, which the round-robin dispatch places on XCD b % 8, so an XCD's 4 MiB
+// L2 only caches 1/8 of each pixel and the footprints of the RoIs it has in
+// flight (spatially sorted, xcd_roi_order with n_xcd = 1) fit in it: the 4.5x
+// inter-RoI footprint overlap is served from L2 and the fabric moves about the
+// compulsory bytes (variant 8 re-fetches ~1.6x of them).
+// One wave owns one (RoI, slice) and walks the P output rows.  Per row it loads
+// the RoI's tap columns [xmin, xmax] eight at a time -- lane group g = lane / 8
+// holds column xmin + 8c + g, lane q = lane % 8 four channels, so one 1 KiB wave
+// load fetches eight pixel slices and every pixel slice is fetched once per row
+// (the separable kernel's sliding-window count) -- and combines the live tap
+// rows into V(x) = sum_k w_k F(row_k, x) in registers.  V goes to a
+// wave-private LDS row; then lane group g computes bin pw = g (+8, ...) as
+// acc += hx V(xl) + lx V(xh) per sample.  Same arithmetic, same order as
+// roi_align_fpn_nhwc_sep_kernel: bit-identical outputs.
+// --------------------------------------------------------------------------
+static constexpr int kXcdMaxSpan = 64;  // tap columns per RoI row held in LDS
+
+template <int SR>
+__global__ __launch_bounds__(256) void roi_align_fpn_nhwc_xcd_kernel(
+    FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
+    const int *__restrict__ roi_order, int P, int nslice, float *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float4 vrow[4][kXcdMaxSpan][8];
+    const int s = blockIdx.x % nslice;
+    const int wv = wave_id();
+    const int i = (blockIdx.x / nslice) * num_waves() + wv;
+    if (i >= fa.R) return;  // wave-uniform; no block-wide barrier below
+    int r = roi_order ? roi_order[i] : i;
+    r = __builtin_amdgcn_readfirstlane(r);
+    if (r < 0 || r >= fa.R) return;
+    int li = roi_level ? roi_level[r] : 0;
+    li = __builtin_amdgcn_readfirstlane(li);
+    const RoiGeom g = roi_geom(fa, C, rois + (int64_t)r * 5, li, P, P, SR);
+    const int lane = lane_id();
+    const int grp = lane >> 3, q = lane & 7;
+    const int c0 = s * 32 + q * 4;
+    const float *base = g.feat + c0;
+    const int W = g.W;
+    const int64_t rowstride = (int64_t)W * C;
+    const float inv = 1.f / g.count;
+    // tap-column range of the valid samples (x grows with the sample index)
+    int xmin = 1 << 30, xmax = -1;
+    for (int j = 0; j < P * SR; ++j) {
+        const int pw = j / SR, ix = j - pw * SR;
+        float x = g.sw + pw * g.bw + (ix + .5f) * g.bw / SR;
+        if (x < -1.0f || x > (float)W) continue;
+        if (x <= 0) x = 0;
+        int a = (int)x, b;
+        if (a >= W - 1) { b = a = W - 1; } else b = a + 1;
+        xmin = min(xmin, a);
+        xmax = max(xmax, b);
+    }
+    const int span = xmax >= xmin ? xmax - xmin + 1 : 0;
+    if (span > kXcdMaxSpan) {
+        // RoIs wider than the LDS row (extreme aspect ratios): each lane group
+        // fetches its own bin's tap columns straight from memory (same order)
+        for (int ph = 0; ph < P; ++ph) {
+            const RowTaps<SR> taps = row_taps<SR>(g, ph);
+            for (int pw = grp; pw < P; pw += 8) {
+                auto column = [&](int x) -> float4 {
+                    return combine_column<SR>(
+                        taps, load_column<SR>(taps, base, rowstride, (int64_t)x * C));
+                };
+                int cl = -1, ch = -1;
+                float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va, acc = va;
+#pragma unroll
+                for (int ix = 0; ix < SR; ++ix) {
+                    float x = g.sw + pw * g.bw + (ix + .5f) * g.bw / SR;
+                    if (x < -1.0f || x > (float)W) continue;
+                    if (x <= 0) x = 0;
+                    int xl = (int)x, xh;
+                    if (xl >= W - 1) { xh = xl = W - 1; x = (float)xl; } else xh = xl + 1;
+                    const float lx = x - xl, hx = 1.f - lx;
+                    if (xl != cl || xh != ch) {
+                        if (xl == ch) va = vb;
+                        else va = column(xl);
+                        vb = (xh == xl) ? va : column(xh);
+                        cl = xl;
+                        ch = xh;
+                    }
+                    acc.x += hx * va.x + lx * vb.x;
+                    acc.y += hx * va.y + lx * vb.y;
+                    acc.z += hx * va.z + lx * vb.z;
+                    acc.w += hx * va.w + lx * vb.w;
+                }
+                vf4 o = {acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv};
+                __builtin_nontemporal_store(
+                    o, reinterpret_cast<vf4 *>(out + (((int64_t)r * P + ph) * P + pw) * C + c0));
+            }
+        }
+        return;
+    }
+    const int nchunk = (span + 7) >> 3;
+    float4(*vw)[8] = vrow[wv];
+    for (int ph = 0; ph < P; ++ph) {
+        const RowTaps<SR> taps = row_taps<SR>(g, ph);
+        for (int c = 0; c < nchunk; ++c) {
+            const int col = xmin + c * 8 + grp;
+            const bool in = col <= xmax;
+            const float *p = base + (int64_t)(in ? col : xmin) * C;
+            float4 f[2 * SR];
+#pragma unroll
+            for (int k = 0; k < 2 * SR; ++k)
+                if (taps.alive[k]) f[k] = ld4(p + taps.row[k] * rowstride);
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int k = 0; k < 2 * SR; ++k)
+                if (taps.alive[k]) {
+                    v.x += taps.w[k] * f[k].x;
+                    v.y += taps.w[k] * f[k].y;
+                    v.z += taps.w[k] * f[k].z;
+                    v.w += taps.w[k] * f[k].w;
+                }
+            vw[c * 8 + grp][q] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int pw = grp; pw < P; pw += 8) {
+            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int ix = 0; ix < SR; ++ix) {
+                float x = g.sw + pw * g.bw + (ix + .5f) * g.bw / SR;
+                if (x < -1.0f || x > (float)W) continue;
+                if (x <= 0) x = 0;
+                int xl = (int)x, xh;
+                if (xl >= W - 1) { xh = xl = W - 1; x = (float)xl; } else xh = xl + 1;
+                const float lx = x - xl, hx = 1.f - lx;
+                const float4 va = vw[xl - xmin][q], vb = vw[xh - xmin][q];
+                acc.x += hx * va.x + lx * vb.x;
+                acc.y += hx * va.y + lx * vb.y;
+                acc.z += hx * va.z + lx * vb.z;
+                acc.w += hx * va.w + lx * vb.w;
+            }
+            vf4 o = {acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv};
+            __builtin_nontemporal_store(
+                o, reinterpret_cast<vf4 *>(out + (((int64_t)r * P + ph) * P + pw) * C + c0));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+

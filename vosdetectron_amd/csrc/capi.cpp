@@ -49,17 +49,12 @@ int vd_roi_align_backward(int ah, int aw, float spatial_scale, int sampling_rati
                                      sampling_ratio, bottom_grad, VD_STREAM(stream));
 }
 
-int vd_roi_align_fpn_forward(const VdFeatLevel *levels, int num_levels, int B, int C, int layout,
-                             const float *rois, const int32_t *roi_level,
-                             const int32_t *roi_order, int num_rois, int ah, int aw,
-                             int sampling_ratio, int output_layout, float *output,
-                             void *stream) {
-    if (num_rois == 0) return VD_OK;
-    if (!levels || num_levels < 1 || num_levels > VD_MAX_LEVELS || !rois || !output || B < 1 ||
-        C < 1 || ah < 1 || aw < 1 || num_rois < 0)
+static int fpn_levels(const VdFeatLevel *levels, int num_levels, int B, int C, int num_rois,
+                      FpnLevels &fa) {
+    if (!levels || num_levels < 1 || num_levels > VD_MAX_LEVELS || B < 1 || C < 1 ||
+        num_rois < 0)
         return VD_ERR_ARG;
-    if (num_levels > 1 && !roi_level) return VD_ERR_ARG;
-    FpnLevels fa = {};
+    fa = FpnLevels{};
     for (int l = 0; l < num_levels; ++l) {
         if (bad_feat(levels[l].data, B, C, levels[l].H, levels[l].W)) return VD_ERR_ARG;
         fa.feat[l] = levels[l].data;
@@ -70,6 +65,20 @@ int vd_roi_align_fpn_forward(const VdFeatLevel *levels, int num_levels, int B, i
     fa.L = num_levels;
     fa.B = B;
     fa.R = num_rois;
+    return VD_OK;
+}
+
+int vd_roi_align_fpn_forward(const VdFeatLevel *levels, int num_levels, int B, int C, int layout,
+                             const float *rois, const int32_t *roi_level,
+                             const int32_t *roi_order, int num_rois, int ah, int aw,
+                             int sampling_ratio, int output_layout, float *output,
+                             void *stream) {
+    if (num_rois == 0) return VD_OK;
+    if (!rois || !output || ah < 1 || aw < 1) return VD_ERR_ARG;
+    if (num_levels > 1 && !roi_level) return VD_ERR_ARG;
+    FpnLevels fa;
+    const int st = fpn_levels(levels, num_levels, B, C, num_rois, fa);
+    if (st != VD_OK) return st;
     if (output_layout != VD_LAYOUT_NCHW && output_layout != VD_LAYOUT_NHWC) return VD_ERR_ARG;
     if (layout == VD_LAYOUT_NHWC)
         return launch_roi_align_fpn_nhwc(fa, C, rois, roi_level, roi_order, num_rois, ah, aw,

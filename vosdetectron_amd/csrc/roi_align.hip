@@ -21,6 +21,7 @@
 #include <stdlib.h>
 
 #include "common.hpp"
+#include "roi_geom.hpp"
 #include "vosdet_internal.hpp"
 
 namespace vd {
@@ -125,43 +126,6 @@ __global__ __launch_bounds__(256) void roi_align_bwd_nchw_kernel(
     }
 }
 
-// --------------------------------------------------------------------------
-// NHWC multi-level forward.
-// --------------------------------------------------------------------------
-struct RoiGeom {
-    const float *feat;  // this RoI's image base in its level
-    int H, W;
-    float sw, sh, bw, bh;
-    int gh, gw;
-    float count;
-};
-
-// A RoI whose level index or batch index is out of range (a malformed caller of
-// the public C ABI) pools to exactly zero instead of reading out of bounds: its
-// box is moved far off the map, where every sample is out of range (y < -1).
-__device__ __forceinline__ RoiGeom roi_geom(const FpnLevels &fa, int C, const float *roi,
-                                            int li, int PH, int PW, int sr) {
-    RoiGeom g;
-    const int b = (int)roi[0];
-    const bool ok = li >= 0 && li < fa.L && b >= 0 && b < fa.B;
-    if (!ok) li = 0;
-    g.H = fa.H[li];
-    g.W = fa.W[li];
-    const float scale = fa.scale[li];
-    g.feat = fa.feat[li] + (ok ? (int64_t)b * g.H * g.W * C : 0);
-    const float kOff = -1e30f;
-    g.sw = ok ? roi[1] * scale : kOff;
-    g.sh = ok ? roi[2] * scale : kOff;
-    float ew = ok ? roi[3] * scale : kOff, eh = ok ? roi[4] * scale : kOff;
-    float rw = fmaxf(ew - g.sw, 1.f), rh = fmaxf(eh - g.sh, 1.f);
-    g.bh = rh / PH;
-    g.bw = rw / PW;
-    g.gh = sr > 0 ? sr : (int)ceilf(rh / PH);
-    g.gw = sr > 0 ? sr : (int)ceilf(rw / PW);
-    g.count = (float)(g.gh * g.gw);
-    return g;
-}
-
 __device__ __forceinline__ void bilerp_acc(float4 &acc, float w1, float w2, float w3, float w4,
                                            const float4 &a, const float4 &b, const float4 &c,
                                            const float4 &d) {
@@ -171,9 +135,6 @@ __device__ __forceinline__ void bilerp_acc(float4 &acc, float w1, float w2, floa
     acc.w += (w1 * a.w + w2 * b.w + w3 * c.w + w4 * d.w);
 }
 
-__device__ __forceinline__ float4 ld4(const float *p) {
-    return *reinterpret_cast<const float4 *>(p);
-}
 
 // One wave computes output row `ph` for 256 channels starting at c0 (lane owns
 // c0 + 4*lane .. +3); acc[P] lives in registers.
@@ -291,89 +252,10 @@ __device__ __forceinline__ void nhwc_row_sr(const RoiGeom &g, int C, int ph, int
     }
 }
 
-// --------------------------------------------------------------------------
-// Separable NHWC forward.  Bilinear sampling on a tensor-product grid factors:
-//   sum_{iy,ix} [hy hx F(yl,xl) + hy lx F(yl,xh) + ly hx F(yh,xl) + ly lx F(yh,xh)]
-//     = sum_ix [hx V(xl) + lx V(xh)],   V(x) = sum_iy [hy F(yl,x) + ly F(yh,x)],
-// with out-of-range samples dropping out of either sum.  Per output row the
-// 2*SR y taps are merged into distinct pixel rows (usually 2-3), and V(x) is
-// computed once per distinct column while the x samples sweep left to right
-// (their columns are non-decreasing), so a 1 KiB pixel is fetched ~once per row
-// instead of once per tap: ~4x fewer vector-memory instructions than
-// nhwc_row_sr, which is what bounds the gather (texture-addresser issue).  Each
-// bin is finished and stored before the next starts, so no per-row accumulator
-// array is live (low VGPRs, high occupancy).  Rounding differs from the
-// reference's per-sample order by a few ulp (north_star's RoIAlign tolerance is
-// 1e-4 fp32); the bit-exact kernels above stay selectable.
-// --------------------------------------------------------------------------
-template <int SR>
-struct RowTaps {
-    int row[2 * SR];
-    float w[2 * SR];
-    bool alive[2 * SR];
-};
 
-template <int SR>
-__device__ __forceinline__ RowTaps<SR> row_taps(const RoiGeom &g, int ph) {
-    RowTaps<SR> t;
-    const int H = g.H;
-#pragma unroll
-    for (int iy = 0; iy < SR; ++iy) {
-        float y = g.sh + ph * g.bh + (iy + .5f) * g.bh / SR;
-        const bool ok = !(y < -1.0f || y > (float)H);
-        if (y <= 0) y = 0;
-        int yl = (int)y, yh;
-        if (yl >= H - 1) { yh = yl = H - 1; y = (float)yl; } else yh = yl + 1;
-        const float ly = y - yl;
-        t.row[2 * iy] = yl;
-        t.w[2 * iy] = 1.f - ly;
-        t.alive[2 * iy] = ok;
-        t.row[2 * iy + 1] = yh;
-        t.w[2 * iy + 1] = ly;
-        t.alive[2 * iy + 1] = ok;
-    }
-#pragma unroll
-    for (int k = 1; k < 2 * SR; ++k)
-#pragma unroll
-        for (int k2 = 0; k2 < k; ++k2)
-            if (t.alive[k] && t.alive[k2] && t.row[k2] == t.row[k]) {
-                t.w[k2] += t.w[k];
-                t.alive[k] = false;
-            }
-    return t;
-}
 
-template <int SR>
-struct TapCol {
-    float4 f[2 * SR];
-};
-
-template <int SR>
-__device__ __forceinline__ TapCol<SR> load_column(const RowTaps<SR> &t, const float *base,
-                                                  int64_t rowstride, int64_t xoff) {
-    TapCol<SR> c;
-#pragma unroll
-    for (int k = 0; k < 2 * SR; ++k)
-        if (t.alive[k]) c.f[k] = ld4(base + t.row[k] * rowstride + xoff);
-    return c;
-}
-
-template <int SR>
-__device__ __forceinline__ float4 combine_column(const RowTaps<SR> &t, const TapCol<SR> &c) {
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int k = 0; k < 2 * SR; ++k)
-        if (t.alive[k]) {
-            v.x += t.w[k] * c.f[k].x;
-            v.y += t.w[k] * c.f[k].y;
-            v.z += t.w[k] * c.f[k].z;
-            v.w += t.w[k] * c.f[k].w;
-        }
-    return v;
-}
-
-typedef float vf4 __attribute__((ext_vector_type(4)));
-
+// Separable NHWC forward (variant 8, the product kernel): see roi_geom.hpp for
+// the row-tap / column decomposition it uses.
 // NT: output rows are written once and never re-read by this launch; storing
 // them non-temporal keeps them from evicting pyramid lines that overlapping
 // RoIs on the same XCD are about to re-read from L2.
@@ -456,120 +338,6 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
     for (int i = n4 * 4 + threadIdx.x; i < C * P * P; i += blockDim.x) o[i] = tile[i];
 }
 
-
-// --------------------------------------------------------------------------
-// XCD-sliced separable forward (variant 40).  Channel slice s (32 channels =
-// 128 B of every pyramid pixel) of every RoI runs on XCD s: block b takes slice
-// b % 8, which the round-robin dispatch places on XCD b % 8, so an XCD's 4 MiB
-// L2 only ever caches 1/8 of each pixel and the footprints of the RoIs it has
-// in flight (spatially sorted by xcd_roi_order) fit in it -- the 4.5x
-// inter-RoI footprint overlap is then served from L2 instead of the fabric.
-// One wave owns one (RoI, slice) and walks the P output rows; lane group
-// g = lane / 8 owns output bin pw = g (+8, +16 ...), lane q = lane % 8 owns 4
-// channels.  Per row the wave loads each bin's distinct tap columns (2 samples
-// x (xl, xh): usually 3 distinct) for every live tap row -- one 1 KiB wave load
-// fetches 8 bins' 128 B slices -- and combines them in exactly the order of
-// roi_align_fpn_nhwc_sep_kernel (V(x) = sum_k w_k F(row_k, x), then
-// acc += hx V(xl) + lx V(xh) per sample), so its output is bit-identical to the
-// separable kernel's.  The per-RoI geometry is computed once per (RoI, slice)
-// wave instead of once per (RoI, slice, row) as in the round-1 slice kernel.
-// --------------------------------------------------------------------------
-template <int SR>
-__global__ __launch_bounds__(256) void roi_align_fpn_nhwc_xcd_kernel(
-    FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
-    const int *__restrict__ roi_order, int P, int nslice, float *__restrict__ out) {
-    const int s = blockIdx.x % nslice;
-    const int i = (blockIdx.x / nslice) * num_waves() + wave_id();
-    if (i >= fa.R) return;
-    int r = roi_order ? roi_order[i] : i;
-    r = __builtin_amdgcn_readfirstlane(r);
-    if (r < 0 || r >= fa.R) return;
-    int li = roi_level ? roi_level[r] : 0;
-    li = __builtin_amdgcn_readfirstlane(li);
-    const RoiGeom g = roi_geom(fa, C, rois + (int64_t)r * 5, li, P, P, SR);
-    const int lane = lane_id();
-    const int grp = lane >> 3, q = lane & 7;
-    const int c0 = s * 32 + q * 4;
-    const float *base = g.feat + c0;
-    const int W = g.W;
-    const int64_t rowstride = (int64_t)W * C;
-    const float inv = 1.f / g.count;
-    for (int pw = grp; pw < P; pw += 8) {
-        // the bin's SR sample columns (same for every output row)
-        int xl[SR], xh[SR];
-        float lx[SR];
-        bool vx[SR];
-#pragma unroll
-        for (int ix = 0; ix < SR; ++ix) {
-            float x = g.sw + pw * g.bw + (ix + .5f) * g.bw / SR;
-            vx[ix] = !(x < -1.0f || x > (float)W);
-            if (x <= 0) x = 0;
-            int a = (int)x, b;
-            if (a >= W - 1) { b = a = W - 1; x = (float)a; } else b = a + 1;
-            xl[ix] = a;
-            xh[ix] = b;
-            lx[ix] = x - a;
-        }
-        // distinct tap columns: slot j = (sample j/2, xl|xh); dup[j] = earlier slot
-        // holding the same column (-1: load it), dead[j]: sample out of range
-        int col[2 * SR], dup[2 * SR];
-        bool need[2 * SR];
-#pragma unroll
-        for (int j = 0; j < 2 * SR; ++j) {
-            col[j] = (j & 1) ? xh[j >> 1] : xl[j >> 1];
-            need[j] = vx[j >> 1];
-            dup[j] = -1;
-#pragma unroll
-            for (int k = 0; k < j; ++k)
-                if (dup[j] < 0 && need[k] && dup[k] < 0 && col[k] == col[j]) dup[j] = k;
-        }
-        for (int ph = 0; ph < P; ++ph) {
-            const RowTaps<SR> taps = row_taps<SR>(g, ph);
-            float4 F[2 * SR][2 * SR];  // [tap row k][column slot j]
-#pragma unroll
-            for (int k = 0; k < 2 * SR; ++k) {
-                if (!taps.alive[k]) continue;  // wave-uniform
-                const float *rp = base + taps.row[k] * rowstride;
-#pragma unroll
-                for (int j = 0; j < 2 * SR; ++j)
-                    if (need[j] && dup[j] < 0) F[k][j] = ld4(rp + (int64_t)col[j] * C);
-            }
-            float4 V[2 * SR];
-#pragma unroll
-            for (int j = 0; j < 2 * SR; ++j) {
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-                for (int k = 0; k < 2 * SR; ++k)
-                    if (taps.alive[k]) {
-                        v.x += taps.w[k] * F[k][j].x;
-                        v.y += taps.w[k] * F[k][j].y;
-                        v.z += taps.w[k] * F[k][j].z;
-                        v.w += taps.w[k] * F[k][j].w;
-                    }
-                V[j] = v;
-            }
-#pragma unroll
-            for (int j = 1; j < 2 * SR; ++j)
-#pragma unroll
-                for (int k = 0; k < j; ++k)
-                    if (dup[j] == k) V[j] = V[k];
-            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int ix = 0; ix < SR; ++ix) {
-                if (!vx[ix]) continue;
-                const float4 va = V[2 * ix], vb = V[2 * ix + 1];
-                const float hx = 1.f - lx[ix];
-                acc.x += hx * va.x + lx[ix] * vb.x;
-                acc.y += hx * va.y + lx[ix] * vb.y;
-                acc.z += hx * va.z + lx[ix] * vb.z;
-                acc.w += hx * va.w + lx[ix] * vb.w;
-            }
-            vf4 o = {acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv};
-            __builtin_nontemporal_store(
-                o, reinterpret_cast<vf4 *>(out + (((int64_t)r * P + ph) * P + pw) * C + c0));
-        }
-    }
-}
 
 template <int P, int SR, int D>
 __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_kernel(
@@ -732,8 +500,10 @@ static int launch_rows(const FpnLevels &fa, int C, const float *rois, const int 
 
 static int roialign_variant() {  // read per launch so tests can switch kernels
     const char *e = getenv("VOSDET_ROIALIGN_VARIANT");
-    // 8: separable kernel (product default, RoIAlign tolerance 1e-4);
-    // 3: bit-exact row kernel (the reference's per-sample arithmetic order)
+    // 8: separable kernel (product default, RoIAlign tolerance 1e-4 vs the
+    //    reference's per-sample order); 3: bit-exact row kernel (the reference's
+    //    per-sample arithmetic order).  Round-2 alternatives (XCD channel slices,
+    //    tile-binned LDS windows) are in tools/research/ with their measurements.
     return e ? atoi(e) : 8;
 }
 
@@ -757,13 +527,6 @@ int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, con
     if (C % 4 != 0) return VD_ERR_SHAPE;
     const int variant = roialign_variant();
     if (out_nhwc) {  // product path: [R][P][P][C] written straight from registers
-        if (variant == 40 && sr == 2 && PH == PW && C == 256) {
-            const int waves = 4, nslice = C / 32;
-            const int64_t blocks = (int64_t)((R + waves - 1) / waves) * nslice;
-            hipLaunchKernelGGL((roi_align_fpn_nhwc_xcd_kernel<2>), dim3((unsigned)blocks),
-                               dim3(64 * waves), 0, s, fa, C, rois, lvl, order, PH, nslice, out);
-            return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
-        }
         if (variant >= 8 && sr == 2 && PH == PW)
             return launch_sep(fa, C, rois, lvl, order, R, PH, 1, out, s);
         if (PH == PW && PH == 7)
