@@ -113,16 +113,32 @@ int vd_roi_pool_backward(const float *top_grad, const int32_t *argmax, int64_t n
 int vd_roi_crop_forward(const float *input, int B, int C, int H, int W, const float *grid_yx,
                         int num_rois, int GH, int GW, float *output, void *stream);
 
+/* 1x1 convolution on channels_last tensors as a GEMM with the conv epilogue
+ * fused (hipBLASLt): D[M][N] = act(A[M][K] . W[N][K]^T + bias[N] (+ R[M][N])),
+ * row-major fp32, act = ReLU when relu != 0.  With bias = the folded frozen-BN
+ * shift and R = the block input, this is the whole tail of the reference's
+ * bottleneck_transformation (lib/modeling/ResNet.py:246-294: conv3 ->
+ * AffineChannel2d -> + residual -> ReLU) in one kernel.  residual may be NULL.
+ * workspace: >= vd_gemm_workspace_size() bytes, stream-ordered.  Not a
+ * replacement for a reference custom op (those convs run in PyTorch there);
+ * it removes the separate epilogue pass over the conv output. */
+size_t vd_gemm_workspace_size(void);
+int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,
+                     const float *residual, int relu, float *D, void *workspace,
+                     size_t workspace_bytes, void *stream);
+
 /* ---------------------------------------------------------------------------
  * NMS with the semantics of the NMS the reference executes,
  * utils.boxes.nms -> cython_nms.nms (lib/utils/boxes.py:329-333,
  * lib/utils/cython_nms.pyx:37-87): dets n x det_stride fp32 [x1,y1,x2,y2,score,..],
  * processing order score-descending (ties: higher index first), suppression
  * when IoU (+1 convention) >= thresh, kept indices written ascending to
- * keep_out (int64), their count to *num_out (device int32).  Also replaces the
- * unused GPU path nms_cuda(THCudaIntTensor *keep_out, THCudaTensor *boxes,
- * THCudaIntTensor *num_out, float thresh)  lib/model/nms/src/nms_cuda.c:8-19.
- * n <= 8192. */
+ * keep_out (int64), their count to *num_out (device int32).  n <= 8192.
+ * Stands in for the reference's unused GPU path nms_cuda(THCudaIntTensor
+ * *keep_out, THCudaTensor *boxes, THCudaIntTensor *num_out, float thresh)
+ * (lib/model/nms/src/nms_cuda.c:8-19) WITH THE CYTHON SEMANTICS above: it is
+ * not a drop-in for nms_cuda's own rule, which suppresses on IoU > thresh
+ * (strict) over pre-sorted input (lib/model/nms/src/nms_cuda_kernel.cu:78). */
 size_t vd_nms_workspace_size(int n);
 int vd_nms(const float *dets, int n, int det_stride, float thresh, int64_t *keep_out,
            int32_t *num_out, void *workspace, size_t workspace_bytes, void *stream);

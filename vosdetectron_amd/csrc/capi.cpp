@@ -90,6 +90,16 @@ int vd_roi_align_fpn_forward(const VdFeatLevel *levels, int num_levels, int B, i
                                      fa.scale[0], sampling_ratio, output, VD_STREAM(stream));
 }
 
+size_t vd_gemm_workspace_size(void) { return gemm_epi_workspace_bytes(); }
+
+int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,
+                     const float *residual, int relu, float *D, void *workspace,
+                     size_t workspace_bytes, void *stream) {
+    if (M < 0 || K < 1 || N < 1 || !W || !bias || !D || (M > 0 && !A)) return VD_ERR_ARG;
+    return launch_gemm_bias_act(A, M, K, W, N, bias, residual, relu, D, workspace,
+                                workspace_bytes, VD_STREAM(stream));
+}
+
 int vd_roi_align_legacy_forward(int ah, int aw, float spatial_scale, const float *features,
                                 int B, int C, int H, int W, const float *rois, int num_rois,
                                 float *output, void *stream) {

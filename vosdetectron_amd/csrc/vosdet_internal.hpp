@@ -29,6 +29,11 @@ int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, con
                               const int *order, int R, int PH, int PW, int sr, int out_nhwc,
                               float *out, hipStream_t s);
 
+size_t gemm_epi_workspace_bytes();
+int launch_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,
+                         const float *R, int relu, float *D, void *ws, size_t ws_bytes,
+                         hipStream_t s);
+
 int launch_roi_align_legacy_fwd(const float *feat, int B, int C, int H, int W, const float *rois,
                                 int R, int PH, int PW, float scale, float *out, hipStream_t s);
 int launch_roi_pool_fwd(const float *feat, int B, int C, int H, int W, const float *rois, int R,

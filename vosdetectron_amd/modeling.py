@@ -81,6 +81,8 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         if self.fused and self.epilogue and x.is_cuda:
+            if _gemm_ok(x):
+                return self._forward_gemm(x)
             out = _conv_epi(self.f1, x)
             out = _conv_epi(self.f2, out)
             if self.downsample is not None:
@@ -97,6 +99,47 @@ class Bottleneck(nn.Module):
         out = self.bn3(self.conv3(out))
         res = self.downsample(x) if self.downsample is not None else x
         return F.relu(out + res, inplace=True)
+
+
+    def _forward_gemm(self, x):
+        """channels_last: the stride-1 1x1 convs run as hipBLASLt GEMMs with their
+        epilogue fused -- conv1: relu(x W1^T + b1); conv3: relu(h W3^T + b3 + r)
+        with the residual r (identity, or the downsample conv whose bias is
+        folded into b3) read by the GEMM itself (ops.gemm_bias_act)."""
+        if self.f1.stride == (1, 1):
+            out = _gemm_conv1x1(x, self.w1, self.f1.bias, relu=True)
+        else:
+            out = _conv_epi(self.f1, x)
+        out = _conv_epi(self.f2, out)
+        if self.downsample is not None:
+            return _gemm_conv1x1(out, self.w3, self.b3d, relu=True, res=_conv_nb(self.fd, x))
+        return _gemm_conv1x1(out, self.w3, self.f3.bias, relu=True, res=x)
+
+
+def _gemm_ok(x) -> bool:
+    """GEMM epilogue path: channels_last fp32 activations (VOSDET_GEMM_EPILOGUE=0
+    switches it off for A/B measurements)."""
+    import os
+    return (os.environ.get("VOSDET_GEMM_EPILOGUE", "1") != "0" and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous()
+            and x.dtype == torch.float32)
+
+
+def _nhwc2d(x):
+    N, C, H, W = x.shape
+    return x.permute(0, 2, 3, 1).reshape(N * H * W, C)
+
+
+def _gemm_conv1x1(x, w2d, bias, relu=True, res=None):
+    """Stride-1 1x1 conv of a channels_last NCHW tensor as act(X W^T + b [+ res])."""
+    N, C, H, W = x.shape
+    r = None
+    if res is not None:
+        if not res.is_contiguous(memory_format=torch.channels_last):
+            res = res.contiguous(memory_format=torch.channels_last)
+        r = _nhwc2d(res)
+    y = ops.gemm_bias_act(_nhwc2d(x), w2d, bias, residual=r, relu=relu)
+    return y.view(N, H, W, w2d.shape[0]).permute(0, 3, 1, 2)
 
 
 def group_gn(dim: int, cfg) -> int:
@@ -291,6 +334,9 @@ class FPNBody(nn.Module):
         c = self.conv_body.forward_stages(x)  # res1..res5
         if self.use_gn:
             inner = [self._gn_seq(self.conv_top, c[-1])]
+        elif self.epilogue and c[-1].is_cuda and _gemm_ok(c[-1]):
+            w = self.conv_top.weight.reshape(self.conv_top.out_channels, -1)
+            inner = [_gemm_conv1x1(c[-1], w, self.conv_top.bias, relu=False)]
         else:
             inner = [self.conv_top(c[-1])]
         for i in range(3):
@@ -671,6 +717,10 @@ def prepare_bottlenecks(blocks, epilogue: bool = True):
             blk.f3 = _fold(blk.conv3, blk.bn3)
             if blk.downsample is not None:
                 blk.fd = _fold(blk.downsample[0], blk.downsample[1])
+                blk.b3d = (blk.f3.bias + blk.fd.bias).contiguous()
+            # 2-D weights of the 1x1 convs for the GEMM epilogue path
+            blk.w1 = blk.f1.weight.reshape(blk.f1.out_channels, -1).contiguous()
+            blk.w3 = blk.f3.weight.reshape(blk.f3.out_channels, -1).contiguous()
             blk.fused = True
         blk.epilogue = epilogue
 

@@ -380,6 +380,42 @@ def bias_act_(x: torch.Tensor, bias: Optional[torch.Tensor], residual=None, resi
     return x
 
 
+_GEMM_WS = {}
+
+
+def gemm_bias_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
+                  residual: Optional[torch.Tensor] = None, relu: bool = True,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """act(a @ w.T + bias (+ residual)) in one hipBLASLt GEMM (vd_gemm_bias_act):
+    a [M,K], w [N,K], bias [N], residual / out [M,N], all fp32 contiguous."""
+    a_ = _need(a, "a")
+    w_ = _need(w, "w")
+    b_ = _need(bias, "bias")
+    M, K = a_.shape
+    N = w_.shape[0]
+    if w_.shape[1] != K or b_.numel() != N:
+        raise ValueError("gemm_bias_act: a %s, w %s, bias %s" % (tuple(a_.shape), tuple(w_.shape),
+                                                                 tuple(b_.shape)))
+    r_ = None
+    if residual is not None:
+        r_ = _need(residual, "residual")
+        if tuple(r_.shape) != (M, N):
+            raise ValueError("residual must be %s, got %s" % ((M, N), tuple(r_.shape)))
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a_.device)
+    elif tuple(out.shape) != (M, N) or not out.is_contiguous():
+        raise ValueError("out must be a contiguous %s tensor" % ((M, N),))
+    ws = _GEMM_WS.get(a_.device)
+    if ws is None:  # one stream-ordered workspace per device (single launch stream)
+        ws = _ws(lib().vd_gemm_workspace_size(), a_.device)
+        _GEMM_WS[a_.device] = ws
+    check(lib().vd_gemm_bias_act(a_.data_ptr(), M, K, w_.data_ptr(), N, b_.data_ptr(),
+                                 r_.data_ptr() if r_ is not None else None, int(relu),
+                                 out.data_ptr(), ws.data_ptr(), ws.numel(), _stream()),
+          "vd_gemm_bias_act")
+    return out
+
+
 def pixel_lut(pixel_means=(102.9801, 115.9465, 122.7717)) -> np.ndarray:
     """float32(u - mean_c) for u in 0..255 exactly as numpy computes
     ``im.astype(float32); im -= PIXEL_MEANS`` (float64 subtraction, float32 store,
