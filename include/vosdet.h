@@ -212,13 +212,26 @@ int vd_box_detections(const float *rois, const float *cls_prob, const float *bbo
                       int32_t *det_count_out, void *workspace, size_t workspace_bytes,
                       void *stream);
 
-/* Frame preparation, lib/utils/blob.py:37-114 at identity scale: u8 BGR frames
+/* Frame preparation, lib/utils/blob.py:37-114 at identity scale (im_scale 1): u8 BGR frames
  * (F x H x W x 3) -> fp32 blob minus PIXEL_MEANS, zero-padded to Hp x Wp
  * (multiples of FPN.COARSEST_STRIDE).  lut[3*256] = float32(u - mean_c) for
  * every byte value (numpy's float64 subtraction, then the float32 store).
  * nhwc = 0 -> F x 3 x Hp x Wp, 1 -> F x Hp x Wp x 3. */
 int vd_image_to_blob(const uint8_t *frames, int F, int H, int W, const float *lut, int Hp,
                      int Wp, int nhwc, float *blob, void *stream);
+
+/* Frame preparation at any scale: prep_im_for_blob (lib/utils/blob.py:117-139,
+ * driven by get_image_blob :37-60 and tools/infer_simple.py:142-149) --
+ * float32(BGR) - PIXEL_MEANS, cv2.resize(fx = fy = im_scale, INTER_LINEAR) to
+ * Hr x Wr (= rint(H * im_scale), rint(W * im_scale), cv::resize's dsize) --
+ * then zero-padded to Hp x Wp like vd_image_to_blob.  The resize restates
+ * OpenCV's scalar float INTER_LINEAR path (scale = 1 / im_scale in double,
+ * coefficient tables, horizontal then vertical pass, see misc.hip); cv2 is not
+ * importable in the build container, so this step's parity against an executed
+ * cv2 is unpinned (it is pinned against the numpy restatement and known answers). */
+int vd_image_resize_to_blob(const uint8_t *frames, int F, int H, int W, const float *lut,
+                            double im_scale, int Hr, int Wr, int Hp, int Wp, int nhwc,
+                            float *blob, void *stream);
 
 /* Convolution epilogue, in place on x (N x C x H x W logical, physical NHWC when
  * nhwc = 1):  x = act((x + bias[c]) + r),  r = 0 (residual_mode 0), residual

@@ -418,9 +418,54 @@ def box_results_with_nms_and_limit(scores, boxes, num_classes=81, score_thresh=0
     return im_results[:, -1], im_results[:, :-1], cls_boxes
 
 
+def cv2_resize_fx(src, fx, fy=None):
+    """cv2.resize(src, None, None, fx=fx, fy=fy, interpolation=INTER_LINEAR) for an
+    H x W x C float32 image, restating OpenCV's scalar float path: dsize =
+    (round(W*fx), round(H*fy)) (saturate_cast<int>, half to even), scale = 1/fx
+    (cv::resize keeps inv_scale = fx when dsize is derived from it), coefficient
+    tables and the horizontal-then-vertical passes as cv2_resize_linear.
+    cv2 is not importable here: parity against an executed cv2 is unpinned."""
+    fy = fx if fy is None else fy
+    src = np.asarray(src, np.float32)
+    sh, sw = src.shape[:2]
+    w, h = int(round(sw * fx)), int(round(sh * fy))
+    scale_x, scale_y = 1. / fx, 1. / fy
+    if scale_x == 2.0 and scale_y == 2.0:
+        return _area2(src, h, w)
+    dx = np.arange(w)
+    fxs = ((dx + 0.5) * scale_x - 0.5).astype(np.float32)
+    sx = np.floor(fxs).astype(np.int64)
+    fxs = (fxs - sx.astype(np.float32)).astype(np.float32)
+    lo = sx < 0
+    fxs[lo], sx[lo] = 0, 0
+    hi = sx >= sw - 1
+    fxs[hi], sx[hi] = 0, sw - 1
+    a0, a1 = (np.float32(1) - fxs).astype(np.float32), fxs
+    sx1 = np.minimum(sx + 1, sw - 1)
+    ex = (slice(None),) + (None,) * (src.ndim - 2)
+    D = src[:, sx] * a0[ex] + src[:, sx1] * a1[ex]  # HResizeLinear, every source row
+    dy = np.arange(h)
+    fys = ((dy + 0.5) * scale_y - 0.5).astype(np.float32)
+    sy = np.floor(fys).astype(np.int64)
+    fys = (fys - sy.astype(np.float32)).astype(np.float32)
+    r0, r1 = np.clip(sy, 0, sh - 1), np.clip(sy + 1, 0, sh - 1)
+    b0, b1 = (np.float32(1) - fys).astype(np.float32), fys
+    ey = (slice(None),) + (None,) * (src.ndim - 1)
+    return (D[r0] * b0[ey] + D[r1] * b1[ey]).astype(np.float32)  # VResizeLinear
+
+
+def target_scale(im_size_min, im_size_max, target_size, max_size):
+    """lib/utils/blob.py:153-160 get_target_scale."""
+    scale = float(target_size) / float(im_size_min)
+    if np.round(scale * im_size_max) > max_size:
+        scale = float(max_size) / float(im_size_max)
+    return scale
+
+
 def get_image_blob(im, target_scale=800, max_size=1333, stride=32):
-    """lib/utils/blob.py:37-161 at identity scale (cv2.resize is absent here; an
-    800x1333 frame has im_scale 1.0, so the resize is the identity)."""
+    """lib/utils/blob.py:37-161: prep_im_for_blob (mean subtraction, then the
+    INTER_LINEAR resize restated by cv2_resize_fx when the scale is not 1) and
+    im_list_to_blob's zero padding to `stride` (1 = no padding, as without FPN)."""
     im = im.astype(np.float32, copy=False) - PIXEL_MEANS
     im = im.astype(np.float32)
     smin, smax = min(im.shape[:2]), max(im.shape[:2])
@@ -428,7 +473,7 @@ def get_image_blob(im, target_scale=800, max_size=1333, stride=32):
     if np.round(scale * smax) > max_size:
         scale = float(max_size) / float(smax)
     if scale != 1.0:
-        raise NotImplementedError("oracle supports identity-scale frames only")
+        im = cv2_resize_fx(im, scale)
     H = int(np.ceil(im.shape[0] / stride) * stride)
     W = int(np.ceil(im.shape[1] / stride) * stride)
     blob = np.zeros((1, H, W, 3), np.float32)
@@ -463,12 +508,40 @@ def expand_boxes(boxes, scale):
     return boxes_exp
 
 
+def _area2(src, h, w):
+    """OpenCV's resize dispatch runs INTER_AREA's fast path for INTER_LINEAR when
+    both scales are exactly 2: each output is the mean of its 2 x 2 source block,
+    summed ((a + b) + c) + d in float and times 0.25f (a partial block at an odd
+    edge: the sum of the taps inside / their count).  Restated from OpenCV's
+    resize.cpp as published; cv2 absent here, so unpinned."""
+    src = np.asarray(src, np.float32)
+    sh, sw = src.shape[:2]
+    out = np.zeros((h, w) + src.shape[2:], np.float32)
+    fh, fw = min(h, sh // 2), min(w, sw // 2)  # blocks entirely inside the image
+    a, b = src[0:2 * fh:2, 0:2 * fw:2], src[0:2 * fh:2, 1:2 * fw:2]
+    c, d = src[1:2 * fh:2, 0:2 * fw:2], src[1:2 * fh:2, 1:2 * fw:2]
+    out[:fh, :fw] = (((a + b) + c) + d) * np.float32(0.25)
+    for y in range(h):  # partial blocks at odd edges
+        for x in range(w):
+            if y < fh and x < fw:
+                continue
+            taps = [src[2 * y + dy, 2 * x + dx] for dy in (0, 1) for dx in (0, 1)
+                    if 2 * y + dy < sh and 2 * x + dx < sw]
+            acc = np.zeros(src.shape[2:], np.float32)
+            for t in taps:
+                acc = (acc + t).astype(np.float32)
+            out[y, x] = acc / np.float32(len(taps))
+    return out
+
+
 def cv2_resize_linear(src, w, h):
     """cv2.resize(src, (w, h)) for a single-channel float32 image, INTER_LINEAR."""
     src = np.asarray(src, np.float32)
     sh, sw = src.shape
     scale_x = 1. / (float(w) / sw)
     scale_y = 1. / (float(h) / sh)
+    if scale_x == 2.0 and scale_y == 2.0:
+        return _area2(src, h, w)
     dx = np.arange(w)
     fx = ((dx + 0.5) * scale_x - 0.5).astype(np.float32)
     sx = np.floor(fx).astype(np.int64)

@@ -147,7 +147,7 @@ class RefCPUPipelineC4(RefCPUPipeline):
 
     def __init__(self, sd, block_counts=(3, 4, 6), pre_nms=6000, post_nms=1000,
                  test_scale=800, **kw):
-        self.test_scale = test_scale  # TEST.SCALE (frames must be at identity scale)
+        self.test_scale = test_scale  # TEST.SCALE (get_image_blob resizes when != 1)
         kw.setdefault("box_res", 14)
         kw.setdefault("box_sr", 0)
         kw.setdefault("mask_res", 14)

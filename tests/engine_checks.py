@@ -22,8 +22,9 @@ def _nchw(mf, C):
 def stagewise(cfg, pipe, out, frame, f=0):
     """Frame f of an engine output (run with keep_intermediates=True)."""
     from vosdetectron_amd import ops
-    _, _, im_info = orc.get_image_blob(frame, target_scale=cfg.TEST.SCALE,
-                                       max_size=cfg.TEST.MAX_SIZE, stride=cfg.FPN.COARSEST_STRIDE)
+    _, im_scale, im_info = orc.get_image_blob(frame, target_scale=cfg.TEST.SCALE,
+                                              max_size=cfg.TEST.MAX_SIZE,
+                                              stride=cfg.FPN.COARSEST_STRIDE)
     tst = cfg.TEST
     rl, pl = [], []
     for i, lvl in enumerate(range(cfg.FPN.RPN_MIN_LEVEL, cfg.FPN.RPN_MAX_LEVEL + 1)):
@@ -57,7 +58,7 @@ def stagewise(cfg, pipe, out, frame, f=0):
     K = cfg.MODEL.NUM_CLASSES
     sc = out["cls_prob"].view(-1, post, K)[f, :n].cpu().numpy()
     dl = out["bbox_pred"].view(-1, post, out["bbox_pred"].shape[-1])[f, :n].cpu().numpy()
-    pred = orc.clip_tiled_boxes(orc.bbox_transform(rois[:, 1:5] / 1.0, dl,
+    pred = orc.clip_tiled_boxes(orc.bbox_transform(rois[:, 1:5] / im_scale, dl,
                                                    tuple(cfg.MODEL.BBOX_REG_WEIGHTS)), frame.shape)
     s_ref, b_ref, _ = orc.box_results_with_nms_and_limit(
         sc, pred, K, tst.SCORE_THRESH, tst.NMS, tst.DETECTIONS_PER_IM,

@@ -86,3 +86,28 @@ def test_roi_pool_and_crop_basics():
     grid = np.stack([gy, gx], -1)[None].astype(np.float32)
     crop = orc.roi_crop(f, grid)
     assert np.allclose(crop[0], f[0], atol=1e-5)
+
+
+def test_resize_known_answers():
+    """The oracle's restatement of cv2.resize INTER_LINEAR (prep_im_for_blob,
+    lib/utils/blob.py:117-139) on known answers -- cv2 is not importable here, so
+    these pin the restatement, not an executed cv2: a 2x upscale of [a, b] is
+    OpenCV's well-known [a, .75a+.25b, .25a+.75b, b] in each direction; scale 1 is
+    the identity; dsize = round(size * fx) (half to even); both scales exactly 2
+    take INTER_AREA's fast path (2 x 2 means)."""
+    src = np.array([[0., 4.]], np.float32)[:, :, None]
+    assert np.array_equal(orc.cv2_resize_fx(src, 2.0)[0, :, 0], [0, 1, 3, 4])
+    assert np.array_equal(orc.cv2_resize_fx(src.transpose(1, 0, 2), 2.0)[:, 0, 0], [0, 1, 3, 4])
+    x = np.random.default_rng(0).standard_normal((9, 11, 3)).astype(np.float32)
+    assert np.array_equal(orc.cv2_resize_fx(x, 1.0), x)
+    assert orc.cv2_resize_fx(np.zeros((353, 500, 3), np.float32), 800 / 353).shape == (800, 1133, 3)
+    assert orc.cv2_resize_fx(np.zeros((5, 7, 1), np.float32), 0.5).shape == (2, 4, 1)  # 2.5->2, 3.5->4
+    y = np.arange(8 * 6, dtype=np.float32).reshape(8, 6)
+    down = orc.cv2_resize_fx(y[:, :, None], 0.5)[:, :, 0]
+    assert np.array_equal(down, (y[0::2, 0::2] + y[0::2, 1::2] + y[1::2, 0::2] + y[1::2, 1::2]) / 4)
+    m = np.random.default_rng(1).uniform(0, 1, (30, 30)).astype(np.float32)
+    area = orc.cv2_resize_linear(m, 15, 15)
+    assert np.array_equal(area, (((m[0::2, 0::2] + m[0::2, 1::2]) + m[1::2, 0::2]) + m[1::2, 1::2])
+                          * np.float32(0.25))
+    blob, scale, info = orc.get_image_blob(np.zeros((353, 500, 3), np.uint8))
+    assert blob.shape == (1, 3, 800, 1152) and info[0, 0] == 800 and abs(scale - 800 / 353) < 1e-15

@@ -60,6 +60,8 @@ SIGNATURES = {
     "vd_box_detections": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P, _F, _F, _I, _P, _I, _P, _P,
                                _P, _P, _S, _P]),
     "vd_image_to_blob": (_I, [_P, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
+    "vd_image_resize_to_blob": (_I, [_P, _I, _I, _I, _P, ctypes.c_double, _I, _I, _I, _I, _I,
+                                     _P, _P]),
     "vd_nchw_to_nhwc": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "vd_bias_act": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "vd_detections_postfilter": (_I, [_P, _P, _P, _I, _I, _F, _I, _P]),

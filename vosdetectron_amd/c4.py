@@ -183,7 +183,7 @@ class C4FramePipeline(FramePipeline):
     def __init__(self, model, cfg, frame_hw=(800, 1333), batch=1, channels_last=False,
                  det_cap=256, device="cuda"):
         super().__init__(model, cfg, frame_hw, batch, channels_last, det_cap, device)
-        self.Hp, self.Wp = self.H, self.W  # get_max_shape pads only with FPN_ON
+        self.Hp, self.Wp = self.Hr, self.Wr  # get_max_shape pads only with FPN_ON
         F_ = batch
         self.im_info = torch.tensor([[self.Hp, self.Wp, self.im_scale]] * F_,
                                     dtype=torch.float32, device=self.device)
@@ -191,11 +191,7 @@ class C4FramePipeline(FramePipeline):
         self.scale = model.Conv_Body.spatial_scale
 
     def backbone(self, frames):
-        nhwc = self.channels_last
-        blob = ops.image_to_blob(frames, self.lut, self.Hp, self.Wp, nhwc=nhwc)
-        if nhwc:
-            blob = blob.permute(0, 3, 1, 2)
-        return self.model.Conv_Body(blob)
+        return self.model.Conv_Body(self.make_blob(frames))
 
     def _roi_feat(self, res4_nhwc, rois, res, sr, order=None):
         lvl = torch.zeros((rois.shape[0],), dtype=torch.int32, device=self.device)

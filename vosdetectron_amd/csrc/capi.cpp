@@ -213,6 +213,14 @@ int vd_image_to_blob(const uint8_t *frames, int F, int H, int W, const float *lu
     return launch_image_to_blob(frames, F, H, W, lut, Hp, Wp, nhwc, blob, VD_STREAM(stream));
 }
 
+int vd_image_resize_to_blob(const uint8_t *frames, int F, int H, int W, const float *lut,
+                            double im_scale, int Hr, int Wr, int Hp, int Wp, int nhwc,
+                            float *blob, void *stream) {
+    if (!frames || !lut || !blob) return VD_ERR_ARG;
+    return launch_resize_to_blob(frames, F, H, W, lut, im_scale, Hr, Wr, Hp, Wp, nhwc, blob,
+                                 VD_STREAM(stream));
+}
+
 int vd_bias_act(float *x, const float *bias, const float *residual, const float *residual_bias,
                 int N, int C, int H, int W, int nhwc, int residual_mode, int relu, void *stream) {
     if (!x || N < 1 || C < 1 || H < 1 || W < 1 || residual_mode < 0 || residual_mode > 2 ||

@@ -224,6 +224,123 @@ int launch_image_to_blob(const uint8_t *frames, int F, int H, int W, const float
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
+// prep_im_for_blob with a non-identity scale (lib/utils/blob.py:117-139):
+//   im = float32(BGR u8) - PIXEL_MEANS;  cv2.resize(im, None, fx=s, fy=s,
+//   INTER_LINEAR);  zero-pad to (Hp, Wp) (im_list_to_blob, :86-110).
+// The resize restates OpenCV's scalar float INTER_LINEAR path (cv::resize with
+// dsize from fx/fy keeps inv_scale = s, so scale = 1/s in double):
+//   fx = (float)((dx + 0.5) * scale - 0.5), sx = floor(fx), fx -= sx;
+//   sx < 0 -> (0, 0); sx >= W-1 -> (W-1, 0)         (coefficient tables)
+//   row value  D = S[sx] * (1 - fx) + S[sx+1] * fx   (HResizeLinear)
+//   fy likewise, rows clip(sy, 0, H-1), clip(sy+1, 0, H-1), no fy clamp,
+//   value      D0 * (1 - fy) + D1 * fy              (VResizeLinear)
+// per channel on the mean-subtracted float image (the LUT holds numpy's
+// float32(u - mean)).  -ffp-contract=off keeps every product and sum rounded
+// as the scalar path and the numpy restatement in oracle/oracle.py round them;
+// OpenCV's SIMD builds may fuse a multiply-add (parity unpinned: cv2 absent).
+__global__ __launch_bounds__(256) void resize_to_blob_kernel(
+    const uint8_t *__restrict__ frames, int H, int W, const float *__restrict__ lut,
+    double scale_x, double scale_y, int Hr, int Wr, int Hp, int Wp, int nhwc,
+    float *__restrict__ blob) {
+    __shared__ float slut[768];
+    for (int i = threadIdx.x; i < 768; i += blockDim.x) slut[i] = lut[i];
+    __syncthreads();
+    const int f = blockIdx.z, y = blockIdx.y;
+    // both scales exactly 2: OpenCV runs INTER_AREA's fast path instead (mean of
+    // each 2 x 2 block, scalar loop order; a partial block at an odd edge
+    // averages the taps inside the image)
+    const bool area2 = scale_x == 2.0 && scale_y == 2.0;
+    if (area2) {
+        for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < Wp; x += gridDim.x * blockDim.x) {
+            float v[3] = {0.f, 0.f, 0.f};
+            if (y < Hr && x < Wr) {
+                const int ys = 2 * y, xs = 2 * x;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const float *L = slut + 256 * c;
+                    float sum = 0.f;
+                    int cnt = 0;
+                    for (int dy = 0; dy < 2 && ys + dy < H; ++dy)
+                        for (int dx = 0; dx < 2 && xs + dx < W; ++dx) {
+                            sum += L[frames[(((int64_t)f * H + ys + dy) * W + xs + dx) * 3 + c]];
+                            ++cnt;
+                        }
+                    v[c] = cnt == 4 ? sum * 0.25f : sum / (float)cnt;
+                }
+            }
+            if (nhwc) {
+                float *d = blob + (((int64_t)f * Hp + y) * Wp + x) * 3;
+                d[0] = v[0];
+                d[1] = v[1];
+                d[2] = v[2];
+            } else {
+                const int64_t plane = (int64_t)Hp * Wp;
+                float *d = blob + (int64_t)f * 3 * plane + (int64_t)y * Wp + x;
+                d[0] = v[0];
+                d[plane] = v[1];
+                d[2 * plane] = v[2];
+            }
+        }
+        return;
+    }
+    int r0 = 0, r1 = 0;
+    float b0 = 0.f, b1 = 0.f;
+    if (y < Hr) {
+        float fy = (float)((y + 0.5) * scale_y - 0.5);
+        const int sy = (int)floorf(fy);
+        fy -= (float)sy;
+        r0 = min(max(sy, 0), H - 1);
+        r1 = min(max(sy + 1, 0), H - 1);
+        b0 = 1.f - fy;
+        b1 = fy;
+    }
+    const uint8_t *row0 = frames + ((int64_t)f * H + r0) * W * 3;
+    const uint8_t *row1 = frames + ((int64_t)f * H + r1) * W * 3;
+    for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < Wp; x += gridDim.x * blockDim.x) {
+        float v[3] = {0.f, 0.f, 0.f};
+        if (y < Hr && x < Wr) {
+            float fx = (float)((x + 0.5) * scale_x - 0.5);
+            int sx = (int)floorf(fx);
+            fx -= (float)sx;
+            if (sx < 0) { fx = 0.f; sx = 0; }
+            if (sx >= W - 1) { fx = 0.f; sx = W - 1; }
+            const int sx1 = min(sx + 1, W - 1);
+            const float a0 = 1.f - fx, a1 = fx;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float *L = slut + 256 * c;
+                const float d0 = L[row0[sx * 3 + c]] * a0 + L[row0[sx1 * 3 + c]] * a1;
+                const float d1 = L[row1[sx * 3 + c]] * a0 + L[row1[sx1 * 3 + c]] * a1;
+                v[c] = d0 * b0 + d1 * b1;
+            }
+        }
+        if (nhwc) {
+            float *d = blob + (((int64_t)f * Hp + y) * Wp + x) * 3;
+            d[0] = v[0];
+            d[1] = v[1];
+            d[2] = v[2];
+        } else {
+            const int64_t plane = (int64_t)Hp * Wp;
+            float *d = blob + (int64_t)f * 3 * plane + (int64_t)y * Wp + x;
+            d[0] = v[0];
+            d[plane] = v[1];
+            d[2 * plane] = v[2];
+        }
+    }
+}
+
+int launch_resize_to_blob(const uint8_t *frames, int F, int H, int W, const float *lut,
+                          double im_scale, int Hr, int Wr, int Hp, int Wp, int nhwc, float *blob,
+                          hipStream_t s) {
+    if (F < 1 || H < 1 || W < 1 || !(im_scale > 0.0) || Hr < 1 || Wr < 1 || Hp < Hr || Wp < Wr)
+        return VD_ERR_ARG;
+    const double scale = 1.0 / im_scale;  // cv::resize: scale_x = 1 / inv_scale_x
+    dim3 grid((Wp + 255) / 256, Hp, F);
+    hipLaunchKernelGGL(resize_to_blob_kernel, grid, dim3(256), 0, s, frames, H, W, lut, scale,
+                       scale, Hr, Wr, Hp, Wp, nhwc, blob);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
 // B x C x HW -> B x HW x C through a 64x64 LDS tile (+1 pad against bank conflicts).
 __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float *__restrict__ in, int C,
                                                            int HW, float *__restrict__ out) {

@@ -57,6 +57,11 @@ __global__ __launch_bounds__(256) void paste_masks_kernel(
     const int x_0 = max(bx0, 0), x_1 = min(bx2 + 1, im_w);
     const int y_0 = max(by0, 0), y_1 = min(by2 + 1, im_h);
     const double scale_x = 1. / ((double)w / (double)S), scale_y = 1. / ((double)h / (double)S);
+    // OpenCV's resize dispatch turns INTER_LINEAR into INTER_AREA's fast path
+    // when both scales are exactly 2 (a 15 x 15 box for R = 28): the mean of
+    // each 2 x 2 block, ((a + b) + c) + d) * 0.25f in its scalar loop order
+    // (restated from OpenCV's resize.cpp as remembered; cv2 absent: unpinned)
+    const bool area2 = scale_x == 2.0 && scale_y == 2.0;
 
     const int ybeg = blockIdx.y * rows_per_band;
     const int yend = min(ybeg + rows_per_band, im_h);
@@ -77,7 +82,12 @@ __global__ __launch_bounds__(256) void paste_masks_kernel(
         }
         for (int x = threadIdx.x; x < im_w; x += blockDim.x) {
             uint8_t v = 0;
-            if (yin && x >= x_0 && x < x_1) {
+            if (yin && x >= x_0 && x < x_1 && area2) {
+                const int dx = x - bx0, dy = y - by0;
+                const float *p0 = pm + (2 * dy) * S + 2 * dx, *p1 = p0 + S;
+                const float val = (((p0[0] + p0[1]) + p1[0]) + p1[1]) * 0.25f;
+                v = val > thresh ? 1 : 0;
+            } else if (yin && x >= x_0 && x < x_1) {
                 const int dx = x - bx0;
                 float fx = (float)((dx + 0.5) * scale_x - 0.5);
                 int sx = (int)floorf(fx);

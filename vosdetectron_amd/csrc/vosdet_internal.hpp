@@ -74,6 +74,9 @@ size_t box_detections_workspace_bytes(int R_cap, int num_images, int num_classes
 
 int launch_image_to_blob(const uint8_t *frames, int F, int H, int W, const float *lut,
                          int Hp, int Wp, int nhwc, float *blob, hipStream_t s);
+int launch_resize_to_blob(const uint8_t *frames, int F, int H, int W, const float *lut,
+                          double im_scale, int Hr, int Wr, int Hp, int Wp, int nhwc, float *blob,
+                          hipStream_t s);
 int launch_bias_act(float *x, const float *bias, const float *z, const float *bias2, int64_t n,
                     int C, int H, int W, int nhwc, int mode, int relu, hipStream_t s);
 int launch_nchw_to_nhwc(const float *in, int B, int C, int H, int W, float *out, hipStream_t s);

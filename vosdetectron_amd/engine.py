@@ -54,19 +54,15 @@ class FramePipeline:
         self.device = torch.device(device)
         self.channels_last = channels_last
         self.det_cap = det_cap
-        # blob geometry (lib/utils/blob.py:37-161); identity scale only
-        smin, smax = min(frame_hw), max(frame_hw)
-        scale = float(cfg.TEST.SCALE) / float(smin)
-        if np.round(scale * smax) > cfg.TEST.MAX_SIZE:
-            scale = float(cfg.TEST.MAX_SIZE) / float(smax)
-        if scale != 1.0:
-            raise NotImplementedError(
-                "frames must be at the configured test scale (cv2.resize is outside the "
-                "hot path); got im_scale %.4f" % scale)
+        # blob geometry (lib/utils/blob.py:37-161): get_target_scale, cv2.resize
+        # to round(H*s) x round(W*s) (done on the device when s != 1), pad to
+        # FPN.COARSEST_STRIDE (get_max_shape; the C4 pipeline does not pad)
+        scale = ops.target_scale(self.H, self.W, cfg.TEST.SCALE, cfg.TEST.MAX_SIZE)
         self.im_scale = scale
+        self.Hr, self.Wr = ops.resized_hw(self.H, self.W, scale)
         st = cfg.FPN.COARSEST_STRIDE
-        self.Hp = int(math.ceil(self.H / st) * st)
-        self.Wp = int(math.ceil(self.W / st) * st)
+        self.Hp = int(math.ceil(self.Hr / st) * st)
+        self.Wp = int(math.ceil(self.Wr / st) * st)
         self.lut = torch.from_numpy(ops.pixel_lut(cfg.PIXEL_MEANS)).to(self.device)
         F = batch
         self.im_info = torch.tensor([[self.Hp, self.Wp, scale]] * F, dtype=torch.float32,
@@ -112,12 +108,19 @@ class FramePipeline:
         """{stage: average seconds per call} (Timer.average_time of the reference)."""
         return {k: v.average_time for k, v in (self.timers or {}).items()}
 
-    def backbone(self, frames):
+    def make_blob(self, frames):
+        """get_image_blob on the device: identity scale -> vd_image_to_blob, else
+        vd_image_resize_to_blob (mean subtraction + INTER_LINEAR resize + pad)."""
         nhwc = self.channels_last
-        blob = ops.image_to_blob(frames, self.lut, self.Hp, self.Wp, nhwc=nhwc)
-        if nhwc:
-            blob = blob.permute(0, 3, 1, 2)  # NCHW view, channels_last memory
-        return self.model.Conv_Body(blob)  # [P6, P5, P4, P3, P2]
+        if self.im_scale == 1.0:
+            blob = ops.image_to_blob(frames, self.lut, self.Hp, self.Wp, nhwc=nhwc)
+        else:
+            blob = ops.image_resize_to_blob(frames, self.lut, self.im_scale, self.Hp, self.Wp,
+                                            nhwc=nhwc)
+        return blob.permute(0, 3, 1, 2) if nhwc else blob  # NCHW view
+
+    def backbone(self, frames):
+        return self.model.Conv_Body(self.make_blob(frames))  # [P6, P5, P4, P3, P2]
 
     def nhwc_pyramid(self, feats):
         """P2..P5 as B x H x W x C (a free view when the body ran channels_last)."""

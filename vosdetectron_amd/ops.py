@@ -437,6 +437,39 @@ def image_to_blob(frames: torch.Tensor, lut: torch.Tensor, Hp: int, Wp: int, nhw
     return out
 
 
+def target_scale(im_h: int, im_w: int, target_size: float, max_size: float) -> float:
+    """lib/utils/blob.py:153-160 get_target_scale (Python floats = doubles)."""
+    smin, smax = min(im_h, im_w), max(im_h, im_w)
+    s = float(target_size) / float(smin)
+    if np.round(s * smax) > max_size:
+        s = float(max_size) / float(smax)
+    return s
+
+
+def resized_hw(im_h: int, im_w: int, im_scale: float):
+    """cv::resize's dsize for fx = fy = im_scale: saturate_cast<int> rounds half
+    to even, as Python's round does."""
+    return int(round(im_h * im_scale)), int(round(im_w * im_scale))
+
+
+def image_resize_to_blob(frames: torch.Tensor, lut: torch.Tensor, im_scale: float, Hp: int,
+                         Wp: int, nhwc: bool = False, out: Optional[torch.Tensor] = None):
+    """prep_im_for_blob + im_list_to_blob at any scale (vd_image_resize_to_blob)."""
+    fr = _need(frames, "frames", torch.uint8)
+    F, H, W, three = fr.shape
+    Hr, Wr = resized_hw(H, W, im_scale)
+    if Hp < Hr or Wp < Wr:
+        raise ValueError("blob %dx%d smaller than the resized frame %dx%d" % (Hp, Wp, Hr, Wr))
+    lt = _need(lut, "lut")
+    if out is None:
+        shape = (F, Hp, Wp, 3) if nhwc else (F, 3, Hp, Wp)
+        out = torch.empty(shape, dtype=torch.float32, device=fr.device)
+    check(lib().vd_image_resize_to_blob(fr.data_ptr(), F, H, W, lt.data_ptr(), float(im_scale),
+                                        Hr, Wr, Hp, Wp, int(nhwc), out.data_ptr(), _stream()),
+          "vd_image_resize_to_blob")
+    return out
+
+
 # --------------------------------------------------------------------------- #
 # Proposals, collect/distribute, detections                                    #
 # --------------------------------------------------------------------------- #
