@@ -284,3 +284,34 @@ def test_detections_postfilter_golden(golden):
         assert n == len(g[tag + "_dets"]), tag
         assert np.array_equal(dets[0, :n].cpu().numpy(), g[tag + "_dets"]), tag
         assert np.array_equal(dcls[0, :n].cpu().numpy(), g[tag + "_cls"]), tag
+
+
+def test_proposals_tie_fixture(golden):
+    """The reference-executed tie study (tools/tie_study.py): on tie-bearing
+    scores the HIP kernel reproduces the package's stable reading bit for bit,
+    and the reference's output rows as a set wherever the reference's unstable
+    numpy order left the set unchanged (see tests/golden/proposals_ties.json)."""
+    import json
+    import os
+    from tests.conftest import GOLDEN
+    from vosdetectron_amd import ops
+    info = json.load(open(os.path.join(GOLDEN, "proposals_ties.json")))
+    g = golden("proposals_ties")
+    for c in info["cases"]:
+        tag = c["case"]
+        if tag + "_probs" not in g.files:
+            continue
+        lvl = int(tag.split("fpn")[1])
+        an = orc.fpn_level_anchors(lvl)
+        p, d = g[tag + "_probs"], g[tag + "_deltas"]
+        rois, _, cnt = ops.generate_proposals(
+            [torch.from_numpy(p).to(DEV)], [torch.from_numpy(d).to(DEV)],
+            [torch.from_numpy(an).to(DEV)], [1. / 2 ** lvl],
+            torch.from_numpy(g["im_info"]).to(DEV), 1000, 1000, 0.7, 0)
+        k = int(cnt[0, 0].item())
+        got = rois[0, 0, :k].cpu().numpy()
+        stable, _ = orc.generate_proposals(an, 1. / 2 ** lvl, p, d, g["im_info"])
+        assert np.array_equal(got, stable), tag
+        if c["same_rows_as_a_set"]:
+            key = lambda a: a[np.lexsort(a.T[::-1])]  # noqa: E731
+            assert np.array_equal(key(got), key(g[tag + "_ref_rois"])), tag
