@@ -412,6 +412,10 @@ def main():
                     help="VOS configs: frames per synthetic sequence (hidden states reset)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo rehearsal of the N-rank launch and gather (no GPU)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal on a one-GPU box: every rank uses device 0 and the "
+                         "collectives run on gloo (RCCL refuses duplicate devices); the N-rank "
+                         "launch, timing and packed gather end to end, not a measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "0"))
@@ -430,11 +434,16 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29512")
         dist.init_process_group("gloo", rank=rank, world_size=world)
         return dry_run(args, dist.get_world_size(), rank)
+    if args.share_gpu:
+        local = 0
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.share_gpu:  # RCCL refuses two ranks on one device: gloo carries the rehearsal
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         world = dist.get_world_size()  # n_gpus from the live world
     dev = torch.device("cuda", local)
     torch.backends.cudnn.benchmark = True
@@ -586,6 +595,8 @@ def main():
                        "gather_bytes_per_rank": gatherer.bytes_per_rank if world > 1 else 0},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if args.share_gpu:
+            line["rehearsal"] = "--share-gpu: %d ranks on one device, not a measurement" % world
         if stages:
             line["stages_ms"] = stages
         line.update(extra)
