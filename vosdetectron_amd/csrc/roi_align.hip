@@ -254,8 +254,58 @@ __device__ __forceinline__ void nhwc_row_sr(const RoiGeom &g, int C, int ph, int
 
 
 
-// Separable NHWC forward (variant 8, the product kernel): see roi_geom.hpp for
-// the row-tap / column decomposition it uses.
+// One output row of the separable sweep (roi_geom.hpp): the x samples of
+// every output column left to right, V(x) computed once per distinct column
+// (cl, ch reuse), store(pw, acc) per finished bin.
+template <int SR, class Store>
+__device__ __forceinline__ void sep_row_sweep(const RoiGeom &g, const RowTaps<SR> &taps,
+                                              const float *base, int64_t rowstride, int C, int P,
+                                              Store store) {
+    const int W = g.W;
+    const float inv = 1.f / g.count;  // count = SR*SR, a power of two for SR=2: exact
+    int cl = -1, ch = -1;
+    float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+    auto column = [&](int x) -> float4 {
+        return combine_column<SR>(taps, load_column<SR>(taps, base, rowstride, (int64_t)x * C));
+    };
+    for (int pw = 0; pw < P; ++pw) {
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int ix = 0; ix < SR; ++ix) {
+            float x = g.sw + pw * g.bw + (ix + .5f) * g.bw / SR;
+            if (x < -1.0f || x > (float)W) continue;  // wave-uniform
+            if (x <= 0) x = 0;
+            int xl = (int)x, xh;
+            if (xl >= W - 1) { xh = xl = W - 1; x = (float)xl; } else xh = xl + 1;
+            const float lx = x - xl, hx = 1.f - lx;
+            if (xl != cl || xh != ch) {
+                if (xl == ch) va = vb;
+                else va = column(xl);
+                vb = (xh == xl) ? va : column(xh);
+                cl = xl;
+                ch = xh;
+            }
+            acc.x += hx * va.x + lx * vb.x;
+            acc.y += hx * va.y + lx * vb.y;
+            acc.z += hx * va.z + lx * vb.z;
+            acc.w += hx * va.w + lx * vb.w;
+        }
+        store(pw, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
+    }
+}
+
+template <bool NT>
+__device__ __forceinline__ void store_bin(float *dst, float4 acc) {
+    if (NT) {
+        vf4 v = {acc.x, acc.y, acc.z, acc.w};
+        __builtin_nontemporal_store(v, reinterpret_cast<vf4 *>(dst));
+    } else {
+        *reinterpret_cast<float4 *>(dst) = acc;
+    }
+}
+
+// Separable NHWC forward (variant 8): see roi_geom.hpp for the row-tap /
+// column decomposition it uses.
 // NT: output rows are written once and never re-read by this launch; storing
 // them non-temporal keeps them from evicting pyramid lines that overlapping
 // RoIs on the same XCD are about to re-read from L2.
@@ -271,9 +321,7 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
     const RoiGeom g = roi_geom(fa, C, rois + (int64_t)r * 5, li, P, P, SR);
     const int chunks = (C + 255) / 256;
     const int lane = lane_id();
-    const int W = g.W;
-    const int64_t rowstride = (int64_t)W * C;
-    const float inv = 1.f / g.count;  // count = SR*SR, a power of two for SR=2: exact
+    const int64_t rowstride = (int64_t)g.W * C;
     for (int u = wave_id(); u < P * chunks; u += num_waves()) {
         const int ph = u / chunks;
         const int ck = u - ph * chunks;
@@ -281,44 +329,11 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
         const bool active = c0 < C;
         const float *base = g.feat + (active ? c0 : 0);
         const RowTaps<SR> taps = row_taps<SR>(g, ph);
-        int cl = -1, ch = -1;
-        float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
-        auto column = [&](int x) -> float4 {
-            return combine_column<SR>(taps,
-                                      load_column<SR>(taps, base, rowstride, (int64_t)x * C));
-        };
-        for (int pw = 0; pw < P; ++pw) {
-            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int ix = 0; ix < SR; ++ix) {
-                float x = g.sw + pw * g.bw + (ix + .5f) * g.bw / SR;
-                if (x < -1.0f || x > (float)W) continue;  // wave-uniform
-                if (x <= 0) x = 0;
-                int xl = (int)x, xh;
-                if (xl >= W - 1) { xh = xl = W - 1; x = (float)xl; } else xh = xl + 1;
-                const float lx = x - xl, hx = 1.f - lx;
-                if (xl != cl || xh != ch) {
-                    if (xl == ch) va = vb;
-                    else va = column(xl);
-                    vb = (xh == xl) ? va : column(xh);
-                    cl = xl;
-                    ch = xh;
-                }
-                acc.x += hx * va.x + lx * vb.x;
-                acc.y += hx * va.y + lx * vb.y;
-                acc.z += hx * va.z + lx * vb.z;
-                acc.w += hx * va.w + lx * vb.w;
-            }
-            acc = make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
-            if (!active) continue;
+        float *orow = out + (((int64_t)r * P + ph) * P) * C + c0;
+        sep_row_sweep<SR>(g, taps, base, rowstride, C, P, [&](int pw, float4 acc) {
+            if (!active) return;
             if (out_nhwc) {
-                float *dst = out + (((int64_t)r * P + ph) * P + pw) * C + c0;
-                if (NT) {
-                    vf4 v = {acc.x, acc.y, acc.z, acc.w};
-                    __builtin_nontemporal_store(v, reinterpret_cast<vf4 *>(dst));
-                } else {
-                    *reinterpret_cast<float4 *>(dst) = acc;
-                }
+                store_bin<NT>(orow + (int64_t)pw * C, acc);
             } else {
                 float *t = tile + (int64_t)c0 * P * P + ph * P + pw;
                 t[0] = acc.x;
@@ -326,7 +341,7 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
                 t[2 * P * P] = acc.z;
                 t[3 * P * P] = acc.w;
             }
-        }
+        });
     }
     if (out_nhwc) return;
     __syncthreads();
@@ -337,7 +352,6 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
     float *o = out + (int64_t)r * C * P * P;
     for (int i = n4 * 4 + threadIdx.x; i < C * P * P; i += blockDim.x) o[i] = tile[i];
 }
-
 
 template <int P, int SR, int D>
 __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_kernel(
@@ -503,7 +517,8 @@ static int roialign_variant() {  // read per launch so tests can switch kernels
     // 8: separable kernel (product default, RoIAlign tolerance 1e-4 vs the
     //    reference's per-sample order); 3: bit-exact row kernel (the reference's
     //    per-sample arithmetic order).  Round-2 alternatives (XCD channel slices,
-    //    tile-binned LDS windows) are in tools/research/ with their measurements.
+    //    tile-binned LDS windows, a pipelined column ring) are in tools/research/
+    //    with their measurements (profiles/r02_roialign/README.md).
     return e ? atoi(e) : 8;
 }
 
