@@ -93,13 +93,15 @@ def xcd_order(rois, lvls, n_xcd=8):
 
 
 ROIALIGN_KERNEL = {"3": "vd::roi_align_fpn_nhwc_kernel<7,2,2> (reference order)",
-                   "8": "vd::roi_align_fpn_nhwc_sep_kernel<2,true> (separable, nt stores)"}
+                   "8": "vd::roi_align_fpn_nhwc_sep_kernel<2,true> (separable, nt stores)",
+                   "10": "vd::roi_align_fpn_nhwc_sep_buf_kernel<2,true> (separable, buffer loads, "
+                         "nt stores)"}
 
 
 # rocprofv3 --pmc passes of this exact launch (tools/prof_roialign.sh, separate
 # passes per counter group; FETCH_SIZE doubled per the MI355X guide): L2<->fabric
 # bytes per launch, committed under profiles/ and reported as "traffic".
-ROIALIGN_PMC = {"8": "separable_v8_xcd.json"}
+ROIALIGN_PMC = {"8": "separable_v8_xcd.json", "10": "separable_buf_v10_xcd.json"}
 
 
 def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=None,
@@ -123,7 +125,7 @@ def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=Non
     rois_np, lv_np = np.concatenate(rois), np.concatenate(lvls)
     rois_t = torch.from_numpy(rois_np).to(dev)
     lv_t = torch.from_numpy(lv_np).to(dev)
-    variant = os.environ.get("VOSDET_ROIALIGN_VARIANT", "8")
+    variant = os.environ.get("VOSDET_ROIALIGN_VARIANT", "10")
     if deal is None:
         deal = 8
     order = ops.xcd_roi_order(rois_t, lv_t, n_xcd=deal, window=window) if use_order else None

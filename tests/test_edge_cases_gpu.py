@@ -182,7 +182,7 @@ def test_roi_align_fpn_malformed_indices_pool_to_zero():
                          [1, 10, 8, 70, 60], [0, 4, 4, 60, 50]], dtype=torch.float32,
                         device=DEV)
     lvl = torch.tensor([0, 0, 1, 1, 7], dtype=torch.int32, device=DEV)
-    for variant in ("8", "3"):
+    for variant in ("10", "8", "3"):
         import os
         os.environ["VOSDET_ROIALIGN_VARIANT"] = variant
         try:

@@ -219,6 +219,16 @@ def test_roi_align_fpn_schedules_and_edges(P):
         got = ops.roi_align_fpn(pyr, scales, rt, lt, P, 2, roi_order=order,
                                 out_layout="nhwc").cpu().numpy()
         assert np.array_equal(got, ref)
+    # variant 8 (global loads) and candidate kernels (VOSDET_TEST_RA_VARIANTS="..."):
+    # bit-identical to the product kernel (variant 10, buffer loads)
+    import os
+    for variant in ["8"] + os.environ.get("VOSDET_TEST_RA_VARIANTS", "").split():
+        os.environ["VOSDET_ROIALIGN_VARIANT"] = variant
+        try:
+            got = ops.roi_align_fpn(pyr, scales, rt, lt, P, 2, out_layout="nhwc").cpu().numpy()
+        finally:
+            del os.environ["VOSDET_ROIALIGN_VARIANT"]
+        assert np.array_equal(got, ref), variant
     sel = rois[:, 0] == 0
     r1 = rois[sel].copy()
     d = orc.distribute(r1)

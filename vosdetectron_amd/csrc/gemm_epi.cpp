@@ -14,9 +14,16 @@
 // hipBLASLt is column-major: the row-major problem is issued as
 //   D'(N x M) = op_T(W stored K x N) . A'(K x M) + beta C'(N x M) + bias(N)
 // where X' is the column-major view of row-major X (no data movement).
-// Algorithms come from hipblasLtMatmulAlgoGetHeuristic, cached per shape.
+// Algorithms: hipblasLtMatmulAlgoGetHeuristic's top kMaxAlgos candidates per
+// shape; the first launch of a shape on an uncaptured stream times each of
+// them (HIP events, kSearchReps launches into the caller's own D) and keeps
+// the fastest (VOSDET_GEMM_SEARCH=0: the heuristic's first choice).  The
+// memory-bound bottleneck shapes (K = 64..256 with the residual) are where the
+// first choice is worst (tools/conv_roofline.py, profiles/r02_conv_roofline*).
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
+
+#include <stdlib.h>
 
 #include <map>
 #include <mutex>
@@ -28,12 +35,16 @@ namespace vd {
 
 namespace {
 
+constexpr int kMaxAlgos = 16, kSearchReps = 3;
+
 struct Plan {
     hipblasLtMatmulDesc_t op = nullptr;
     hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr;
+    hipblasLtMatmulHeuristicResult_t cand[kMaxAlgos];
+    int ncand = 0;
     hipblasLtMatmulAlgo_t algo;
     size_t ws = 0;
-    bool ok = false;
+    bool ok = false, searched = false;
 };
 
 std::mutex g_mu;
@@ -73,16 +84,67 @@ Plan *plan_for(int M, int N, int K, int relu, int has_res) {
     uint64_t wsmax = kMaxWs;
     hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsmax,
                                           sizeof(wsmax));
-    hipblasLtMatmulHeuristicResult_t res[1];
     int n = 0;
     const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(h, p.op, p.a, p.b, p.c, p.c, pref,
-                                                               1, res, &n);
+                                                               kMaxAlgos, p.cand, &n);
     hipblasLtMatmulPreferenceDestroy(pref);
     if (st != HIPBLAS_STATUS_SUCCESS || n < 1) return nullptr;
-    p.algo = res[0].algo;
-    p.ws = res[0].workspaceSize;
+    p.ncand = n;
+    p.algo = p.cand[0].algo;
+    p.ws = p.cand[0].workspaceSize;
     p.ok = true;
     return &p;
+}
+
+bool search_enabled() {
+    const char *e = getenv("VOSDET_GEMM_SEARCH");
+    return !(e && e[0] == '0');
+}
+
+// Time every candidate on the caller's operands (D is overwritten by the real
+// launch that follows) and keep the fastest; any failure keeps the heuristic's
+// first choice.
+void search(Plan &p, const float *A, const float *W, const float *bias, const float *R, float *D,
+            void *ws, size_t ws_bytes, hipStream_t s) {
+    p.searched = true;
+    if (p.ncand < 2 || !search_enabled()) return;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return;
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess) return;
+    if (hipEventCreate(&e1) != hipSuccess) {
+        (void)hipEventDestroy(e0);
+        return;
+    }
+    const float alpha = 1.f, beta = R ? 1.f : 0.f;
+    float best = 1e30f;
+    int best_i = -1;
+    for (int i = 0; i < p.ncand; ++i) {
+        const hipblasLtMatmulHeuristicResult_t &c = p.cand[i];
+        if (c.state != HIPBLAS_STATUS_SUCCESS || c.workspaceSize > ws_bytes ||
+            (c.workspaceSize && !ws))
+            continue;
+        auto launch = [&]() {
+            return hipblasLtMatmul(handle(), p.op, &alpha, W, p.a, A, p.b, &beta, R ? R : D, p.c,
+                                   D, p.c, &c.algo, ws, c.workspaceSize, s);
+        };
+        if (launch() != HIPBLAS_STATUS_SUCCESS) continue;  // warm-up / validity
+        bool ok = hipEventRecord(e0, s) == hipSuccess;
+        for (int r = 0; ok && r < kSearchReps; ++r) ok = launch() == HIPBLAS_STATUS_SUCCESS;
+        ok = ok && hipEventRecord(e1, s) == hipSuccess && hipEventSynchronize(e1) == hipSuccess;
+        float ms = 0.f;
+        if (ok && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms < best) {
+            best = ms;
+            best_i = i;
+        }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipGetLastError();
+    if (best_i >= 0) {
+        p.algo = p.cand[best_i].algo;
+        p.ws = p.cand[best_i].workspaceSize;
+    }
 }
 
 }  // namespace
@@ -96,9 +158,10 @@ int launch_gemm_bias_act(const float *A, int M, int K, const float *W, int N, co
     std::lock_guard<std::mutex> lk(g_mu);
     Plan *p = plan_for(M, N, K, relu ? 1 : 0, R ? 1 : 0);
     if (!p) return VD_ERR_SHAPE;
-    if (p->ws > ws_bytes || (p->ws && !ws)) return VD_ERR_WORKSPACE;
     hipblasLtMatmulDescSetAttribute(p->op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias,
                                     sizeof(bias));
+    if (!p->searched) search(*p, A, W, bias, R, D, ws, ws_bytes, s);
+    if (p->ws > ws_bytes || (p->ws && !ws)) return VD_ERR_WORKSPACE;
     const float alpha = 1.f, beta = R ? 1.f : 0.f;
     const hipblasStatus_t st =
         hipblasLtMatmul(handle(), p->op, &alpha, W, p->a, A, p->b, &beta, R ? R : D, p->c, D,

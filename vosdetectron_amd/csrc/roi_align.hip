@@ -9,10 +9,11 @@
 //    decomposition, kept as the compatibility path.
 //  * NHWC multi-level FPN (the product path): one launch for every RoI of every
 //    FPN level on the NHWC pyramid (one 1 KiB coalesced wave load per pixel,
-//    lane = 4 channels).  The default kernel (roi_align_fpn_nhwc_sep_kernel,
-//    variant 8) factors the bilinear sampling into a row pass and a column pass
-//    so each pixel is fetched ~once per output row; it re-associates the sums,
-//    so it holds the reference to 1e-4 (north_star's RoIAlign tolerance).  The
+//    lane = 4 channels).  The default kernel (roi_align_fpn_nhwc_sep_buf_kernel,
+//    variant 10; variant 8 is the same sweep through global loads) factors the
+//    bilinear sampling into a row pass and a column pass so each pixel is
+//    fetched ~once per output row; it re-associates the sums, so it holds the
+//    reference to 1e-4 (north_star's RoIAlign tolerance).  The
 //    row kernel (variant 3, VOSDET_ROIALIGN_VARIANT=3) keeps the reference's
 //    per-sample order -- sample positions, weights, w1*v1+w2*v2+w3*v3+w4*v4,
 //    iy-major accumulation, final /count, no FMA contraction -- and is
@@ -255,19 +256,15 @@ __device__ __forceinline__ void nhwc_row_sr(const RoiGeom &g, int C, int ph, int
 
 
 // One output row of the separable sweep (roi_geom.hpp): the x samples of
-// every output column left to right, V(x) computed once per distinct column
-// (cl, ch reuse), store(pw, acc) per finished bin.
-template <int SR, class Store>
-__device__ __forceinline__ void sep_row_sweep(const RoiGeom &g, const RowTaps<SR> &taps,
-                                              const float *base, int64_t rowstride, int C, int P,
+// every output column left to right, V(x) = column(x) computed once per
+// distinct column (cl, ch reuse), store(pw, acc) per finished bin.
+template <int SR, class Column, class Store>
+__device__ __forceinline__ void sep_row_sweep(const RoiGeom &g, int P, Column column,
                                               Store store) {
     const int W = g.W;
     const float inv = 1.f / g.count;  // count = SR*SR, a power of two for SR=2: exact
     int cl = -1, ch = -1;
     float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
-    auto column = [&](int x) -> float4 {
-        return combine_column<SR>(taps, load_column<SR>(taps, base, rowstride, (int64_t)x * C));
-    };
     for (int pw = 0; pw < P; ++pw) {
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -330,7 +327,11 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
         const float *base = g.feat + (active ? c0 : 0);
         const RowTaps<SR> taps = row_taps<SR>(g, ph);
         float *orow = out + (((int64_t)r * P + ph) * P) * C + c0;
-        sep_row_sweep<SR>(g, taps, base, rowstride, C, P, [&](int pw, float4 acc) {
+        auto column = [&](int x) -> float4 {
+            return combine_column<SR>(taps,
+                                      load_column<SR>(taps, base, rowstride, (int64_t)x * C));
+        };
+        sep_row_sweep<SR>(g, P, column, [&](int pw, float4 acc) {
             if (!active) return;
             if (out_nhwc) {
                 store_bin<NT>(orow + (int64_t)pw * C, acc);
@@ -351,6 +352,55 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
     for (int i = threadIdx.x; i < n4; i += blockDim.x) o4[i] = t4[i];
     float *o = out + (int64_t)r * C * P * P;
     for (int i = n4 * 4 + threadIdx.x; i < C * P * P; i += blockDim.x) o[i] = tile[i];
+}
+
+// Separable NHWC forward, buffer-load form (variant 10): variant 8's sweep
+// bin for bin (bit-identical), with the tap loads issued as
+// buffer_load_dwordx4 against a per-RoI buffer resource (the RoI's image in
+// its level): every address term but the lane's 16-byte channel offset is
+// wave-uniform, so it travels in the scalar offset -- no per-lane 64-bit
+// address arithmetic or pointer registers -- and a tap outside the image
+// reads 0 from the hardware range check instead of faulting.
+template <int SR, bool NT>
+__global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_buf_kernel(
+    FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
+    const int *__restrict__ roi_order, int P, float *__restrict__ out) {
+    const int r = roi_order ? roi_order[blockIdx.x] : (int)blockIdx.x;
+    if (r < 0 || r >= fa.R) return;  // malformed schedule entry: write nothing
+    int li = roi_level ? roi_level[r] : 0;
+    li = __builtin_amdgcn_readfirstlane(li);
+    const RoiGeom g = roi_geom(fa, C, rois + (int64_t)r * 5, li, P, P, SR);
+    const int chunks = (C + 255) / 256;
+    const int lane = lane_id();
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(g.feat), (short)0, g.H * g.W * C * 4, 0x00020000);
+    const int rowbytes = g.W * C * 4, colbytes = C * 4;
+    for (int u = wave_id(); u < P * chunks; u += num_waves()) {
+        const int ph = u / chunks;
+        const int ck = u - ph * chunks;
+        const int c0 = ck * 256 + lane * 4;
+        const bool active = c0 < C;
+        const int voff = (active ? c0 : 0) * 4;
+        const RowTaps<SR> taps = row_taps<SR>(g, ph);
+        int rowoff[2 * SR];
+#pragma unroll
+        for (int k = 0; k < 2 * SR; ++k)
+            rowoff[k] = __builtin_amdgcn_readfirstlane(taps.row[k] * rowbytes);
+        float *orow = out + (((int64_t)r * P + ph) * P) * C + c0;
+        auto column = [&](int x) -> float4 {
+            const int xo = __builtin_amdgcn_readfirstlane(x * colbytes);
+            TapCol<SR> c;
+#pragma unroll
+            for (int k = 0; k < 2 * SR; ++k)
+                if (taps.alive[k])
+                    c.f[k] = __builtin_bit_cast(
+                        float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, rowoff[k] + xo, 0));
+            return combine_column<SR>(taps, c);
+        };
+        sep_row_sweep<SR>(g, P, column, [&](int pw, float4 acc) {
+            if (active) store_bin<NT>(orow + (int64_t)pw * C, acc);
+        });
+    }
 }
 
 template <int P, int SR, int D>
@@ -514,12 +564,24 @@ static int launch_rows(const FpnLevels &fa, int C, const float *rois, const int 
 
 static int roialign_variant() {  // read per launch so tests can switch kernels
     const char *e = getenv("VOSDET_ROIALIGN_VARIANT");
-    // 8: separable kernel (product default, RoIAlign tolerance 1e-4 vs the
-    //    reference's per-sample order); 3: bit-exact row kernel (the reference's
-    //    per-sample arithmetic order).  Round-2 alternatives (XCD channel slices,
+    // 10: separable kernel with buffer loads (product default, NHWC out; RoIAlign
+    //    tolerance 1e-4 vs the reference's per-sample order); 8: the same sweep
+    //    with global loads (bit-identical to 10; also the NCHW-out path);
+    //    3: bit-exact row kernel (the reference's per-sample arithmetic order).  Round-2 alternatives (XCD channel slices,
     //    tile-binned LDS windows, a pipelined column ring) are in tools/research/
     //    with their measurements (profiles/r02_roialign/README.md).
-    return e ? atoi(e) : 8;
+    return e ? atoi(e) : 10;
+}
+
+static int launch_sep_buf(const FpnLevels &fa, int C, const float *rois, const int *lvl,
+                          const int *order, int R, int P, float *out, hipStream_t s) {
+    for (int l = 0; l < fa.L; ++l)  // 32-bit buffer offsets: every image of a level < 2 GiB
+        if ((int64_t)fa.H[l] * fa.W[l] * C * 4 >= (1ll << 31)) return VD_ERR_SHAPE;
+    int waves = P * ((C + 255) / 256);
+    if (waves > 8) waves = 8;
+    hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_buf_kernel<2, true>), dim3(R), dim3(64 * waves), 0,
+                       s, fa, C, rois, lvl, order, P, out);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
 static int launch_sep(const FpnLevels &fa, int C, const float *rois, const int *lvl,
@@ -542,6 +604,10 @@ int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, con
     if (C % 4 != 0) return VD_ERR_SHAPE;
     const int variant = roialign_variant();
     if (out_nhwc) {  // product path: [R][P][P][C] written straight from registers
+        if (variant == 10 && sr == 2 && PH == PW) {  // product
+            const int st = launch_sep_buf(fa, C, rois, lvl, order, R, PH, out, s);
+            if (st != VD_ERR_SHAPE) return st;
+        }
         if (variant >= 8 && sr == 2 && PH == PW)
             return launch_sep(fa, C, rois, lvl, order, R, PH, 1, out, s);
         if (PH == PW && PH == 7)

@@ -359,6 +359,7 @@ class FPNRPNOutputs(nn.Module):
         self.FPN_RPN_bbox_pred = nn.Conv2d(dim_in, 4 * num_anchors, 1, 1, 0)
         self.num_anchors = num_anchors
         self.fused = None
+        self.fused_w2d = None
 
     def fuse(self):
         A = self.num_anchors
@@ -369,6 +370,7 @@ class FPNRPNOutputs(nn.Module):
                                       self.FPN_RPN_bbox_pred.weight]))
             f.bias.copy_(torch.cat([self.FPN_RPN_cls_score.bias, self.FPN_RPN_bbox_pred.bias]))
         self.fused = f
+        self.fused_w2d = f.weight.detach().reshape(5 * A, -1).contiguous()
 
     def level_outputs(self, x):
         """(sigmoid cls probs N x A x H x W, bbox deltas N x 4A x H x W)."""
@@ -378,7 +380,10 @@ class FPNRPNOutputs(nn.Module):
             h = F.relu(self.FPN_RPN_conv(x), inplace=True)
         A = self.num_anchors
         if self.fused is not None:
-            o = self.fused(h)
+            if _gemm_ok(h):  # the fused cls + bbox 1x1 as one GEMM with the bias epilogue
+                o = _gemm_conv1x1(h, self.fused_w2d, self.fused.bias.detach(), relu=False)
+            else:
+                o = self.fused(h)
             return torch.sigmoid(o[:, :A]).contiguous(), o[:, A:].contiguous()
         return torch.sigmoid(self.FPN_RPN_cls_score(h)), self.FPN_RPN_bbox_pred(h)
 
