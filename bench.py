@@ -308,9 +308,10 @@ def measure_pipeline_roialign(pipe, frames_dev, reps=20):
             "algorithmic_bytes_per_launch": int(nbytes), "avg_launch_us": round(t * 1e6, 2)}
 
 
-def measure_segm(pipe, out, frames=4):
-    """segm_results (device paste + RLE + host rleToString) per frame -- outside
-    the FPS by SURVEY §8d's definition, reported beside it."""
+def measure_segm(pipe, out, frames=16):
+    """segm_results (fused device paste + RLE, device rleToString, host string
+    slicing and class grouping) per frame over one step's frames -- outside the
+    FPS by SURVEY §8d's definition, reported beside it."""
     from vosdetectron_amd.engine import frame_segms
     sub = dict(out)
     k = min(frames, len(out["counts_host"]))
@@ -560,7 +561,12 @@ def main():
         stages = {k: round(v * 1e3, 3) for k, v in pipe.timer_summary().items()}
         pipe.enable_timers(False)
         if not vos and cfg.FPN.FPN_ON:
-            extra["segm_results_ms_per_frame"] = measure_segm(pipe, out)
+            segm_ms = measure_segm(pipe, out)
+            extra["segm_results_ms_per_frame"] = segm_ms
+            # the reference's whole im_detect_all incl. segm_results (RLE strings
+            # on the host), serialised after the timed step: one GPU's rate
+            step_ms_frame = dt / args.steps * 1e3 / F
+            extra["frames_per_s_incl_segm_per_gpu"] = round(1e3 / (step_ms_frame + segm_ms), 2)
 
     roof = None
     if not args.no_roofline and rank == 0:

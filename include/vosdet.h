@@ -347,13 +347,29 @@ int vd_detections_postfilter(float *dets, int32_t *classes, int32_t *counts, int
  * column-major (Fortran) order: counts[m][0..n) with n = ncounts[m], the
  * first run counting zeros.  If a plane needs more than `cap` runs,
  * ncounts[m] = -n and its counts are not written (call again with cap >= n).
- * The run lengths -> ASCII string step (rleToString) is host formatting
- * (vosdetectron_amd/segm.py).
+ * The run lengths -> ASCII string step (rleToString) is vd_rle_strings.
  * ------------------------------------------------------------------------- */
 int vd_paste_masks(const float *masks, int M, int R, const float *boxes, int box_stride,
                    int im_h, int im_w, float thresh, uint8_t *out, void *stream);
 int vd_mask_rle(const uint8_t *masks, int M, int H, int W, uint32_t *counts, int cap,
                 int32_t *ncounts, void *stream);
+
+/* vd_segm_rle: vd_paste_masks followed by vd_mask_rle in one launch, without
+ * the M x im_h x im_w planes: each detection's pasted values are evaluated in
+ * its clipped box only (everything outside is 0) and turned into the same
+ * counts / ncounts (retry contract as vd_mask_rle).  im_w <= 8192.
+ *
+ * vd_rle_strings: pycocotools rleToString (maskApi.c) of each detection's
+ * counts[m][0..ncounts[m]).  chars == NULL: lens[m] = the string's length
+ * (0 for ncounts[m] <= 0).  chars != NULL: lens must hold those lengths
+ * (sum < 2^31); detection m's ASCII string is written at
+ * chars[lens[0] + ... + lens[m-1]], unterminated.  Replaces the host-side
+ * `rleToString` + `.decode('ascii')` of segm_results (test.py:834-842). */
+int vd_segm_rle(const float *masks, int M, int R, const float *boxes, int box_stride,
+                int im_h, int im_w, float thresh, uint32_t *counts, int cap, int32_t *ncounts,
+                void *stream);
+int vd_rle_strings(const uint32_t *counts, const int32_t *ncounts, int M, int cap,
+                   int32_t *lens, uint8_t *chars, void *stream);
 
 #ifdef __cplusplus
 }

@@ -582,15 +582,12 @@ def paste_masks(masks, boxes, im_h, im_w, thresh=0.5):
     return out
 
 
-def rle_encode(im_mask):
-    """pycocotools mask.encode of one H x W u8 mask: {'size', 'counts' (str)}
-    plus the raw run lengths (maskApi.c rleEncode over Fortran order)."""
-    flat = np.asarray(im_mask, np.uint8).flatten(order="F")
-    change = np.flatnonzero(np.diff(np.concatenate([[0], flat])) != 0)
-    bounds = np.concatenate([[0], change, [flat.size]])
-    cnts = np.diff(bounds).astype(np.int64)
+def rle_to_string(cnts):
+    """pycocotools maskApi.c rleToString: each count after the second
+    delta-coded against cnts[i-2] (signed), 5 bits per char low bits first,
+    0x20 = more, + 48; stops at 0 (or -1 with the sign bit 0x10 set)."""
     s = []
-    for i in range(len(cnts)):  # rleToString
+    for i in range(len(cnts)):
         x = int(cnts[i]) - (int(cnts[i - 2]) if i > 2 else 0)
         while True:
             c = x & 0x1f
@@ -599,4 +596,15 @@ def rle_encode(im_mask):
             s.append(chr((c | (0x20 if more else 0)) + 48))
             if not more:
                 break
-    return {"size": [int(im_mask.shape[0]), int(im_mask.shape[1])], "counts": "".join(s)}, cnts
+    return "".join(s)
+
+
+def rle_encode(im_mask):
+    """pycocotools mask.encode of one H x W u8 mask: {'size', 'counts' (str)}
+    plus the raw run lengths (maskApi.c rleEncode over Fortran order)."""
+    flat = np.asarray(im_mask, np.uint8).flatten(order="F")
+    change = np.flatnonzero(np.diff(np.concatenate([[0], flat])) != 0)
+    bounds = np.concatenate([[0], change, [flat.size]])
+    cnts = np.diff(bounds).astype(np.int64)
+    return ({"size": [int(im_mask.shape[0]), int(im_mask.shape[1])],
+             "counts": rle_to_string(cnts)}, cnts)

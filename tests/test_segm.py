@@ -26,7 +26,7 @@ def test_cv2_resize_linear_known_answers():
 
 
 def test_rle_known_answers():
-    from vosdetectron_amd.segm import rle_to_string
+    rle_to_string = orc.rle_to_string
     assert orc.rle_encode(np.zeros((2, 2), np.uint8))[0]["counts"] == "4"
     assert orc.rle_encode(np.ones((2, 2), np.uint8))[0]["counts"] == "04"
     r, c = orc.rle_encode(np.array([[0, 1, 1], [0, 1, 0]], np.uint8))  # Fortran order 0,0,1,1,1,0
@@ -35,11 +35,15 @@ def test_rle_known_answers():
     for _ in range(300):
         a = (rng.uniform(size=(rng.integers(1, 60), rng.integers(1, 60))) > rng.uniform())
         r, c = orc.rle_encode(a.astype(np.uint8))
-        assert r["counts"] == rle_to_string(c) and c.sum() == a.size
+        assert c.sum() == a.size
+        # independent column-walk restatement of rleEncode's change positions
+        f = a.astype(np.uint8).flatten(order="F")
+        pos = [i for i in range(f.size) if f[i] != (f[i - 1] if i else 0)]
+        assert list(np.diff([0] + pos + [f.size])) == list(c)
 
 
 def test_leb_encoding_values():
-    from vosdetectron_amd.segm import rle_to_string
+    rle_to_string = orc.rle_to_string
     # single counts: 0..15 -> one char '0'+x; 16 needs a continuation
     assert rle_to_string([5]) == chr(48 + 5)
     assert rle_to_string([16]) == chr(48 + (16 | 0x20)) + chr(48 + 0)
@@ -111,3 +115,63 @@ def test_engine_frame_segms():
         r, _ = orc.rle_encode(ref[i])
         assert segms[j][seen.get(j, 0)] == r, i
         seen[j] = seen.get(j, 0) + 1
+
+
+def _edge_boxes(im_h, im_w):
+    """Boxes whose pasted masks hit every branch of the fused column walk: full
+    height (a column's last pixel meets the next column's first), full height at
+    the last column (the plane's end), first column, a 15 x 15 expanded box
+    (R = 28: OpenCV's INTER_AREA 2x path), a 1-pixel box."""
+    return np.array([[0, 0, im_w - 1, im_h - 1, 1], [5.5, 0, 40.2, im_h - 1, 1],
+                     [im_w - 30.5, 0, im_w - 1, im_h - 1, 1], [0, 3.3, 9.1, 20.7, 1],
+                     [100.2, 10.2, 113.2, 23.2, 1], [7, 7, 7, 7, 1],
+                     [im_w - 12.4, im_h - 9.6, im_w - 1, im_h - 1, 1]], np.float32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,im_h,im_w", [(28, 800, 1333), (14, 480, 854), (28, 37, 53)])
+def test_segm_rle_fused_vs_oracle(R, im_h, im_w):
+    """vd_segm_rle (paste + RLE without planes) and vd_rle_strings equal the
+    oracle's segm_results loop (paste, rleEncode, rleToString) bit for bit."""
+    from vosdetectron_amd import ops, segm
+    rng = np.random.default_rng(3 * R + im_w)
+    masks, boxes = _cases(rng, 40, im_h, im_w, R)
+    eb = np.clip(_edge_boxes(im_h, im_w), 0, None)
+    eb[:, 0:4:2] = np.minimum(eb[:, 0:4:2], im_w - 1)
+    eb[:, 1:4:2] = np.minimum(eb[:, 1:4:2], im_h - 1)
+    em = rng.uniform(0, 1, (len(eb), R, R)).astype(np.float32)
+    em[0] = 0.9  # all ones in a full-frame box: counts [0, H*W]
+    em[1] = 0.9  # all ones, full height, several columns
+    em[2, :, -3:] = 0.9  # ones up to the plane's last pixel
+    masks = np.concatenate([masks, em])
+    boxes = np.concatenate([boxes, eb])
+    ref = orc.paste_masks(masks, boxes, im_h, im_w)
+    mt, bt = torch.from_numpy(masks).cuda(), torch.from_numpy(boxes).cuda()
+    for cap in (None, 3):  # default capacity, and the retry path
+        cnt, n = ops.segm_rle_counts(mt, bt, im_h, im_w, cap=cap)
+        cnt, n = cnt.cpu().numpy(), n.cpu().numpy()
+        for i in range(len(masks)):
+            _, c = orc.rle_encode(ref[i])
+            assert np.array_equal(cnt[i, :n[i]], c), i
+    rles = segm.encode_masks(mt, bt, im_h, im_w)
+    for i in range(len(masks)):
+        assert rles[i] == orc.rle_encode(ref[i])[0], i
+
+
+@pytest.mark.gpu
+def test_rle_strings_kernel():
+    """vd_rle_strings vs the oracle's rleToString on run lengths with large
+    values (multi-char), negative deltas, one count, and no counts."""
+    from vosdetectron_amd import ops
+    rng = np.random.default_rng(11)
+    rows = [rng.integers(0, 2 ** rng.integers(1, 31), rng.integers(1, 700)) for _ in range(60)]
+    rows += [np.array([1066400]), np.array([0, 1066400]), np.array([5, 1, 2 ** 31 - 1, 3, 0]),
+             np.array([], np.int64)]
+    cap = max(len(r) for r in rows)
+    counts = np.zeros((len(rows), cap), np.int32)
+    for i, r in enumerate(rows):
+        counts[i, :len(r)] = r
+    n = np.array([len(r) for r in rows], np.int32)
+    got = ops.rle_strings(torch.from_numpy(counts).cuda(), torch.from_numpy(n).cuda())
+    for i, r in enumerate(rows):
+        assert got[i] == orc.rle_to_string(r), i

@@ -388,6 +388,24 @@ int vd_mask_rle(const uint8_t *masks, int M, int H, int W, uint32_t *counts, int
     return launch_mask_rle(masks, M, H, W, counts, cap, ncounts, VD_STREAM(stream));
 }
 
+int vd_segm_rle(const float *masks, int M, int R, const float *boxes, int box_stride,
+                int im_h, int im_w, float thresh, uint32_t *counts, int cap, int32_t *ncounts,
+                void *stream) {
+    if (M == 0) return VD_OK;
+    if (!masks || !boxes || !counts || !ncounts || M < 0 || R < 1 || box_stride < 4 ||
+        im_h < 1 || im_w < 1 || cap < 1 || (int64_t)im_h * im_w > 0xffffffffll)
+        return VD_ERR_ARG;
+    return launch_segm_rle(masks, M, R, boxes, box_stride, im_h, im_w, thresh, counts, cap,
+                           ncounts, VD_STREAM(stream));
+}
+
+int vd_rle_strings(const uint32_t *counts, const int32_t *ncounts, int M, int cap,
+                   int32_t *lens, uint8_t *chars, void *stream) {
+    if (M == 0) return VD_OK;
+    if (!counts || !ncounts || !lens || M < 0 || cap < 1) return VD_ERR_ARG;
+    return launch_rle_strings(counts, ncounts, M, cap, lens, chars, VD_STREAM(stream));
+}
+
 int vd_detections_postfilter(float *dets, int32_t *classes, int32_t *counts, int num_images,
                              int det_cap, float nms_cross_class, int num_det_per_class_pre,
                              void *stream) {

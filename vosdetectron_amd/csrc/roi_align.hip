@@ -258,14 +258,16 @@ __device__ __forceinline__ void nhwc_row_sr(const RoiGeom &g, int C, int ph, int
 // One output row of the separable sweep (roi_geom.hpp): the x samples of
 // every output column left to right, V(x) = column(x) computed once per
 // distinct column (cl, ch reuse), store(pw, acc) per finished bin.
+// Bins [pw0, pw1) of the row; V(x) of a column does not depend on which
+// sweep computed it, so splitting a row into segments is bit-identical.
 template <int SR, class Column, class Store>
-__device__ __forceinline__ void sep_row_sweep(const RoiGeom &g, int P, Column column,
+__device__ __forceinline__ void sep_row_sweep(const RoiGeom &g, int pw0, int pw1, Column column,
                                               Store store) {
     const int W = g.W;
     const float inv = 1.f / g.count;  // count = SR*SR, a power of two for SR=2: exact
     int cl = -1, ch = -1;
     float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
-    for (int pw = 0; pw < P; ++pw) {
+    for (int pw = pw0; pw < pw1; ++pw) {
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int ix = 0; ix < SR; ++ix) {
@@ -331,7 +333,7 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
             return combine_column<SR>(taps,
                                       load_column<SR>(taps, base, rowstride, (int64_t)x * C));
         };
-        sep_row_sweep<SR>(g, P, column, [&](int pw, float4 acc) {
+        sep_row_sweep<SR>(g, 0, P, column, [&](int pw, float4 acc) {
             if (!active) return;
             if (out_nhwc) {
                 store_bin<NT>(orow + (int64_t)pw * C, acc);
@@ -361,11 +363,23 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
 // wave-uniform, so it travels in the scalar offset -- no per-lane 64-bit
 // address arithmetic or pointer registers -- and a tap outside the image
 // reads 0 from the hardware range check instead of faulting.
+//
+// segs > 1 splits every output row into `segs` runs of bins, one wave each:
+// a RoI then occupies P*segs waves, so fewer RoIs are resident per XCD at the
+// same occupancy and the union of their footprints stays closer to the 4 MiB
+// L2 (tools/research/ra_l2_sim.py); each run re-reads at most one boundary
+// column of its neighbour.
 template <int SR, bool NT>
-__global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_buf_kernel(
+__global__ __launch_bounds__(1024) void roi_align_fpn_nhwc_sep_buf_kernel(
     FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
-    const int *__restrict__ roi_order, int P, float *__restrict__ out) {
-    const int r = roi_order ? roi_order[blockIdx.x] : (int)blockIdx.x;
+    const int *__restrict__ roi_order, int P, int segs, int parts, float *__restrict__ out) {
+    // parts > 1: a RoI's units are spread over `parts` consecutive workgroups of
+    // the same XCD (block b runs on XCD b % 8): b -> schedule position p.
+    const int b = blockIdx.x;
+    const int p = parts == 1 ? b : (b / 8 / parts) * 8 + (b & 7);
+    const int part = parts == 1 ? 0 : (b / 8) % parts;
+    if (p >= fa.R) return;
+    const int r = roi_order ? roi_order[p] : p;
     if (r < 0 || r >= fa.R) return;  // malformed schedule entry: write nothing
     int li = roi_level ? roi_level[r] : 0;
     li = __builtin_amdgcn_readfirstlane(li);
@@ -375,9 +389,13 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_buf_kernel(
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float *>(g.feat), (short)0, g.H * g.W * C * 4, 0x00020000);
     const int rowbytes = g.W * C * 4, colbytes = C * 4;
-    for (int u = wave_id(); u < P * chunks; u += num_waves()) {
-        const int ph = u / chunks;
-        const int ck = u - ph * chunks;
+    const int units = P * chunks * segs, per = (units + parts - 1) / parts;
+    const int u1 = min(units, (part + 1) * per);
+    for (int u = part * per + wave_id(); u < u1; u += num_waves()) {
+        const int ph = u / (chunks * segs);
+        const int rem = u - ph * chunks * segs;
+        const int ck = rem / segs;
+        const int sg = rem - ck * segs;
         const int c0 = ck * 256 + lane * 4;
         const bool active = c0 < C;
         const int voff = (active ? c0 : 0) * 4;
@@ -397,7 +415,7 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_buf_kernel(
                         float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, rowoff[k] + xo, 0));
             return combine_column<SR>(taps, c);
         };
-        sep_row_sweep<SR>(g, P, column, [&](int pw, float4 acc) {
+        sep_row_sweep<SR>(g, sg * P / segs, (sg + 1) * P / segs, column, [&](int pw, float4 acc) {
             if (active) store_bin<NT>(orow + (int64_t)pw * C, acc);
         });
     }
@@ -577,10 +595,25 @@ static int launch_sep_buf(const FpnLevels &fa, int C, const float *rois, const i
                           const int *order, int R, int P, float *out, hipStream_t s) {
     for (int l = 0; l < fa.L; ++l)  // 32-bit buffer offsets: every image of a level < 2 GiB
         if ((int64_t)fa.H[l] * fa.W[l] * C * 4 >= (1ll << 31)) return VD_ERR_SHAPE;
-    int waves = P * ((C + 255) / 256);
-    if (waves > 8) waves = 8;
-    hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_buf_kernel<2, true>), dim3(R), dim3(64 * waves), 0,
-                       s, fa, C, rois, lvl, order, P, out);
+    // Row segments x workgroups per RoI (VOSDET_RA_SEGS / VOSDET_RA_PARTS, both 1
+    // in the product): bit-identical schedules that keep fewer RoIs resident per
+    // XCD.  Measured (profiles/r02_roialign/README.md): fabric reads fall from
+    // 1.12 to 0.71 GB (1.04x the algorithmic bytes) at segs = parts = 4, but the
+    // launch slows from 301 to 364 us -- the extra boundary loads cost more than
+    // the L2 hits save, the kernel being bound by its vector-memory wave loads.
+    const char *es = getenv("VOSDET_RA_SEGS");
+    int segs = es ? atoi(es) : 1;
+    if (segs < 1 || segs > P) segs = 1;
+    const char *ep = getenv("VOSDET_RA_PARTS");
+    int parts = ep ? atoi(ep) : 1;
+    if (parts < 1) parts = 1;
+    const int units = P * ((C + 255) / 256) * segs;
+    int waves = (units + parts - 1) / parts;
+    if (waves > 16) waves = 16;
+    if (segs == 1 && parts == 1 && waves > 8) waves = 8;
+    const int nblk = parts == 1 ? R : (R + 7) / 8 * 8 * parts;
+    hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_buf_kernel<2, true>), dim3(nblk), dim3(64 * waves),
+                       0, s, fa, C, rois, lvl, order, P, segs, parts, out);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 

@@ -118,6 +118,11 @@ int launch_paste_masks(const float *masks, int M, int R, const float *boxes, int
                        int im_h, int im_w, float thresh, uint8_t *out, hipStream_t s);
 int launch_mask_rle(const uint8_t *planes, int M, int H, int W, uint32_t *counts, int cap,
                     int32_t *ncounts, hipStream_t s);
+int launch_segm_rle(const float *masks, int M, int R, const float *boxes, int box_stride,
+                    int im_h, int im_w, float thresh, uint32_t *counts, int cap,
+                    int32_t *ncounts, hipStream_t s);
+int launch_rle_strings(const uint32_t *counts, const int32_t *ncounts, int M, int cap,
+                       int32_t *lens, uint8_t *chars, hipStream_t s);
 
 int launch_detections_postfilter(float *dets, int32_t *cls, int32_t *counts, int num_images,
                                  int det_cap, float nms_cross_class, int num_det_per_class_pre,

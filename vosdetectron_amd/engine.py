@@ -242,15 +242,23 @@ class FramePipeline:
 
 
 def frame_segms(pipe: FramePipeline, out: dict, num_classes: int = 81):
-    """segm_results for every frame of a pipeline output (device paste + RLE,
-    vosdetectron_amd/segm.py): list over frames of cls_segms."""
+    """segm_results for every frame of a pipeline output: one fused paste + RLE
+    launch and one rleToString pass over all frames' detections
+    (vosdetectron_amd/segm.py), then the per-frame class grouping.  Returns a
+    list over frames of cls_segms."""
     from . import segm
+    ks = [int(k) for k in out["counts_host"]]
+    total = sum(ks)
+    if total == 0:
+        return [[[] for _ in range(num_classes)] for _ in ks]
+    boxes = torch.cat([out["dets"][f, :k] for f, k in enumerate(ks)])
+    classes = torch.cat([out["classes"][f, :k] for f, k in enumerate(ks)]).cpu().tolist()
+    rles = segm.encode_masks(out["masks"][:total], boxes, pipe.H, pipe.W,
+                             pipe.cfg.MRCNN.THRESH_BINARIZE)
     res, start = [], 0
-    for f, k in enumerate(out["counts_host"]):
-        cls_segms, _ = segm.segm_results(
-            out["dets"][f, :k], out["classes"][f, :k], out["masks"][start:start + k],
-            pipe.H, pipe.W, num_classes, pipe.cfg.MRCNN.THRESH_BINARIZE)
-        res.append(cls_segms)
+    for k in ks:
+        res.append(segm.group_by_class(rles[start:start + k], classes[start:start + k],
+                                       num_classes))
         start += k
     return res
 

@@ -8,6 +8,7 @@ only -- all arithmetic happens in the HIP kernels.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Sequence
 
 import numpy as np
@@ -181,6 +182,19 @@ def roi_align_fpn(levels: Sequence[torch.Tensor], spatial_scales: Sequence[float
 _ORDER_CACHE = {}
 
 
+def _spread16(v: torch.Tensor) -> torch.Tensor:
+    """Bits 0..15 of v to the even bit positions 0..30."""
+    v = (v | (v << 8)) & 0x00FF00FF
+    v = (v | (v << 4)) & 0x0F0F0F0F
+    v = (v | (v << 2)) & 0x33333333
+    return (v | (v << 1)) & 0x55555555
+
+
+def _morton16(y: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """Z-order index of 16-bit (y, x): x on the even bits, y on the odd bits."""
+    return _spread16(x) | (_spread16(y) << 1)
+
+
 def _deal(n: int, n_xcd: int, window: Optional[int]) -> np.ndarray:
     """Block b -> position in the sorted order: inside each window of `window`
     consecutive positions (the whole order by default), XCD k (b % n_xcd == k)
@@ -201,21 +215,34 @@ def _deal(n: int, n_xcd: int, window: Optional[int]) -> np.ndarray:
 
 
 def xcd_roi_order(rois: torch.Tensor, roi_level: torch.Tensor, n_xcd: int = 8,
-                  band: int = 8, window: Optional[int] = None) -> torch.Tensor:
+                  band: int = 8, window: Optional[int] = None,
+                  curve: Optional[str] = None) -> torch.Tensor:
     """Scheduling permutation for roi_align_fpn (never changes results): RoIs
-    sorted by (image, level, y-band of 8 level pixels, x) and dealt so that the
-    blocks of one XCD (b % 8 equal) walk one contiguous slice of that order --
-    spatial neighbours, whose footprints overlap, run on the same L2.  With
-    `window` the dealing restarts every `window` positions (e.g. one frame's
-    RoIs), so all XCDs work on the same frame at a time; n_xcd=1 is the plain
-    spatial sort (the XCD-sliced kernel runs every RoI on every XCD)."""
+    sorted by (image, level, position) and dealt so that the blocks of one XCD
+    (b % 8 equal) walk one contiguous slice of that order -- spatial
+    neighbours, whose footprints overlap, run on the same L2.  `curve` orders
+    the positions: 'band' (y-band of `band` level pixels, then x) or 'morton'
+    (Z-order of the level-pixel centre: consecutive RoIs stay inside a square,
+    so the RoIs resident on an XCD at one time share more of their footprint;
+    tools/research/ra_l2_sim.py models the L2 misses of both).  The default is
+    VOSDET_RA_CURVE or 'morton'.  With `window` the dealing restarts every
+    `window` positions (e.g. one frame's RoIs), so all XCDs work on the same
+    frame at a time; n_xcd=1 is the plain spatial sort."""
+    curve = curve or os.environ.get("VOSDET_RA_CURVE", "morton")
     r = rois
     lv = roi_level.to(torch.int64)
     scale = torch.pow(2.0, -(lv + 2).to(torch.float32))
     cy = (r[:, 2] + r[:, 4]) * 0.5 * scale
     cx = (r[:, 1] + r[:, 3]) * 0.5 * scale
-    key = (((r[:, 0].to(torch.int64) * 8 + lv) * 4096 + (cy / band).to(torch.int64)) * 65536
-           + cx.clamp(0, 65535).to(torch.int64))
+    head = r[:, 0].to(torch.int64) * 8 + lv
+    if curve == "band":
+        key = (head * 4096 + (cy / band).to(torch.int64)) * 65536 \
+            + cx.clamp(0, 65535).to(torch.int64)
+    elif curve == "morton":
+        key = head * (1 << 32) + _morton16(cy.clamp(0, 65535).to(torch.int64),
+                                           cx.clamp(0, 65535).to(torch.int64))
+    else:
+        raise ValueError("curve must be 'band' or 'morton', got %r" % (curve,))
     srt = torch.argsort(key)
     n = r.shape[0]
     if n_xcd <= 1:
@@ -615,6 +642,51 @@ def mask_rle_counts(planes: torch.Tensor, cap: Optional[int] = None):
         if need <= cap:
             return counts, n
         cap = need
+
+
+def segm_rle_counts(masks: torch.Tensor, boxes: torch.Tensor, im_h: int, im_w: int,
+                    thresh: float = 0.5, cap: Optional[int] = None):
+    """paste_masks + mask_rle_counts fused (vd_segm_rle): the same counts and n
+    without materialising the M x im_h x im_w planes."""
+    m = _need(masks, "masks")
+    b = _need(boxes, "boxes")
+    M, R = m.shape[0], m.shape[-1]
+    if b.shape[0] != M or b.dim() != 2 or b.shape[1] < 4:
+        raise ValueError("boxes must be M x >=4, got %s" % (tuple(b.shape),))
+    cap = int(cap or (4 * im_w + 2))
+    while True:
+        counts = torch.empty((M, cap), dtype=torch.int32, device=m.device)
+        n = torch.empty((M,), dtype=torch.int32, device=m.device)
+        check(lib().vd_segm_rle(m.data_ptr(), M, R, b.data_ptr(), b.shape[1], int(im_h),
+                                int(im_w), float(np.float32(thresh)), counts.data_ptr(), cap,
+                                n.data_ptr(), _stream()), "vd_segm_rle")
+        need = int((-n).max().item()) if M else 0
+        if need <= cap:
+            return counts, n
+        cap = need
+
+
+def rle_strings(counts: torch.Tensor, n: torch.Tensor) -> list:
+    """pycocotools rleToString of each row's counts[:n] on the device
+    (vd_rle_strings): list of M ASCII strings, as segm_results stores them."""
+    c = _need(counts, "counts", torch.int32)
+    nn = _need(n, "n", torch.int32)
+    M, cap = c.shape
+    if M == 0:
+        return []
+    lens = torch.empty((M,), dtype=torch.int32, device=c.device)
+    check(lib().vd_rle_strings(c.data_ptr(), nn.data_ptr(), M, cap, lens.data_ptr(), None,
+                               _stream()), "vd_rle_strings")
+    offs = np.zeros(M + 1, np.int64)
+    np.cumsum(lens.cpu().numpy(), out=offs[1:])
+    total = int(offs[-1])
+    if total >= 2 ** 31:
+        raise ValueError("RLE strings of %d detections exceed 2 GiB" % M)
+    chars = torch.empty((max(total, 1),), dtype=torch.uint8, device=c.device)
+    check(lib().vd_rle_strings(c.data_ptr(), nn.data_ptr(), M, cap, lens.data_ptr(),
+                               chars.data_ptr(), _stream()), "vd_rle_strings")
+    buf = chars[:total].cpu().numpy().tobytes()
+    return [buf[offs[i]:offs[i + 1]].decode("ascii") for i in range(M)]
 
 
 # --------------------------------------------------------------------------- #
