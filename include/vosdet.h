@@ -331,6 +331,16 @@ int vd_detections_postfilter(float *dets, int32_t *classes, int32_t *counts, int
                              int det_cap, float nms_cross_class, int num_det_per_class_pre,
                              void *stream);
 
+/* vd_rpn_head: the FPN RPN head of one level after its shared 3x3 conv
+ * (lib/modeling/FPN.py:376-422, test branch): x = the conv's raw output WITHOUT
+ * its bias, N x H x W x C (NHWC, contiguous); conv_bias [C]; w [5A][C] = the
+ * cls_score (A rows) then bbox_pred (4A rows) 1x1 weights, b [5A] their biases.
+ * Writes cls_prob N x A x H x W = sigmoid(w_cls . relu(x + conv_bias) + b_cls)
+ * and bbox_pred N x 4A x H x W (NCHW), the layouts vd_generate_proposals reads.
+ * C % 64 == 0, 5A <= 16 (else VD_ERR_SHAPE). */
+int vd_rpn_head(const float *x, const float *conv_bias, const float *w, const float *b, int N,
+                int H, int W, int C, int A, float *cls_prob, float *bbox_pred, void *stream);
+
 /* ---------------------------------------------------------------------------
  * segm_results (lib/core/test.py:801-855; fork lib_vos/tools/vos_test.py:867-921)
  * on the device, SURVEY.md section 8f row 3.

@@ -101,3 +101,24 @@ def test_bottleneck_gemm_path_matches_conv_path(monkeypatch):
             monkeypatch.delenv("VOSDET_GEMM_EPILOGUE")
         assert y.is_contiguous(memory_format=torch.channels_last)
         assert float((y - y0).abs().max()) <= 1e-4 * max(1., float(y0.abs().max()))
+
+
+@pytest.mark.parametrize("N,C,H,W,A", [(2, 256, 50, 84, 3), (3, 64, 7, 11, 1), (1, 128, 1, 1, 3),
+                                       (16, 256, 13, 21, 3)])
+def test_rpn_head_vs_torch(N, C, H, W, A):
+    """vd_rpn_head (bias + ReLU + cls/bbox 1x1 + sigmoid in one pass over the raw
+    RPN conv output) against the unfused fp32 PyTorch sequence of FPN.py:376-422;
+    tile tails (N*H*W not a multiple of 64) included."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(N * 1000 + C + H)
+    x = torch.randn(N, C, H, W, generator=g).cuda().contiguous(memory_format=torch.channels_last)
+    cb = (torch.randn(C, generator=g) * 0.5).cuda()
+    w = (torch.randn(5 * A, C, generator=g) / C ** 0.5).cuda()
+    b = torch.randn(5 * A, generator=g).cuda()
+    h = F.relu(x + cb.view(1, -1, 1, 1))
+    o = F.conv2d(h.contiguous(), w.view(5 * A, C, 1, 1), b)
+    cls, box = ops.rpn_head(x, cb, w, b, A)
+    torch.cuda.synchronize()
+    assert cls.shape == (N, A, H, W) and box.shape == (N, 4 * A, H, W) and cls.is_contiguous()
+    torch.testing.assert_close(cls, torch.sigmoid(o[:, :A]), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(box, o[:, A:], rtol=1e-5, atol=2e-5)

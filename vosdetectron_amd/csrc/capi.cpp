@@ -406,6 +406,14 @@ int vd_rle_strings(const uint32_t *counts, const int32_t *ncounts, int M, int ca
     return launch_rle_strings(counts, ncounts, M, cap, lens, chars, VD_STREAM(stream));
 }
 
+int vd_rpn_head(const float *x, const float *conv_bias, const float *w, const float *b, int N,
+                int H, int W, int C, int A, float *cls_prob, float *bbox_pred, void *stream) {
+    if (!x || !conv_bias || !w || !b || !cls_prob || !bbox_pred || N < 0 || H < 0 || W < 0)
+        return VD_ERR_ARG;
+    return launch_rpn_head(x, conv_bias, w, b, N, H, W, C, A, cls_prob, bbox_pred,
+                           VD_STREAM(stream));
+}
+
 int vd_detections_postfilter(float *dets, int32_t *classes, int32_t *counts, int num_images,
                              int det_cap, float nms_cross_class, int num_det_per_class_pre,
                              void *stream) {

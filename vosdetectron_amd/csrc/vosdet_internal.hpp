@@ -124,6 +124,10 @@ int launch_segm_rle(const float *masks, int M, int R, const float *boxes, int bo
 int launch_rle_strings(const uint32_t *counts, const int32_t *ncounts, int M, int cap,
                        int32_t *lens, uint8_t *chars, hipStream_t s);
 
+int launch_rpn_head(const float *x, const float *conv_bias, const float *w, const float *b,
+                    int N, int H, int W, int C, int A, float *cls_prob, float *bbox_pred,
+                    hipStream_t s);
+
 int launch_detections_postfilter(float *dets, int32_t *cls, int32_t *counts, int num_images,
                                  int det_cap, float nms_cross_class, int num_det_per_class_pre,
                                  hipStream_t s);

@@ -18,6 +18,7 @@ preceding conv (``fold_affine``), the RPN's cls/bbox 1x1 convs are fused into on
 """
 from __future__ import annotations
 
+import os
 from collections import OrderedDict
 
 import numpy as np
@@ -374,11 +375,19 @@ class FPNRPNOutputs(nn.Module):
 
     def level_outputs(self, x):
         """(sigmoid cls probs N x A x H x W, bbox deltas N x 4A x H x W)."""
+        A = self.num_anchors
+        if (self.fused is not None and x.is_cuda and _gemm_ok(x) and 5 * A <= 16
+                and x.shape[1] % 64 == 0 and os.environ.get("VOSDET_RPN_HEAD", "1") != "0"):
+            # conv without bias, then bias + ReLU + both 1x1s + sigmoid in one pass
+            h = _conv_nb(self.FPN_RPN_conv, x)
+            if not h.is_contiguous(memory_format=torch.channels_last):
+                h = h.contiguous(memory_format=torch.channels_last)
+            return ops.rpn_head(h, self.FPN_RPN_conv.bias.detach(), self.fused_w2d,
+                                self.fused.bias.detach(), A)
         if self.fused is not None and x.is_cuda:
             h = _conv_epi(self.FPN_RPN_conv, x)
         else:
             h = F.relu(self.FPN_RPN_conv(x), inplace=True)
-        A = self.num_anchors
         if self.fused is not None:
             if _gemm_ok(h):  # the fused cls + bbox 1x1 as one GEMM with the bias epilogue
                 o = _gemm_conv1x1(h, self.fused_w2d, self.fused.bias.detach(), relu=False)

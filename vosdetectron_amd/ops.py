@@ -644,6 +644,29 @@ def mask_rle_counts(planes: torch.Tensor, cap: Optional[int] = None):
         cap = need
 
 
+def rpn_head(x_raw: torch.Tensor, conv_bias: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
+             num_anchors: int):
+    """FPN RPN head of one level (vd_rpn_head): x_raw = the shared 3x3 conv's
+    output without bias, N x C x H x W in channels_last memory; w [5A, C] (cls
+    then bbox 1x1 weights), b [5A].  Returns (cls_prob N x A x H x W after the
+    sigmoid, bbox_pred N x 4A x H x W), both contiguous NCHW."""
+    N, C, H, W = x_raw.shape
+    if not (x_raw.is_cuda and x_raw.dtype == torch.float32
+            and x_raw.is_contiguous(memory_format=torch.channels_last)):
+        raise ValueError("x_raw must be a channels_last float32 device tensor")
+    A = int(num_anchors)
+    cb = _need(conv_bias, "conv_bias")
+    wt = _need(w, "w")
+    bt = _need(b, "b")
+    if tuple(wt.shape) != (5 * A, C) or bt.numel() != 5 * A or cb.numel() != C:
+        raise ValueError("w must be [5A, C] = [%d, %d], b [5A], conv_bias [C]" % (5 * A, C))
+    cls = torch.empty((N, A, H, W), dtype=torch.float32, device=x_raw.device)
+    box = torch.empty((N, 4 * A, H, W), dtype=torch.float32, device=x_raw.device)
+    check(lib().vd_rpn_head(x_raw.data_ptr(), cb.data_ptr(), wt.data_ptr(), bt.data_ptr(), N, H,
+                            W, C, A, cls.data_ptr(), box.data_ptr(), _stream()), "vd_rpn_head")
+    return cls, box
+
+
 def segm_rle_counts(masks: torch.Tensor, boxes: torch.Tensor, im_h: int, im_w: int,
                     thresh: float = 0.5, cap: Optional[int] = None):
     """paste_masks + mask_rle_counts fused (vd_segm_rle): the same counts and n
