@@ -331,6 +331,14 @@ int vd_detections_postfilter(float *dets, int32_t *classes, int32_t *counts, int
                              int det_cap, float nms_cross_class, int num_det_per_class_pre,
                              void *stream);
 
+/* vd_bias_relu_maxpool: the stem tail of basic_bn_stem (lib/modeling/ResNet.py:
+ * 224-230) after a bias-free conv1: out = MaxPool2d(3, 2, 1)(relu(x + bias[c])),
+ * x N x H x W x C (NHWC), out N x Ho x Wo x C with Ho = (H - 1) / 2 + 1,
+ * Wo = (W - 1) / 2 + 1.  Bit-identical to vd_bias_act followed by the max-pool.
+ * C % 4 == 0. */
+int vd_bias_relu_maxpool(const float *x, const float *bias, int N, int C, int H, int W,
+                         float *out, void *stream);
+
 /* vd_rpn_head: the FPN RPN head of one level after its shared 3x3 conv
  * (lib/modeling/FPN.py:376-422, test branch): x = the conv's raw output WITHOUT
  * its bias, N x H x W x C (NHWC, contiguous); conv_bias [C]; w [5A][C] = the

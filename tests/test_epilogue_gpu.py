@@ -122,3 +122,19 @@ def test_rpn_head_vs_torch(N, C, H, W, A):
     assert cls.shape == (N, A, H, W) and box.shape == (N, 4 * A, H, W) and cls.is_contiguous()
     torch.testing.assert_close(cls, torch.sigmoid(o[:, :A]), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(box, o[:, A:], rtol=1e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("N,C,H,W", [(2, 64, 40, 66), (1, 64, 13, 7), (3, 8, 1, 2), (1, 64, 400, 672)])
+def test_bias_relu_maxpool_bit_exact(N, C, H, W):
+    """vd_bias_relu_maxpool == vd_bias_act(relu) + MaxPool2d(3, 2, 1) bit for bit
+    (basic_bn_stem's tail, ResNet.py:224-230), odd sizes included."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(H * W + C)
+    x = torch.randn(N, C, H, W, generator=g).cuda().contiguous(memory_format=torch.channels_last)
+    b = torch.randn(C, generator=g).cuda()
+    ref = F.max_pool2d(ops.bias_act_(x.clone(memory_format=torch.channels_last), b, relu=True),
+                       kernel_size=3, stride=2, padding=1)
+    got = ops.bias_relu_maxpool(x, b)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(got, ref)

@@ -68,6 +68,7 @@ SIGNATURES = {
     # segm_results (paste + binarize + RLE counts)
     "vd_paste_masks": (_I, [_P, _I, _I, _P, _I, _I, _I, _F, _P, _P]),
     "vd_mask_rle": (_I, [_P, _I, _I, _I, _P, _I, _P, _P]),
+    "vd_bias_relu_maxpool": (_I, [_P, _P, _I, _I, _I, _I, _P, _P]),
     "vd_rpn_head": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "vd_segm_rle": (_I, [_P, _I, _I, _P, _I, _I, _I, _F, _P, _I, _P, _P]),
     "vd_rle_strings": (_I, [_P, _P, _I, _I, _P, _P, _P]),

@@ -406,6 +406,12 @@ int vd_rle_strings(const uint32_t *counts, const int32_t *ncounts, int M, int ca
     return launch_rle_strings(counts, ncounts, M, cap, lens, chars, VD_STREAM(stream));
 }
 
+int vd_bias_relu_maxpool(const float *x, const float *bias, int N, int C, int H, int W,
+                         float *out, void *stream) {
+    if (!x || !bias || !out || N < 0 || C < 0 || H < 0 || W < 0) return VD_ERR_ARG;
+    return launch_bias_relu_maxpool(x, bias, N, C, H, W, out, VD_STREAM(stream));
+}
+
 int vd_rpn_head(const float *x, const float *conv_bias, const float *w, const float *b, int N,
                 int H, int W, int C, int A, float *cls_prob, float *bbox_pred, void *stream) {
     if (!x || !conv_bias || !w || !b || !cls_prob || !bbox_pred || N < 0 || H < 0 || W < 0)

@@ -464,4 +464,56 @@ int launch_bias_act(float *x, const float *bias, const float *z, const float *bi
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
+// ---------------------------------------------------------------- stem epilogue
+// basic_bn_stem's tail (lib/modeling/ResNet.py:224-230) after the bias-free
+// conv1: AffineChannel bias + ReLU + MaxPool2d(3, stride 2, pad 1) in one pass,
+// NHWC in and out.  Each window element is relu(x + b) exactly as vd_bias_act
+// computes it, and the max of those is what max_pool2d returns (padding never
+// wins: every window holds at least one in-image pixel), so the result is
+// bit-identical to bias_act + max_pool2d while the full-resolution activation
+// is read once instead of written and read again (HBM bytes per output pixel:
+// ~2.25 x 4C read through L2 for 4C written).
+__global__ __launch_bounds__(256) void bias_relu_maxpool_nhwc4_kernel(
+    const float *__restrict__ x, const float *__restrict__ bias, float *__restrict__ out,
+    uint32_t n4, uint32_t C4, uint32_t H, uint32_t W, uint32_t Ho, uint32_t Wo) {
+    for (uint32_t i4 = blockIdx.x * blockDim.x + threadIdx.x; i4 < n4;
+         i4 += blockDim.x * gridDim.x) {
+        const uint32_t c4 = i4 % C4, pix = i4 / C4;
+        const uint32_t wo = pix % Wo, t = pix / Wo;
+        const uint32_t ho = t % Ho, n = t / Ho;
+        const float4 b = reinterpret_cast<const float4 *>(bias)[c4];
+        float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+            const int y = 2 * (int)ho - 1 + dy;
+            if (y < 0 || y >= (int)H) continue;
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) {
+                const int xx = 2 * (int)wo - 1 + dx;
+                if (xx < 0 || xx >= (int)W) continue;
+                const float4 v = reinterpret_cast<const float4 *>(
+                    x)[((uint64_t)(n * H + y) * W + xx) * C4 + c4];
+                m.x = fmaxf(m.x, fmaxf(v.x + b.x, 0.f));
+                m.y = fmaxf(m.y, fmaxf(v.y + b.y, 0.f));
+                m.z = fmaxf(m.z, fmaxf(v.z + b.z, 0.f));
+                m.w = fmaxf(m.w, fmaxf(v.w + b.w, 0.f));
+            }
+        }
+        reinterpret_cast<float4 *>(out)[i4] = m;
+    }
+}
+
+int launch_bias_relu_maxpool(const float *x, const float *bias, int N, int C, int H, int W,
+                             float *out, hipStream_t s) {
+    if ((int64_t)N * H * W == 0) return VD_OK;
+    const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;  // (H + 2 - 3) / 2 + 1
+    const int64_t n4 = (int64_t)N * Ho * Wo * (C / 4);
+    if (C % 4 != 0 || (int64_t)N * H * W * C >= ((int64_t)1 << 32) || n4 >= ((int64_t)1 << 31))
+        return VD_ERR_SHAPE;
+    hipLaunchKernelGGL(bias_relu_maxpool_nhwc4_kernel, dim3(blocks_for(n4, 256)), dim3(256), 0, s,
+                       x, bias, out, (uint32_t)n4, (uint32_t)(C / 4), (uint32_t)H, (uint32_t)W,
+                       (uint32_t)Ho, (uint32_t)Wo);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
 }  // namespace vd

@@ -124,6 +124,8 @@ int launch_segm_rle(const float *masks, int M, int R, const float *boxes, int bo
 int launch_rle_strings(const uint32_t *counts, const int32_t *ncounts, int M, int cap,
                        int32_t *lens, uint8_t *chars, hipStream_t s);
 
+int launch_bias_relu_maxpool(const float *x, const float *bias, int N, int C, int H, int W,
+                             float *out, hipStream_t s);
 int launch_rpn_head(const float *x, const float *conv_bias, const float *w, const float *b,
                     int N, int H, int W, int C, int A, float *cls_prob, float *bbox_pred,
                     hipStream_t s);

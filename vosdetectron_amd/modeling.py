@@ -235,7 +235,11 @@ class _StemEpilogue(nn.Module):
 
     def forward(self, x):
         if x.is_cuda:
-            return self.maxpool(_conv_epi(self.conv1, x))
+            h = _conv_nb(self.conv1, x)
+            if (h.is_contiguous(memory_format=torch.channels_last) and not h.is_contiguous()
+                    and h.shape[1] % 4 == 0 and os.environ.get("VOSDET_STEM_FUSED", "1") != "0"):
+                return ops.bias_relu_maxpool(h, self.conv1.bias)  # one pass, bit-identical
+            return self.maxpool(ops.bias_act_(h, self.conv1.bias, relu=True))
         return self.maxpool(F.relu(self.conv1(x), inplace=True))
 
 

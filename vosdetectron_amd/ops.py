@@ -644,6 +644,24 @@ def mask_rle_counts(planes: torch.Tensor, cap: Optional[int] = None):
         cap = need
 
 
+def bias_relu_maxpool(x_raw: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    """ResNet stem tail (vd_bias_relu_maxpool): MaxPool2d(3, 2, 1)(relu(x + b)) of
+    a channels_last N x C x H x W tensor; returns channels_last N x C x Ho x Wo."""
+    N, C, H, W = x_raw.shape
+    if not (x_raw.is_cuda and x_raw.dtype == torch.float32
+            and x_raw.is_contiguous(memory_format=torch.channels_last)):
+        raise ValueError("x_raw must be a channels_last float32 device tensor")
+    b = _need(bias, "bias")
+    if b.numel() != C:
+        raise ValueError("bias must have C = %d entries" % C)
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    out = torch.empty((N, C, Ho, Wo), dtype=torch.float32, device=x_raw.device,
+                      memory_format=torch.channels_last)
+    check(lib().vd_bias_relu_maxpool(x_raw.data_ptr(), b.data_ptr(), N, C, H, W,
+                                     out.data_ptr(), _stream()), "vd_bias_relu_maxpool")
+    return out
+
+
 def rpn_head(x_raw: torch.Tensor, conv_bias: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
              num_anchors: int):
     """FPN RPN head of one level (vd_rpn_head): x_raw = the shared 3x3 conv's
