@@ -43,8 +43,94 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int mask) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, mask);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), mask);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Register form of the bitonic network below: thread t holds elements
+// t + e*T (T = blockDim.x, e < E).  Compare-exchange partners i ^ j are another
+// lane of the same wave for j < 64 (shuffle, no barrier), another element of
+// the same thread for j >= T (register), and otherwise go through LDS (one
+// barrier pair per stage).  Every pair ends with (max, min) or (min, max) by
+// the same rule as the LDS network, so the sorted array is identical.
+template <int E>
+__device__ __forceinline__ void bitonic_sort_desc_reg(uint64_t *keys, int n) {
+    const int T = blockDim.x, t = threadIdx.x;
+    const bool act = t < n;  // n < T: only the first n threads (whole waves) hold data
+    uint64_t v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = act ? keys[t + e * T] : 0ull;
+    for (int k = 2; k <= n; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= T) {
+                const int je = j / T;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int pe = e ^ je;
+                    if (pe > e) {
+                        const bool desc = ((t + e * T) & k) == 0;
+                        const uint64_t a = v[e], b = v[pe];
+                        const uint64_t mx = a > b ? a : b, mn = a > b ? b : a;
+                        v[e] = desc ? mx : mn;
+                        v[pe] = desc ? mn : mx;
+                    }
+                }
+            } else if (j >= 64) {
+                __syncthreads();
+                if (act) {
+#pragma unroll
+                    for (int e = 0; e < E; ++e) keys[t + e * T] = v[e];
+                }
+                __syncthreads();
+                if (act) {
+#pragma unroll
+                    for (int e = 0; e < E; ++e) {
+                        const int i = t + e * T;
+                        const uint64_t b = keys[i ^ j];
+                        const bool take_max = ((i & j) == 0) == ((i & k) == 0);
+                        v[e] = take_max ? (v[e] > b ? v[e] : b) : (v[e] > b ? b : v[e]);
+                    }
+                }
+            } else if (act) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int i = t + e * T;
+                    const uint64_t b = shfl_xor64(v[e], j);
+                    const bool take_max = ((i & j) == 0) == ((i & k) == 0);
+                    v[e] = take_max ? (v[e] > b ? v[e] : b) : (v[e] > b ? b : v[e]);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (act) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) keys[t + e * T] = v[e];
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void bitonic_sort_desc_lds(uint64_t *keys, int n);
+
 // Block-wide descending bitonic sort of n (power of two) 64-bit keys in LDS.
-__device__ inline void bitonic_sort_desc(uint64_t *keys, int n) {
+// Register network when blockDim.x is a power of two >= 64, n >= 64 and
+// n <= 8 * blockDim.x; the all-LDS network otherwise.
+// Forced inline: out of line, the LDS pointer becomes generic (flat accesses).
+__device__ __forceinline__ void bitonic_sort_desc(uint64_t *keys, int n) {
+    const int T = blockDim.x;
+    if (n >= 64 && T >= 64 && (T & (T - 1)) == 0 && (n <= T || n % T == 0)) {
+        const int E = n <= T ? 1 : n / T;
+        if (E == 1) return bitonic_sort_desc_reg<1>(keys, n);
+        if (E == 2) return bitonic_sort_desc_reg<2>(keys, n);
+        if (E == 4) return bitonic_sort_desc_reg<4>(keys, n);
+        if (E == 8) return bitonic_sort_desc_reg<8>(keys, n);
+    }
+    bitonic_sort_desc_lds(keys, n);
+}
+
+__device__ __forceinline__ void bitonic_sort_desc_lds(uint64_t *keys, int n) {
     for (int k = 2; k <= n; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
             for (int i = threadIdx.x; i < n; i += blockDim.x) {

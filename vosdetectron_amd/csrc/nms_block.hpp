@@ -42,9 +42,11 @@ __device__ inline void nms_build_mask_rows(const float *__restrict__ x1, const f
     }
 }
 
-// Phase 2, executed by ONE wave (all 64 lanes).  keep[rank] = 1/0.
-__device__ inline void nms_resolve_wave(const uint64_t *__restrict__ mask, int m,
-                                        uint8_t *__restrict__ keep) {
+// Phase 2, executed by ONE wave (all 64 lanes).  keep[rank] = 1/0.  Forced
+// inline: as an out-of-line call the 64-bit state spills to scratch and every
+// LDS mask read goes through flat addressing.
+__device__ __forceinline__ void nms_resolve_wave(const uint64_t *__restrict__ mask, int m,
+                                                 uint8_t *__restrict__ keep) {
     const int words = (m + 63) >> 6;
     const int lane = lane_id();
     uint64_t remv[kNmsMaxWordsPerLane];
@@ -58,25 +60,40 @@ __device__ inline void nms_resolve_wave(const uint64_t *__restrict__ mask, int m
 #pragma unroll
         for (int q = 0; q < kNmsMaxWordsPerLane; ++q)
             if (q == (blk >> 6)) cur = readlane64(remv[q], blk & 63);
-        uint64_t kept = 0;
+        // Greedy inside the block, visiting only rows that can change it: a
+        // row with an empty diagonal word suppresses nothing here, so the loop
+        // steps (find-first-set) through the not-yet-removed rows that do have
+        // suppression edges; every row left unremoved at the end is kept.
         const int nrows = min(64, m - (blk << 6));
-        for (int t = 0; t < nrows; ++t) {
-            if (!((cur >> t) & 1ull)) {
-                kept |= 1ull << t;
-                cur |= readlane64(diag, t);
-            }
+        const uint64_t valid = nrows == 64 ? ~0ull : ((1ull << nrows) - 1ull);
+        const uint64_t nz = ballot(diag != 0ull);
+        uint64_t todo = nz & ~cur & valid;
+        while (todo) {
+            const int t = __ffsll((unsigned long long)todo) - 1;
+            cur |= readlane64(diag, t);  // bits > t only (upper triangle)
+            todo &= ~cur & (~1ull << t);
         }
+        const uint64_t kept = ~cur & valid;
         if (row < m) keep[row] = (uint8_t)((kept >> lane) & 1ull);
-        // OR the kept rows of this block into the later words
+        // OR the kept rows of this block into the later words: 16 rows' words
+        // loaded before any is used (a dependent load per kept row made this
+        // loop one memory round trip per kept box)
 #pragma unroll
         for (int q = 0; q < kNmsMaxWordsPerLane; ++q) {
             const int w = lane + (q << 6);
             if (w > blk && w < words) {
-                uint64_t acc = 0, kb = kept;
-                while (kb) {
-                    const int t = __ffsll((unsigned long long)kb) - 1;
-                    kb &= kb - 1;
-                    acc |= mask[(int64_t)((blk << 6) + t) * words + w];
+                uint64_t acc = 0;
+                const uint64_t *col = mask + (int64_t)(blk << 6) * words + w;
+                for (int t0 = 0; t0 < nrows; t0 += 16) {
+                    const uint64_t kb = (kept >> t0) & 0xffffull;
+                    if (!kb) continue;  // wave-uniform
+                    uint64_t v[16];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        v[i] = col[(int64_t)min(t0 + i, nrows - 1) * words];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i)
+                        if ((kb >> i) & 1ull) acc |= v[i];
                 }
                 remv[q] |= acc;
             }

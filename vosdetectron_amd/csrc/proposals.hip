@@ -20,6 +20,8 @@
 //              the float64 BBOX_XFORM_CLIP; clip; min-size/centre filter.
 //   nms     -- processing order (score desc, position desc), ballot bitmask,
 //              single-wave resolve; survivors ascending, first post_nms_topN.
+#include <stdlib.h>
+
 #include "nms_block.hpp"
 #include "vosdet_internal.hpp"
 
@@ -66,6 +68,14 @@ static bool rpn_plan(const VdRpnLevel *levels, int num_levels, int pre_nms_topN,
     return true;
 }
 
+// Split NMS (the mask built by many workgroups, resolved by a third kernel):
+// always for the large variant; for the small one unless VOSDET_RPN_SPLIT=0.
+static bool rpn_split(bool large) {
+    if (large) return true;
+    const char *e = getenv("VOSDET_RPN_SPLIT");
+    return !(e && e[0] == '0');
+}
+
 static inline size_t rpn_slot_bytes(int max_pre, bool large) {
     const int p = max_pre < 64 ? 64 : max_pre;
     return large ? rpn_mask_bytes(p) + rpn_box_bytes(p) + rpn_key_bytes(p) : rpn_mask_bytes(p);
@@ -77,7 +87,8 @@ size_t rpn_workspace_bytes(const VdRpnLevel *levels, int num_levels, int num_ima
     bool large;
     if (num_levels < 1 || !rpn_plan(levels, num_levels, pre_nms_topN, &max_pre, &large))
         return 256;
-    return rpn_slot_bytes(max_pre, large) * (size_t)num_levels * (size_t)num_images + 256;
+    return rpn_slot_bytes(max_pre, rpn_split(large)) * (size_t)num_levels * (size_t)num_images +
+           256;
 }
 
 // numpy-2 bbox_transform of one box with weights (wx, wy, ww, wh): returns
@@ -132,6 +143,47 @@ struct RpnLds {
     int scratch[32];
 };
 
+// Block-strided walk over probs[0, n) in memory order, 8 loads per thread in
+// flight before any is consumed (a plain strided loop waits on every load:
+// ~200 dependent HBM round trips per pass over a P2 score map).  f(m, s) is
+// called for every m with s = probs[m], each wave's lanes on consecutive m;
+// in the last partial row the lanes past n call f(-1, 0) so that every lane of
+// a wave with work takes part in f's ballots.
+#ifdef VD_PROF
+#define PROF_DECL __shared__ long long prof_t[16]; int prof_n = 0;
+#define PROF_MARK() do { __syncthreads(); if (threadIdx.x == 0) prof_t[prof_n] = wall_clock64(); ++prof_n; } while (0)
+#define PROF_DUMP(tag) do { if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) { \
+    for (int i_ = 1; i_ < prof_n; ++i_) printf("%s phase %d: %.1f us\n", tag, i_, (prof_t[i_] - prof_t[i_ - 1]) * 0.01); } } while (0)
+#else
+#define PROF_DECL
+#define PROF_MARK()
+#define PROF_DUMP(tag)
+#endif
+
+template <class F>
+__device__ inline void sweep_probs(const float *__restrict__ probs, int n, F f) {
+    constexpr int U = 8;
+    const int bd = blockDim.x;
+    int m = threadIdx.x;
+    // full batches: every lane of the block has all U elements
+    const int full = (n / (U * bd)) * (U * bd);
+    for (; m < full; m += U * bd) {
+        float v[U];
+#pragma unroll
+        for (int i = 0; i < U; ++i) v[i] = probs[m + i * bd];
+#pragma unroll
+        for (int i = 0; i < U; ++i) f(m + i * bd, v[i]);
+    }
+    // tail: whole waves step together (ballots inside f stay wave-uniform)
+    for (int base = full; base < n; base += bd) {
+        const int i = base + (int)threadIdx.x;
+        if (base + (int)(threadIdx.x & ~63u) >= n) break;  // this wave has no element
+        const float v = i < n ? probs[i] : 0.f;
+        if (i < n) f(i, v);
+        else f(-1, 0.f);
+    }
+}
+
 template <int SelCap, int PreMax, bool GB>
 __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
     RpnArgs args, int num_levels, const float *__restrict__ im_info, int pre_nms_topN,
@@ -140,6 +192,8 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
     size_t slot_bytes, size_t mask_bytes, size_t box_bytes) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     auto &L = *reinterpret_cast<RpnLds<SelCap, PreMax, GB> *>(lds_raw);
+    PROF_DECL
+    PROF_MARK();
     const int l = blockIdx.x, img = blockIdx.y;
     const VdRpnLevel lv = args.lv[l];
     const int A = lv.A, H = lv.H, W = lv.W, K = H * W;
@@ -168,10 +222,17 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
         return ((uint64_t)float_key(s) << 32) | (uint32_t)(0xffffffffu - (uint32_t)e);
     };
     // memory-order walk for coalesced count passes: m = a*K + hw  ->  e
-    auto key_mem = [&](int m) -> uint64_t {
+    auto key_at = [&](int m, float s) -> uint64_t {
         const int a = m / K, hw = m - a * K;
         const int e = hw * A + a;
-        return ((uint64_t)float_key(probs[m]) << 32) | (uint32_t)(0xffffffffu - (uint32_t)e);
+        return ((uint64_t)float_key(s) << 32) | (uint32_t)(0xffffffffu - (uint32_t)e);
+    };
+
+    // key_at(m, s) >= thr, the index part (an integer division) only on a
+    // score tie with the threshold
+    auto ge_thr = [&](int m, float s, uint64_t thr) -> bool {
+        const uint32_t fk = float_key(s), th = (uint32_t)(thr >> 32);
+        return fk != th ? fk > th : key_at(m, s) >= thr;
     };
 
     const bool take_all = pre_nms_topN <= 0 || pre_nms_topN >= n_all;
@@ -187,9 +248,13 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
         for (int j = threadIdx.x; j < kSampleMax; j += blockDim.x)
             L.keys[j] = j < S ? key_of((int)(((int64_t)j * n_all) / S)) : 0ull;
         __syncthreads();
+        PROF_MARK();
         bitonic_sort_desc(L.keys, kSampleMax);
+        PROF_MARK();
         int lo = 0, hi = S - 1;  // rank window in the sorted sample
-        int rank = (int)(((int64_t)2 * pre * S + n_all - 1) / n_all);
+        // threshold at ~1.5x pre expected candidates: <= 2048 keys to sort for
+        // pre = 1000 (P2: rank 16 of the 2048-sample, ~4 % need a second count)
+        int rank = (int)(((int64_t)3 * pre * S + 2 * (int64_t)n_all - 1) / (2 * (int64_t)n_all));
         if (rank > S - 1) rank = S - 1;
         uint64_t thr = 0;
         ncand = -1;
@@ -197,7 +262,7 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
             thr = L.keys[rank];
             __syncthreads();
             int c = 0;
-            for (int m = threadIdx.x; m < n_all; m += blockDim.x) c += key_mem(m) >= thr;
+            sweep_probs(probs, n_all, [&](int m, float s) { c += m >= 0 && ge_thr(m, s, thr); });
             c = block_sum(c, L.scratch);
             if (c >= pre && c <= SelCap) { ncand = c; break; }
             if (c < pre) lo = rank + 1; else hi = rank - 1;
@@ -212,15 +277,31 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
             }
             return;
         }
-        block_compact(
-            n_all, [&](int m) { return key_mem(m) >= thr; },
-            [&](int pos, int m) { L.keys[pos] = key_mem(m); }, L.scratch);
+        PROF_MARK();
+        // unordered compaction (the candidates are sorted by their unique keys
+        // next): one LDS atomic per wave and batch, no barrier per element row
+        if (threadIdx.x == 0) L.scratch[31] = 0;
+        __syncthreads();
+        sweep_probs(probs, n_all, [&](int m, float s) {
+            const bool p = m >= 0 && ge_thr(m, s, thr);
+            const uint64_t b = ballot(p);
+            if (!b) return;
+            const uint64_t k = p ? key_at(m, s) : 0ull;
+            int base = 0;
+            if (lane_id() == __ffsll((unsigned long long)b) - 1)
+                base = atomicAdd(&L.scratch[31], __popcll(b));
+            base = __shfl(base, __ffsll((unsigned long long)b) - 1);
+            if (p) L.keys[base + lane_prefix(b)] = k;
+        });
+        __syncthreads();
     }
     {
         const int np2 = next_pow2(ncand);
         for (int i = ncand + threadIdx.x; i < np2; i += blockDim.x) L.keys[i] = 0ull;
         __syncthreads();
+        PROF_MARK();
         bitonic_sort_desc(L.keys, np2);
+        PROF_MARK();
     }
 
     // ---- decode + clip + filter (positions in score order)
@@ -288,11 +369,19 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
 
     // ---- NMS: processing order = scores.argsort()[::-1] on the sorted array
     {
+        // psc is non-increasing (candidates sorted by score); only equal scores
+        // can reorder, so without ties the processing order is the identity
+        int ties = 0;
+        for (int p = threadIdx.x; p + 1 < m; p += blockDim.x)
+            ties |= float_key(psc[p]) == float_key(psc[p + 1]);
+        ties = block_sum(ties, L.scratch);
         const int np2 = next_pow2(m);
         for (int p = threadIdx.x; p < np2; p += blockDim.x)
             L.keys[p] = p < m ? ((uint64_t)float_key(psc[p]) << 32) | (uint32_t)p : 0ull;
         __syncthreads();
-        if (m > 1) bitonic_sort_desc(L.keys, np2);
+        PROF_MARK();
+        if (m > 1 && ties) bitonic_sort_desc(L.keys, np2);
+        PROF_MARK();
     }
     for (int r = threadIdx.x; r < m; r += blockDim.x) {
         const int p = (int)(uint32_t)L.keys[r];
@@ -305,6 +394,8 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
         if (GB) gkeys[r] = L.keys[r];
     }
     if (GB) {  // mask rows and resolve run as rpn_nms_mask_kernel / rpn_nms_finish_kernel
+        PROF_MARK();
+        PROF_DUMP("select");
         if (threadIdx.x == 0) *gm = m;
         return;
     }
@@ -354,20 +445,28 @@ __global__ __launch_bounds__(1024) void rpn_nms_mask_kernel(char *__restrict__ w
                         gridDim.x * wpb);
 }
 
-// Large variant, phase 3: greedy resolve (one wave) + ascending compaction.
-struct RpnFinishLds {
-    uint64_t keys[kPreMaxL];
-    uint8_t keep_rank[kPreMaxL];
-    uint8_t keep_pos[kPreMaxL];
-    int scratch[32];
-};
+// Split NMS, phase 3: greedy resolve (one wave) + ascending compaction.  The
+// slot's mask is first copied into LDS by the whole workgroup when it fits
+// (m <= ~1300 at 160 KiB): the resolve then waits on LDS, not on a global
+// round trip per 64-row block.  LDS: keys[cap] u64 | keep_rank[cap] |
+// keep_pos[cap] | scratch int[32] | mask (optional).
+__host__ __device__ inline size_t finish_lds_base(int cap) {
+    return a256((size_t)cap * 8 + 2 * (size_t)cap) + 32 * sizeof(int);
+}
 
 __global__ __launch_bounds__(1024) void rpn_nms_finish_kernel(
     int num_levels, int post_nms_topN, float *__restrict__ rois_out,
     float *__restrict__ probs_out, int32_t *__restrict__ counts_out, char *__restrict__ ws,
-    size_t slot_bytes, size_t mask_bytes, size_t box_bytes) {
+    size_t slot_bytes, size_t mask_bytes, size_t box_bytes, int cap_keys, int lds_mask_rows) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-    RpnFinishLds &L = *reinterpret_cast<RpnFinishLds *>(lds_raw);
+    uint64_t *keys = reinterpret_cast<uint64_t *>(lds_raw);
+    uint8_t *keep_rank = reinterpret_cast<uint8_t *>(keys + cap_keys);
+    uint8_t *keep_pos = keep_rank + cap_keys;
+    const size_t base_bytes = finish_lds_base(cap_keys);
+    int *scratch = reinterpret_cast<int *>(lds_raw + base_bytes - 32 * sizeof(int));
+    uint64_t *lmask = reinterpret_cast<uint64_t *>(lds_raw + base_bytes);
+    PROF_DECL
+    PROF_MARK();
     const int l = blockIdx.x, img = blockIdx.y;
     const int slot = img * num_levels + l;
     char *base = ws + (size_t)slot * slot_bytes;
@@ -378,19 +477,31 @@ __global__ __launch_bounds__(1024) void rpn_nms_finish_kernel(
     if (m < 0) return;  // finished in phase 1 (no NMS, or could not bracket)
     const float *px1 = boxes, *py1 = boxes + bstride, *px2 = boxes + 2 * bstride;
     const float *py2 = boxes + 3 * bstride, *psc = boxes + 4 * bstride;
-    for (int r = threadIdx.x; r < m; r += blockDim.x) L.keys[r] = gkeys[r];
+    for (int r = threadIdx.x; r < m; r += blockDim.x) keys[r] = gkeys[r];
+    const uint64_t *gmask = reinterpret_cast<const uint64_t *>(base);
+    const bool in_lds = m <= lds_mask_rows;
+    if (in_lds) {  // whole mask (m rows x words) into LDS
+        const int n = m * ((m + 63) >> 6);
+        for (int i = threadIdx.x; i < n; i += blockDim.x) lmask[i] = gmask[i];
+    }
     __syncthreads();
-    if (wave_id() == 0 && m > 0)
-        nms_resolve_wave(reinterpret_cast<const uint64_t *>(base), m, L.keep_rank);
+    PROF_MARK();
+    if (wave_id() == 0 && m > 0) {  // two inlined copies: ds_read / global_load
+        if (in_lds)
+            nms_resolve_wave(lmask, m, keep_rank);
+        else
+            nms_resolve_wave(gmask, m, keep_rank);
+    }
     __syncthreads();
+    PROF_MARK();
     for (int r = threadIdx.x; r < m; r += blockDim.x)
-        L.keep_pos[(int)(uint32_t)L.keys[r]] = L.keep_rank[r];
+        keep_pos[(int)(uint32_t)keys[r]] = keep_rank[r];
     __syncthreads();
     const int cap = post_nms_topN;
     float *ro = rois_out + (size_t)slot * cap * 5;
     float *po = probs_out + (size_t)slot * cap;
     const int kept = block_compact(
-        m, [&](int p) { return L.keep_pos[p] != 0; },
+        m, [&](int p) { return keep_pos[p] != 0; },
         [&](int pos, int p) {
             if (pos < cap) {
                 ro[pos * 5 + 0] = (float)img;
@@ -401,7 +512,9 @@ __global__ __launch_bounds__(1024) void rpn_nms_finish_kernel(
                 po[pos] = psc[p];
             }
         },
-        L.scratch);
+        scratch);
+    PROF_MARK();
+    PROF_DUMP("finish");
     if (threadIdx.x == 0) counts_out[slot] = min(kept, cap);
 }
 
@@ -416,27 +529,42 @@ int launch_rpn_proposals(const VdRpnLevel *levels, int num_levels, int num_image
     int max_pre;
     bool large;
     if (!rpn_plan(levels, num_levels, pre_nms_topN, &max_pre, &large)) return VD_ERR_SHAPE;
+    const bool split = rpn_split(large);
     const int p = max_pre < 64 ? 64 : max_pre;
     const size_t mb = rpn_mask_bytes(p);
-    const size_t bb = large ? rpn_box_bytes(p) : 0;
-    const size_t sb = rpn_slot_bytes(max_pre, large);
+    const size_t bb = split ? rpn_box_bytes(p) : 0;
+    const size_t sb = rpn_slot_bytes(max_pre, split);
     if (!workspace || ws_bytes < sb * (size_t)num_levels * (size_t)num_images)
         return VD_ERR_WORKSPACE;
     const dim3 grid(num_levels, num_images);
-    if (large) {
-        using Lds = RpnLds<kSelCapL, kPreMaxL, true>;
-        hipLaunchKernelGGL((rpn_proposals_kernel<kSelCapL, kPreMaxL, true>), grid, dim3(1024),
-                           sizeof(Lds), s, args, num_levels, im_info,
-                           pre_nms_topN, post_nms_topN, nms_thresh, min_size, rois_out,
-                           probs_out, counts_out, (char *)workspace, sb, mb, bb);
+    if (split) {
+        if (large) {
+            using Lds = RpnLds<kSelCapL, kPreMaxL, true>;
+            hipLaunchKernelGGL((rpn_proposals_kernel<kSelCapL, kPreMaxL, true>), grid,
+                               dim3(1024), sizeof(Lds), s, args, num_levels, im_info,
+                               pre_nms_topN, post_nms_topN, nms_thresh, min_size, rois_out,
+                               probs_out, counts_out, (char *)workspace, sb, mb, bb);
+        } else {
+            using Lds = RpnLds<kSelCap, kPreMax, true>;
+            hipLaunchKernelGGL((rpn_proposals_kernel<kSelCap, kPreMax, true>), grid, dim3(1024),
+                               sizeof(Lds), s, args, num_levels, im_info, pre_nms_topN,
+                               post_nms_topN, nms_thresh, min_size, rois_out, probs_out,
+                               counts_out, (char *)workspace, sb, mb, bb);
+        }
         if (nms_thresh > 0.f) {
             const int rows_per_block = 16;  // 16 waves, one row each per pass
             const dim3 mgrid((p + rows_per_block - 1) / rows_per_block, num_levels * num_images);
             hipLaunchKernelGGL(rpn_nms_mask_kernel, mgrid, dim3(64 * rows_per_block), 0, s,
                                (char *)workspace, sb, mb, bb, nms_thresh);
-            hipLaunchKernelGGL(rpn_nms_finish_kernel, grid, dim3(1024), sizeof(RpnFinishLds), s,
-                               num_levels, post_nms_topN, rois_out, probs_out, counts_out,
-                               (char *)workspace, sb, mb, bb);
+            // keys / keep arrays for p candidates, plus the mask when it fits
+            const size_t lbase = finish_lds_base(p);
+            const int words = (p + 63) / 64;
+            const size_t lmask = (size_t)p * words * 8;
+            const bool in_lds = lbase + lmask <= 160 * 1024;
+            hipLaunchKernelGGL(rpn_nms_finish_kernel, grid, dim3(1024),
+                               lbase + (in_lds ? lmask : 0), s, num_levels, post_nms_topN,
+                               rois_out, probs_out, counts_out, (char *)workspace, sb, mb, bb,
+                               p, in_lds ? p : 0);
         }
     } else {
         using Lds = RpnLds<kSelCap, kPreMax, false>;
