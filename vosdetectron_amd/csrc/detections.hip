@@ -72,15 +72,41 @@ __device__ __forceinline__ void decode_box_w(float bx1, float by1, float bx2, fl
     y2 = (float)((double)pcy + 0.5 * ph - 1.0);
 }
 
+// Per-workgroup LDS, sized for cap = next_pow2(R_cap) candidates at launch
+// (55 KiB at R_cap = 1000, two workgroups per CU; a fixed kDetRMax layout
+// took 110 KiB and serialised the (class, image) workgroups one per CU).
 struct ClsLds {
-    uint64_t keys[kDetRMax];
-    int cand[kDetRMax];
-    float cx1[kDetRMax], cy1[kDetRMax], cx2[kDetRMax], cy2[kDetRMax], csc[kDetRMax];
-    float ox1[kDetRMax], oy1[kDetRMax], ox2[kDetRMax], oy2[kDetRMax], oar[kDetRMax];
-    uint8_t keep_rank[kDetRMax], keep_t[kDetRMax];
-    float wts[4];
-    int scratch[32];
+    uint64_t *keys;
+    int *cand;
+    float *cx1, *cy1, *cx2, *cy2, *csc, *ox1, *oy1, *ox2, *oy2, *oar;
+    uint8_t *keep_rank, *keep_t;
+    float *wts;
+    int *scratch;
 };
+
+__host__ __device__ inline size_t cls_lds_bytes(int cap) {
+    return (size_t)cap * (8 + 4 + 10 * 4 + 2) + 4 * 4 + 32 * 4;
+}
+
+__device__ inline ClsLds cls_lds(char *p, int cap) {
+    ClsLds L;
+    L.keys = reinterpret_cast<uint64_t *>(p);
+    p += (size_t)cap * 8;
+    L.cand = reinterpret_cast<int *>(p);
+    p += (size_t)cap * 4;
+    float **f[10] = {&L.cx1, &L.cy1, &L.cx2, &L.cy2, &L.csc, &L.ox1, &L.oy1, &L.ox2, &L.oy2, &L.oar};
+    for (int i = 0; i < 10; ++i) {
+        *f[i] = reinterpret_cast<float *>(p);
+        p += (size_t)cap * 4;
+    }
+    L.wts = reinterpret_cast<float *>(p);
+    p += 16;
+    L.scratch = reinterpret_cast<int *>(p);
+    p += 128;
+    L.keep_rank = reinterpret_cast<uint8_t *>(p);
+    L.keep_t = L.keep_rank + cap;
+    return L;
+}
 
 __global__ __launch_bounds__(1024) void class_nms_kernel(
     const float *__restrict__ rois, const float *__restrict__ cls_prob,
@@ -88,7 +114,7 @@ __global__ __launch_bounds__(1024) void class_nms_kernel(
     const float *__restrict__ im_scale, const int32_t *__restrict__ im_hw, float score_thresh,
     float nms_thresh, float4 bbox_w, DetWs ws) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-    ClsLds &L = *reinterpret_cast<ClsLds *>(lds_raw);
+    const ClsLds L = cls_lds(lds_raw, next_pow2(R_cap < 64 ? 64 : R_cap));
     const int j = blockIdx.x + 1, img = blockIdx.y;
     const int R = min(roi_count[img], R_cap);
     if (threadIdx.x == 0) {
@@ -240,7 +266,8 @@ int launch_box_detections(const float *rois, const float *cls_prob, const float 
         return VD_ERR_WORKSPACE;
     DetWs ws = det_ws(workspace, R_cap, num_images, K);
     const float4 bw = make_float4(bbox_weights[0], bbox_weights[1], bbox_weights[2], bbox_weights[3]);
-    hipLaunchKernelGGL(class_nms_kernel, dim3(K - 1, num_images), dim3(1024), sizeof(ClsLds), s,
+    const int cap = next_pow2(R_cap < 64 ? 64 : R_cap);
+    hipLaunchKernelGGL(class_nms_kernel, dim3(K - 1, num_images), dim3(1024), cls_lds_bytes(cap), s,
                        rois, cls_prob, bbox_pred, roi_count, R_cap, K, im_scale, im_hw,
                        score_thresh, nms_thresh, bw, ws);
     hipLaunchKernelGGL(det_limit_kernel, dim3(num_images), dim3(1024), 0, s, roi_count, R_cap, K,

@@ -20,6 +20,8 @@
 // [C][16] copy held in LDS and read as broadcasts).  Sums run over the
 // channels in order with FMA (the 1x1 convolutions' summation order is the
 // library's in the reference: tolerance, not bit parity).
+#include <stdlib.h>
+
 #include "common.hpp"
 #include "vosdet_internal.hpp"
 
@@ -42,17 +44,30 @@ __global__ __launch_bounds__(256) void rpn_head_kernel(
         const int c = i >> 4, j = i & 15;
         wt[i] = j < cout ? w[(int64_t)j * C + c] : 0.f;
     }
-    const float *src = x + p0 * C;
-    for (int i = threadIdx.x; i < np * C4; i += blockDim.x) {
+    // tile fill: 16 float4 loads per thread (the whole 64 KiB tile at C = 256)
+    // in flight before any is stored (a load -> store loop waits one HBM round
+    // trip per float4)
+    const float4 *src = reinterpret_cast<const float4 *>(x + p0 * C);
+    const int n4 = np * C4, bd = blockDim.x;
+    auto put = [&](int i, float4 v) {
         const int p = i / C4, c = (i - p * C4) * 4;
-        float4 v = *reinterpret_cast<const float4 *>(src + (int64_t)i * 4);
         const float4 cb = *reinterpret_cast<const float4 *>(conv_bias + c);
         v.x = fmaxf(v.x + cb.x, 0.f);
         v.y = fmaxf(v.y + cb.y, 0.f);
         v.z = fmaxf(v.z + cb.z, 0.f);
         v.w = fmaxf(v.w + cb.w, 0.f);
         *reinterpret_cast<float4 *>(tile + p * C + (((c >> 2) ^ (p & 15)) << 2)) = v;
+    };
+    constexpr int U = 16;
+    int i = threadIdx.x;
+    for (; i + (U - 1) * bd < n4; i += U * bd) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = src[i + u * bd];
+#pragma unroll
+        for (int u = 0; u < U; ++u) put(i + u * bd, v[u]);
     }
+    for (; i < n4; i += bd) put(i, src[i]);
     __syncthreads();
     const int lane = lane_id(), j0 = 4 * wave_id();
     if (j0 >= cout || lane >= np) return;
@@ -86,6 +101,72 @@ __global__ __launch_bounds__(256) void rpn_head_kernel(
     }
 }
 
+// MFMA form (C = 256, 5A <= 16): a wave computes 16 pixels x 16 outputs per
+// step with v_mfma_f32_16x16x4_f32, straight from global memory, no LDS tile.
+// Lane l: pixel (block base + l % 16), channel group kq = l / 16.  For step s
+// (0..15) the lane loads the float4 of channels 16 s + 4 kq .. + 3 of its pixel
+// (the 4 lane groups read 64 contiguous bytes of each pixel; over the 16 steps
+// every byte of the 1 KiB pixel once), applies bias + ReLU, and feeds the 4
+// values to 4 MFMAs as A[pixel][k = kq]; B[k = kq][n = l % 16] is the matching
+// weight, held in 64 VGPRs for the whole launch.  The k order is a permutation
+// of the channels, shared by A and B, so D = relu(x + b_conv) . W^T exactly up
+// to summation order.  D: lane l, register r = output n = l % 16 of pixel
+// 4 kq + r.  16 loads (16 KiB per wave) are in flight per step block.
+__global__ __launch_bounds__(256) void rpn_head_mfma_kernel(
+    const float *__restrict__ x, const float *__restrict__ conv_bias,
+    const float *__restrict__ w, const float *__restrict__ b, int A, int64_t npix, int HW,
+    float *__restrict__ cls_prob, float *__restrict__ bbox_pred) {
+    constexpr int C = 256, S = C / 16;
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) float cb_s[C];
+    for (int i = threadIdx.x; i < C; i += blockDim.x) cb_s[i] = conv_bias[i];
+    __syncthreads();
+    const int lane = lane_id(), n = lane & 15, kq = lane >> 4;
+    const int cout = 5 * A;
+    float4 wr[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+        wr[s] = n < cout ? *reinterpret_cast<const float4 *>(w + (int64_t)n * C + 16 * s + 4 * kq)
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float bn = n < cout ? b[n] : 0.f;
+    const int64_t nblk = (npix + 15) / 16;
+    const int64_t wave0 = (int64_t)blockIdx.x * num_waves() + wave_id();
+    const int64_t nwaves = (int64_t)gridDim.x * num_waves();
+    for (int64_t blk = wave0; blk < nblk; blk += nwaves) {
+        int64_t p = blk * 16 + n;
+        if (p >= npix) p = npix - 1;  // tail lanes read a valid pixel, result dropped
+        const float4 *xp = reinterpret_cast<const float4 *>(x + p * C + 4 * kq);
+        float4 a[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) a[s] = xp[4 * s];
+        f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const float4 cb = *reinterpret_cast<const float4 *>(cb_s + 16 * s + 4 * kq);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fmaxf(a[s].x + cb.x, 0.f), wr[s].x, acc,
+                                                      0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fmaxf(a[s].y + cb.y, 0.f), wr[s].y, acc,
+                                                      0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fmaxf(a[s].z + cb.z, 0.f), wr[s].z, acc,
+                                                      0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fmaxf(a[s].w + cb.w, 0.f), wr[s].w, acc,
+                                                      0, 0, 0);
+        }
+        if (n >= cout) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t pp = blk * 16 + 4 * kq + r;
+            if (pp >= npix) break;
+            const int64_t img = pp / HW, q = pp - img * HW;
+            const float o = acc[r] + bn;
+            if (n < A)
+                cls_prob[(img * A + n) * HW + q] = 1.f / (1.f + expf(-o));
+            else
+                bbox_pred[(img * 4 * A + (n - A)) * HW + q] = o;
+        }
+    }
+}
+
 int launch_rpn_head(const float *x, const float *conv_bias, const float *w, const float *b,
                     int N, int H, int W, int C, int A, float *cls_prob, float *bbox_pred,
                     hipStream_t s) {
@@ -94,6 +175,15 @@ int launch_rpn_head(const float *x, const float *conv_bias, const float *w, cons
     if (C % 64 != 0 || A < 1 || 5 * A > 16) return VD_ERR_SHAPE;  // swizzle: 16 | C/4
     const size_t lds = ((size_t)kRpnTile * C + (size_t)C * 16) * 4;
     if (lds > 160 * 1024) return VD_ERR_SHAPE;
+    const char *e = getenv("VOSDET_RPN_HEAD_MFMA");
+    if (C == 256 && !(e && e[0] == '0')) {
+        const int64_t waves = (npix + 15) / 16;
+        int64_t grid = (waves + 3) / 4;
+        if (grid > 256 * 8) grid = 256 * 8;  // grid-stride over 16-pixel blocks
+        hipLaunchKernelGGL(rpn_head_mfma_kernel, dim3((unsigned)grid), dim3(256), 0, s, x,
+                           conv_bias, w, b, A, npix, H * W, cls_prob, bbox_pred);
+        return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+    }
     const int64_t blocks = (npix + kRpnTile - 1) / kRpnTile;
     hipLaunchKernelGGL(rpn_head_kernel, dim3((unsigned)blocks), dim3(256), lds, s, x, conv_bias,
                        w, b, C, A, npix, H * W, cls_prob, bbox_pred);
