@@ -382,7 +382,8 @@ int vd_mask_rle(const uint8_t *masks, int M, int H, int W, uint32_t *counts, int
  * (0 for ncounts[m] <= 0).  chars != NULL: lens must hold those lengths
  * (sum < 2^31); detection m's ASCII string is written at
  * chars[lens[0] + ... + lens[m-1]], unterminated.  Replaces the host-side
- * `rleToString` + `.decode('ascii')` of segm_results (test.py:834-842). */
+ * mask_util.encode(...)['counts'].decode('ascii') of segm_results
+ * (lib/core/test.py:844-847). */
 int vd_segm_rle(const float *masks, int M, int R, const float *boxes, int box_stride,
                 int im_h, int im_w, float thresh, uint32_t *counts, int cap, int32_t *ncounts,
                 void *stream);
