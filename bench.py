@@ -217,15 +217,11 @@ def cpu_model():
     return platform.processor() or platform.machine()
 
 
-def cpu_baseline(cfg_name, sd, n_frames=16, threads=None, cfg=None, min_seconds=10.0):
-    """The reference's CPU path (oracle/pipeline.py, oracle/vos_pipeline.py) on a
-    bounded sample: frames are run until ``min_seconds`` of CPU work (at least 2 frames,
-    at most ``n_frames``), so the sample is ~10-30 s whatever the host."""
+def ref_cpu_pipeline(sd, n_frames, cfg):
+    """(pipeline, frames, description): the reference's CPU im_detect_all for the
+    config (oracle/pipeline.py, oracle/vos_pipeline.py) and its synthetic frames."""
     from oracle.pipeline import RefCPUPipeline
-    share, caps = cpu_share()
-    threads = threads or share
-    torch.set_num_threads(threads)
-    if cfg is not None and cfg.get("VOS", False):
+    if cfg.get("VOS", False):
         from oracle.vos_pipeline import RefCPUVOSPipeline
         ref = RefCPUVOSPipeline(sd, dynamic=cfg.CONVGRU.DYNAMIC_MODEL,
                                 num_classes=cfg.MODEL.NUM_CLASSES, max_size=cfg.TEST.MAX_SIZE)
@@ -245,6 +241,75 @@ def cpu_baseline(cfg_name, sd, n_frames=16, threads=None, cfg=None, min_seconds=
                              groups=cfg.RESNETS.NUM_GROUPS)
         fr = synthetic_frames(n_frames + 1, 1000)
         what = "800x1333 frames"
+    return ref, fr, what
+
+
+def frame_flops(sd, cfg):
+    """Algorithmic FLOPs of one frame (torch.utils.flop_counter,
+    2 per MAC, convs + linears incl. the mask head at that frame's detections),
+    counted on the reference's CPU path -- independent of how the GPU path
+    fuses or lays out the contractions.  Returns (flops, detections)."""
+    from torch.utils.flop_counter import FlopCounterMode
+    ref, fr, _ = ref_cpu_pipeline(sd, 0, cfg)
+    with FlopCounterMode(display=False) as fc:
+        res = ref(fr[0])
+    return int(fc.get_total_flops()), int(len(res[1]))
+
+
+def measure_hbm_copy(dev, nbytes=2 << 30, iters=20):
+    """Device-to-device copy bandwidth (read + write bytes / time), SURVEY.md 8(d)'s
+    'measured stream-copy bandwidth' beside the 8 TB/s spec peak."""
+    n = nbytes // 4
+    src = torch.empty(n, device=dev).uniform_()
+    dst = torch.empty_like(src)
+    for _ in range(3):
+        dst.copy_(src)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        dst.copy_(src)
+    e1.record(s)
+    e1.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / iters
+    del src, dst
+    return {"GBs": round(2 * n * 4 / t / 1e9, 1), "frac_of_spec": round(2 * n * 4 / t / 1e9 /
+                                                                         HBM_PEAK_GBS, 4),
+            "bytes_per_copy": 2 * n * 4, "how": "torch copy_ of a 2 GiB fp32 buffer, HIP events"}
+
+
+MFMA_FP32_PEAK_TFS = 157.3  # MI355X dense fp32 matrix peak (SURVEY.md 8(d))
+
+
+def step_roofline(flops_frame, dets_cpu, frames, ms_per_step, engine_launch, frame_hw, blob_hw):
+    """the FPS as a fraction of the roofline = sum of per-stage
+    bound times / measured step time.  MFMA-bound stages: the frame's algorithmic
+    FLOPs at the fp32 matrix peak; HBM-bound stages: the box RoIAlign's algorithmic
+    bytes (the engine's own launch) and frame prep (u8 read + fp32 blob write) at
+    8 TB/s; latency-bound stages (proposals, NMS) carry no bound."""
+    mfma_ms = flops_frame * frames / (MFMA_FP32_PEAK_TFS * 1e12) * 1e3
+    h, w = frame_hw
+    blob_bytes = frames * (h * w * 3 + 3 * 4 * blob_hw[0] * blob_hw[1])
+    ra_bytes = engine_launch["algorithmic_bytes_per_launch"] if engine_launch else 0
+    hbm_ms = (blob_bytes + ra_bytes) / (HBM_PEAK_GBS * 1e9) * 1e3
+    bound = mfma_ms + hbm_ms
+    return {"bound_ms_per_step": round(bound, 3), "mfma_bound_ms": round(mfma_ms, 3),
+            "hbm_bound_ms": round(hbm_ms, 3), "frac": round(bound / ms_per_step, 4),
+            "gflop_per_frame": round(flops_frame / 1e9, 2), "dets_in_counted_frame": dets_cpu,
+            "mfma_util_step": round(mfma_ms / ms_per_step, 4),
+            "peaks": {"fp32_matrix_TFs": MFMA_FP32_PEAK_TFS, "hbm_GBs": HBM_PEAK_GBS},
+            "flops_source": "torch.utils.flop_counter over one frame of the reference CPU path "
+                            "(oracle/pipeline.py), 2 flop per MAC"}
+
+
+def cpu_baseline(cfg_name, sd, n_frames=16, threads=None, cfg=None, min_seconds=10.0):
+    """The reference's CPU path (oracle/pipeline.py, oracle/vos_pipeline.py) on a
+    bounded sample: frames are run until ``min_seconds`` of CPU work (at least 2 frames,
+    at most ``n_frames``), so the sample is ~10-30 s whatever the host."""
+    share, caps = cpu_share()
+    threads = threads or share
+    torch.set_num_threads(threads)
+    ref, fr, what = ref_cpu_pipeline(sd, n_frames, cfg)
     ref(fr[0])  # warm-up
     t0 = time.perf_counter()
     done = 0
@@ -573,6 +638,14 @@ def main():
         roof = measure_roialign_roofline(dev)
         if not vos and cfg.FPN.FPN_ON:
             roof["engine_launch"] = measure_pipeline_roialign(pipe, any_frames)
+        extra["hbm_copy"] = measure_hbm_copy(dev)
+        nthr = torch.get_num_threads()
+        torch.set_num_threads(cpu_share()[0])
+        flops, dets_cpu = frame_flops(sd, cfg)
+        torch.set_num_threads(nthr)
+        extra["step_roofline"] = step_roofline(
+            flops, dets_cpu, F, dt / args.steps * 1e3, roof.get("engine_launch"), (fh, fw),
+            (getattr(pipe, "Hp", fh), getattr(pipe, "Wp", fw)))
     cpu = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:
         cpu = cpu_baseline(args.config, sd, args.cpu_frames, cfg=cfg)

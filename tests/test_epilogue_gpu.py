@@ -80,6 +80,29 @@ def test_gemm_bias_act_vs_torch():
         assert float((got2 - ref2).abs().max()) <= 2e-5 * max(1., float(ref2.abs().max()))
 
 
+@pytest.mark.parametrize("K,N", [(64, 256), (64, 64), (256, 64)])
+@pytest.mark.parametrize("M", [4096, 1003, 16, 1])
+def test_gemm1x1_mfma_vs_torch(monkeypatch, K, N, M):
+    """The hand-written MFMA 1x1-conv GEMM (csrc/gemm1x1.hip, forced with
+    VOSDET_GEMM_MFMA=1) vs a plain torch fp32 reference: relu(a @ w.T + b + r),
+    relu(a @ w.T + b), a @ w.T + b + r and a @ w.T + b, incl. a ragged pixel tail."""
+    from vosdetectron_amd import ops
+    monkeypatch.setenv("VOSDET_GEMM_MFMA", "1")
+    g = torch.Generator(device="cuda").manual_seed(K + N + M)
+    a = torch.randn(M, K, device="cuda", generator=g)
+    w = torch.randn(N, K, device="cuda", generator=g) / K ** .5
+    b = torch.randn(N, device="cuda", generator=g)
+    r = torch.randn(M, N, device="cuda", generator=g)
+    for res in (r, None):
+        for relu in (True, False):
+            ref = a @ w.t() + b + (res if res is not None else 0.)
+            if relu:
+                ref = torch.relu(ref)
+            got = ops.gemm_bias_act(a, w, b, residual=res, relu=relu)
+            tol = 2e-5 * max(1., float(ref.abs().max()))
+            assert float((got - ref).abs().max()) <= tol, (M, K, N, res is not None, relu)
+
+
 def test_bottleneck_gemm_path_matches_conv_path(monkeypatch):
     """A folded Bottleneck on channels_last input: the GEMM-epilogue path equals
     the MIOpen conv + vd_bias_act path within fp32 accumulation-order noise

@@ -20,6 +20,9 @@
 // the fastest (VOSDET_GEMM_SEARCH=0: the heuristic's first choice).  The
 // memory-bound bottleneck shapes (K = 64..256 with the residual) are where the
 // first choice is worst (tools/conv_roofline.py, profiles/r02_conv_roofline*).
+// For those shapes the search also times the hand-written MFMA kernel
+// (gemm1x1.hip) and keeps it when it is faster; VOSDET_GEMM_MFMA=1 forces it
+// (where supported), =0 excludes it.
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
 
@@ -45,6 +48,7 @@ struct Plan {
     hipblasLtMatmulAlgo_t algo;
     size_t ws = 0;
     bool ok = false, searched = false;
+    bool own = false;  // the hand-written MFMA kernel won the search
 };
 
 std::mutex g_mu;
@@ -101,13 +105,19 @@ bool search_enabled() {
     return !(e && e[0] == '0');
 }
 
+int own_mode() {  // -1: never, 0: when it wins the search, 1: always (where supported)
+    const char *e = getenv("VOSDET_GEMM_MFMA");
+    return !e ? 0 : (e[0] == '0' ? -1 : 1);
+}
+
 // Time every candidate on the caller's operands (D is overwritten by the real
 // launch that follows) and keep the fastest; any failure keeps the heuristic's
 // first choice.
-void search(Plan &p, const float *A, const float *W, const float *bias, const float *R, float *D,
-            void *ws, size_t ws_bytes, hipStream_t s) {
+void search(Plan &p, int M, int N, int K, int relu, const float *A, const float *W,
+            const float *bias, const float *R, float *D, void *ws, size_t ws_bytes, hipStream_t s) {
     p.searched = true;
-    if (p.ncand < 2 || !search_enabled()) return;
+    const bool try_own = own_mode() == 0 && gemm1x1_mfma_supported(K, N);
+    if ((p.ncand < 2 && !try_own) || !search_enabled()) return;
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return;
     hipEvent_t e0, e1;
@@ -138,10 +148,21 @@ void search(Plan &p, const float *A, const float *W, const float *bias, const fl
             best_i = i;
         }
     }
+    if (try_own && launch_gemm1x1_mfma(A, M, K, W, N, bias, R, relu, D, s) == VD_OK) {
+        bool ok = hipEventRecord(e0, s) == hipSuccess;
+        for (int r = 0; ok && r < kSearchReps; ++r)
+            ok = launch_gemm1x1_mfma(A, M, K, W, N, bias, R, relu, D, s) == VD_OK;
+        ok = ok && hipEventRecord(e1, s) == hipSuccess && hipEventSynchronize(e1) == hipSuccess;
+        float ms = 0.f;
+        if (ok && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms < best) {
+            best = ms;
+            p.own = true;
+        }
+    }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     (void)hipGetLastError();
-    if (best_i >= 0) {
+    if (best_i >= 0 && !p.own) {
         p.algo = p.cand[best_i].algo;
         p.ws = p.cand[best_i].workspaceSize;
     }
@@ -155,12 +176,16 @@ int launch_gemm_bias_act(const float *A, int M, int K, const float *W, int N, co
                          const float *R, int relu, float *D, void *ws, size_t ws_bytes,
                          hipStream_t s) {
     if (M == 0) return VD_OK;
+    const int mode = own_mode();
+    if (mode == 1 && gemm1x1_mfma_supported(K, N))
+        return launch_gemm1x1_mfma(A, M, K, W, N, bias, R, relu, D, s);
     std::lock_guard<std::mutex> lk(g_mu);
     Plan *p = plan_for(M, N, K, relu ? 1 : 0, R ? 1 : 0);
     if (!p) return VD_ERR_SHAPE;
     hipblasLtMatmulDescSetAttribute(p->op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias,
                                     sizeof(bias));
-    if (!p->searched) search(*p, A, W, bias, R, D, ws, ws_bytes, s);
+    if (!p->searched) search(*p, M, N, K, relu ? 1 : 0, A, W, bias, R, D, ws, ws_bytes, s);
+    if (p->own && mode == 0) return launch_gemm1x1_mfma(A, M, K, W, N, bias, R, relu, D, s);
     if (p->ws > ws_bytes || (p->ws && !ws)) return VD_ERR_WORKSPACE;
     const float alpha = 1.f, beta = R ? 1.f : 0.f;
     const hipblasStatus_t st =

@@ -33,6 +33,9 @@ size_t gemm_epi_workspace_bytes();
 int launch_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,
                          const float *R, int relu, float *D, void *ws, size_t ws_bytes,
                          hipStream_t s);
+bool gemm1x1_mfma_supported(int K, int N);
+int launch_gemm1x1_mfma(const float *A, int M, int K, const float *W, int N, const float *bias,
+                        const float *R, int relu, float *D, hipStream_t s);
 
 int launch_roi_align_legacy_fwd(const float *feat, int B, int C, int H, int W, const float *rois,
                                 int R, int PH, int PW, float scale, float *out, hipStream_t s);

@@ -413,7 +413,8 @@ _GEMM_WS = {}
 def gemm_bias_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
                   residual: Optional[torch.Tensor] = None, relu: bool = True,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """act(a @ w.T + bias (+ residual)) in one hipBLASLt GEMM (vd_gemm_bias_act):
+    """act(a @ w.T + bias (+ residual)) in one GEMM launch (vd_gemm_bias_act: hipBLASLt
+    with the epilogue fused, or the hand-written MFMA kernel where it is faster):
     a [M,K], w [N,K], bias [N], residual / out [M,N], all fp32 contiguous."""
     a_ = _need(a, "a")
     w_ = _need(w, "w")
