@@ -80,7 +80,7 @@ def test_gemm_bias_act_vs_torch():
         assert float((got2 - ref2).abs().max()) <= 2e-5 * max(1., float(ref2.abs().max()))
 
 
-@pytest.mark.parametrize("K,N", [(64, 256), (64, 64), (256, 64)])
+@pytest.mark.parametrize("K,N", [(64, 256), (64, 64), (256, 64), (128, 512)])
 @pytest.mark.parametrize("M", [4096, 1003, 16, 1])
 def test_gemm1x1_mfma_vs_torch(monkeypatch, K, N, M):
     """The hand-written MFMA 1x1-conv GEMM (csrc/gemm1x1.hip, forced with

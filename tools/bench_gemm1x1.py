@@ -18,7 +18,8 @@ SHAPES = [  # (M, K, N, residual): P2 / P3 bottleneck GEMMs of a 16-frame step
     (16 * 200 * 336, 64, 256, True),   # res2 conv3 + identity / downsample residual
     (16 * 200 * 336, 256, 64, False),  # res2 conv1 (blocks 1, 2)
     (16 * 200 * 336, 64, 64, False),   # res2 block 0 conv1
-    (16 * 200 * 336, 64, 256, False),  # res2 downsample (bias folded, no ReLU in the ref)
+    (16 * 200 * 336, 64, 256, False),  # res2 downsample shape
+    (16 * 100 * 168, 128, 512, True),  # res3 conv3 + residual (N split over 4 workgroups)
 ]
 
 
@@ -49,10 +50,10 @@ def main():
         flops = 2 * M * N * K
         outs = {}
         for mode in ("0", "1"):
-            os.environ["VOSDET_GEMM_MFMA"] = mode
+            os.environ["VOSDET_GEMM_MFMA"] = mode[0]
             us = timed(lambda: ops.gemm_bias_act(a, w, b, residual=r, relu=True, out=d))
             outs[mode] = d.clone()
-            key = "mfma" if mode == "1" else "hipblaslt"
+            key = {"0": "hipblaslt", "1": "mfma"}[mode]
             row[key + "_us"] = round(us, 1)
             row[key + "_hbm_frac"] = round(nbytes / (us * 1e-6) / HBM, 3)
             row[key + "_mfma_frac"] = round(flops / (us * 1e-6) / MFMA, 3)

@@ -41,13 +41,116 @@ namespace {
 
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-template <int K, int N, bool RES, bool RELU>
+
+// S > 1 splits the N output channels over S workgroups of the same XCD
+// (block b runs on XCD b % 8; the S splits of a pixel range are blocks
+// 8 (S w + s) + xcd), each staging an N / S-channel weight slice, so the
+// slices fit LDS and the pixel rows they share are read from one L2.
+template <int K, int NFULL, int S, bool RES, bool RELU>
 __global__ __launch_bounds__(512, 4) void gemm1x1_mfma_kernel(const float *__restrict__ A,
                                                            const float *__restrict__ W,
                                                            const float *__restrict__ bias,
                                                            const float *__restrict__ R,
                                                            float *__restrict__ D, int64_t M) {
-    constexpr int NT = N / 16, KB = K / 16;
+    constexpr int N = NFULL / S, NT = N / 16, KB = K / 16;
+    extern __shared__ __attribute__((aligned(16))) float4 wfrag[];  // [NT][KB][64] + bias[N]
+    float *bias_s = reinterpret_cast<float *>(wfrag + NT * KB * 64);
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int split = slot % S;
+    const int n0 = split * N;
+    const int64_t worker = (int64_t)(slot / S) * 8 + xcd, nworkers = gridDim.x / S;
+    for (int i = threadIdx.x; i < NT * KB * 64; i += blockDim.x) {
+        const int l = i & 63, tk = i >> 6;
+        const int t = tk / KB, kb = tk - t * KB;
+        wfrag[i] = *reinterpret_cast<const float4 *>(W + (int64_t)(n0 + 16 * t + (l & 15)) * K +
+                                                     16 * kb + 4 * (l >> 4));
+    }
+    for (int i = threadIdx.x; i < N; i += blockDim.x) bias_s[i] = bias ? bias[n0 + i] : 0.f;
+    __syncthreads();
+    const int lane = lane_id(), pj = lane & 15, q = lane >> 4;
+    const int64_t nblk = (M + 15) / 16;
+    const int64_t nw = nworkers * num_waves();
+    // the next block's inputs are loaded while this block's groups run
+    auto load_x = [&](int64_t blk, float4 (&x)[KB]) {
+        const int64_t p = min(blk * 16 + pj, M - 1);
+        const float *ap = A + p * K + 4 * q;
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) x[kb] = *reinterpret_cast<const float4 *>(ap + 16 * kb);
+    };
+    int64_t blk = worker * num_waves() + wave_id();
+    float4 x[KB];
+    if (blk < nblk) load_x(blk, x);
+    for (; blk < nblk; blk += nw) {
+        int64_t p = blk * 16 + pj;
+        const bool live = p < M;
+        if (!live) p = M - 1;  // tail lanes compute on a valid pixel; their stores are dropped
+        float4 xn[KB];
+        if (blk + nw < nblk) load_x(blk + nw, xn);
+        const int64_t orow = p * NFULL + n0 + 4 * q;
+        // channel tiles in groups of G: a group's residual / output float4s of a
+        // pixel are G x 64 contiguous bytes touched by back-to-back instructions
+        // (whole 128-byte lines while they are in L2); the next group's residual
+        // is loaded while this group's MFMAs run
+        constexpr int G = (NT >= 8 && K <= 64) ? 4 : (NT >= 2 ? 2 : 1), NG = NT / G;
+        float4 r[G], rn[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u)
+            r[u] = RES ? *reinterpret_cast<const float4 *>(R + orow + 16 * u)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+        for (int g = 0; g < NG; ++g) {
+#pragma unroll
+            for (int u = 0; u < G; ++u)
+                rn[u] = (RES && g + 1 < NG)
+                            ? *reinterpret_cast<const float4 *>(R + orow + 16 * (G * (g + 1) + u))
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+            f4v acc[G];
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                acc[u] = f4v{0.f, 0.f, 0.f, 0.f};
+                const float4 *wt = wfrag + (G * g + u) * KB * 64 + lane;
+#pragma unroll
+                for (int kb = 0; kb < KB; ++kb) {
+                    const float4 w = wt[kb * 64];
+                    acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, x[kb].x, acc[u], 0, 0, 0);
+                    acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, x[kb].y, acc[u], 0, 0, 0);
+                    acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, x[kb].z, acc[u], 0, 0, 0);
+                    acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, x[kb].w, acc[u], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                const int t = G * g + u;
+                const float4 b = *reinterpret_cast<const float4 *>(bias_s + 16 * t + 4 * q);
+                float4 o = make_float4(acc[u][0] + b.x + r[u].x, acc[u][1] + b.y + r[u].y,
+                                       acc[u][2] + b.z + r[u].z, acc[u][3] + b.w + r[u].w);
+                if (RELU) {
+                    o.x = fmaxf(o.x, 0.f);
+                    o.y = fmaxf(o.y, 0.f);
+                    o.z = fmaxf(o.z, 0.f);
+                    o.w = fmaxf(o.w, 0.f);
+                }
+                if (live) *reinterpret_cast<float4 *>(D + orow + 16 * t) = o;
+                r[u] = rn[u];
+            }
+        }
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) x[kb] = xn[kb];
+    }
+}
+
+// K >= 128: the K axis is walked in chunks of 64 input channels with the
+// accumulators of all N / 16 tiles live (N <= 128), the next chunk's (or the
+// next block's first chunk's) inputs loaded while the current chunk's MFMAs
+// run -- a flattened (block, chunk) loop, so the prefetch crosses blocks.
+template <int K, int N, bool RES, bool RELU>
+__global__ __launch_bounds__(512) void gemm1x1_mfma_chunk_kernel(const float *__restrict__ A,
+                                                                 const float *__restrict__ W,
+                                                                 const float *__restrict__ bias,
+                                                                 const float *__restrict__ R,
+                                                                 float *__restrict__ D, int64_t M) {
+    constexpr int NT = N / 16, KB = K / 16, CH = 4, NCH = KB / CH;
+    static_assert(KB % CH == 0 && NT <= 8, "chunked shape");
     extern __shared__ __attribute__((aligned(16))) float4 wfrag[];  // [NT][KB][64] + bias[N]
     float *bias_s = reinterpret_cast<float *>(wfrag + NT * KB * 64);
     for (int i = threadIdx.x; i < NT * KB * 64; i += blockDim.x) {
@@ -61,67 +164,93 @@ __global__ __launch_bounds__(512, 4) void gemm1x1_mfma_kernel(const float *__res
     const int lane = lane_id(), pj = lane & 15, q = lane >> 4;
     const int64_t nblk = (M + 15) / 16;
     const int64_t nw = (int64_t)gridDim.x * num_waves();
-    for (int64_t blk = (int64_t)blockIdx.x * num_waves() + wave_id(); blk < nblk; blk += nw) {
-        int64_t p = blk * 16 + pj;
-        const bool live = p < M;
-        if (!live) p = M - 1;  // tail lanes compute on a valid pixel; their stores are dropped
-        const float *ap = A + p * K + 4 * q;
-        float4 x[KB];
+    const int64_t blk0 = (int64_t)blockIdx.x * num_waves() + wave_id();
+    if (blk0 >= nblk) return;
+    const int64_t nmine = (nblk - blk0 + nw - 1) / nw;  // blocks this wave walks
+    auto pixel = [&](int64_t blk) {
+        const int64_t p = blk * 16 + pj;
+        return p < M ? p : M - 1;  // tail lanes compute on a valid pixel; stores dropped
+    };
+    auto load_chunk = [&](int64_t blk, int c, float4 (&x)[CH]) {
+        const float *ap = A + pixel(blk) * K + 64 * c + 4 * q;
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) x[kb] = *reinterpret_cast<const float4 *>(ap + 16 * kb);
-        const int64_t orow = p * N + 4 * q;
-        // the residual of tile t + 1 is loaded while tile t's MFMAs run
-        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (RES) r = *reinterpret_cast<const float4 *>(R + orow);
+        for (int kb = 0; kb < CH; ++kb) x[kb] = *reinterpret_cast<const float4 *>(ap + 16 * kb);
+    };
+    float4 xc[CH];
+    load_chunk(blk0, 0, xc);
+    f4v acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
+    const int64_t steps = nmine * NCH;
 #pragma unroll 1
-        for (int t = 0; t < NT; ++t) {
-            float4 rn = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (RES && t + 1 < NT) rn = *reinterpret_cast<const float4 *>(R + orow + 16 * (t + 1));
-            f4v acc = {0.f, 0.f, 0.f, 0.f};
-            const float4 *wt = wfrag + t * KB * 64 + lane;
+    for (int64_t st = 0; st < steps; ++st) {
+        const int64_t blk = blk0 + (st / NCH) * nw;
+        const int c = (int)(st % NCH);
+        float4 xn[CH];
+        if (st + 1 < steps)
+            load_chunk(blk0 + ((st + 1) / NCH) * nw, (int)((st + 1) % NCH), xn);
 #pragma unroll
-            for (int kb = 0; kb < KB; ++kb) {
+        for (int t = 0; t < NT; ++t) {
+            const float4 *wt = wfrag + (t * KB + c * CH) * 64 + lane;
+#pragma unroll
+            for (int kb = 0; kb < CH; ++kb) {
                 const float4 w = wt[kb * 64];
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, x[kb].x, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, x[kb].y, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, x[kb].z, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, x[kb].w, acc, 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, xc[kb].x, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, xc[kb].y, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, xc[kb].z, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, xc[kb].w, acc[t], 0, 0, 0);
             }
-            const float4 b = *reinterpret_cast<const float4 *>(bias_s + 16 * t + 4 * q);
-            float4 o = make_float4(acc[0] + b.x, acc[1] + b.y, acc[2] + b.z, acc[3] + b.w);
-            if (RES) {
-                o.x += r.x;
-                o.y += r.y;
-                o.z += r.z;
-                o.w += r.w;
-                r = rn;
-            }
-            if (RELU) {
-                o.x = fmaxf(o.x, 0.f);
-                o.y = fmaxf(o.y, 0.f);
-                o.z = fmaxf(o.z, 0.f);
-                o.w = fmaxf(o.w, 0.f);
-            }
-            if (live) *reinterpret_cast<float4 *>(D + orow + 16 * t) = o;
         }
+        if (c == NCH - 1) {
+            const int64_t p = blk * 16 + pj;
+            const int64_t orow = pixel(blk) * N + 4 * q;
+            float4 r[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+                r[t] = RES ? *reinterpret_cast<const float4 *>(R + orow + 16 * t)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const float4 b = *reinterpret_cast<const float4 *>(bias_s + 16 * t + 4 * q);
+                float4 o = make_float4(acc[t][0] + b.x + r[t].x, acc[t][1] + b.y + r[t].y,
+                                       acc[t][2] + b.z + r[t].z, acc[t][3] + b.w + r[t].w);
+                if (RELU) {
+                    o.x = fmaxf(o.x, 0.f);
+                    o.y = fmaxf(o.y, 0.f);
+                    o.z = fmaxf(o.z, 0.f);
+                    o.w = fmaxf(o.w, 0.f);
+                }
+                if (p < M) *reinterpret_cast<float4 *>(D + orow + 16 * t) = o;
+                acc[t] = f4v{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+#pragma unroll
+        for (int kb = 0; kb < CH; ++kb) xc[kb] = xn[kb];
     }
 }
 
-template <int K, int N, bool RES, bool RELU>
+template <int K, int N, int S, bool RES, bool RELU>
 int launch_shape(const float *A, int64_t M, const float *W, const float *bias, const float *R,
                  float *D, hipStream_t s) {
-    constexpr size_t lds = (size_t)N * K * 4 + (size_t)N * 4;
+    constexpr size_t lds = (size_t)(N / S) * K * 4 + (size_t)(N / S) * 4;
     static_assert(lds <= 80 * 1024, "two workgroups per CU");
-    auto kern = gemm1x1_mfma_kernel<K, N, RES, RELU>;
-    static bool attr = [&] {
-        return hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)lds) == hipSuccess;
-    }();
+    constexpr bool chunked = K >= 128 && S == 1;
+    void (*kern)(const float *, const float *, const float *, const float *, float *, int64_t);
+    if constexpr (chunked)
+        kern = gemm1x1_mfma_chunk_kernel<K, N, RES, RELU>;
+    else
+        kern = gemm1x1_mfma_kernel<K, N, S, RES, RELU>;
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)lds) == hipSuccess;
     if (!attr) return VD_ERR_LAUNCH;
+    // persistent: 2 workgroups of 8 waves per CU (LDS: a weight slice + bias each);
+    // a multiple of 8 * S blocks so every split of every XCD exists
     const int64_t blocks16 = (M + 15) / 16;
-    int64_t grid = 256 * 2;  // persistent: 2 workgroups (16 waves) per CU
-    if (grid * 8 > blocks16) grid = (blocks16 + 7) / 8;
+    int64_t grid = 256 * 2;
+    const int64_t need = (blocks16 + 7) / 8 * S;
+    if (grid > need) grid = need;
+    grid = (grid + 8 * S - 1) / (8 * S) * (8 * S);
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), lds, s, A, W, bias, R, D, M);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
@@ -129,22 +258,23 @@ int launch_shape(const float *A, int64_t M, const float *W, const float *bias, c
 }  // namespace
 
 bool gemm1x1_mfma_supported(int K, int N) {
-    return (K == 64 && (N == 64 || N == 256)) || (K == 256 && N == 64);
+    return (K == 64 && (N == 64 || N == 256)) || (K == 256 && N == 64) || (K == 128 && N == 512);
 }
 
 int launch_gemm1x1_mfma(const float *A, int M, int K, const float *W, int N, const float *bias,
                         const float *R, int relu, float *D, hipStream_t s) {
     if (M == 0) return VD_OK;
-#define VD_G1(KK, NN)                                                                     \
+#define VD_G1(KK, NN, SS)                                                                 \
     if (K == KK && N == NN) {                                                             \
-        if (R) return relu ? launch_shape<KK, NN, true, true>(A, M, W, bias, R, D, s)     \
-                           : launch_shape<KK, NN, true, false>(A, M, W, bias, R, D, s);   \
-        return relu ? launch_shape<KK, NN, false, true>(A, M, W, bias, R, D, s)           \
-                    : launch_shape<KK, NN, false, false>(A, M, W, bias, R, D, s);         \
+        if (R) return relu ? launch_shape<KK, NN, SS, true, true>(A, M, W, bias, R, D, s) \
+                           : launch_shape<KK, NN, SS, true, false>(A, M, W, bias, R, D, s); \
+        return relu ? launch_shape<KK, NN, SS, false, true>(A, M, W, bias, R, D, s)       \
+                    : launch_shape<KK, NN, SS, false, false>(A, M, W, bias, R, D, s);     \
     }
-    VD_G1(64, 256)
-    VD_G1(64, 64)
-    VD_G1(256, 64)
+    VD_G1(64, 256, 1)
+    VD_G1(64, 64, 1)
+    VD_G1(256, 64, 1)
+    VD_G1(128, 512, 4)
 #undef VD_G1
     return VD_ERR_SHAPE;
 }
