@@ -127,6 +127,18 @@ int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const 
                      const float *residual, int relu, float *D, void *workspace,
                      size_t workspace_bytes, void *stream);
 
+/* Two 1x1 convolutions of two channels_last inputs summed, with the epilogue:
+ * D[M][N] = act(A1[M][K1] . W[:, :K1]^T + A2[M][K2] . W[:, K1:]^T + bias[N]),
+ * W = [W1 | W2] as N x (K1 + K2) row-major.  With A1 = the bottleneck's conv2
+ * output, A2 = the block input, W = [W3 | Wdownsample] and bias = b3 + bd, this
+ * is a ResNet stage's first block tail (ResNet.py:246-294 with the stride-1
+ * basic_bn_shortcut, :195-205) without the downsample tensor's HBM round trip.
+ * One hand-written MFMA kernel (K1 = K2 = 64, N = 256: res2 of the R-50/R-101
+ * FPN bodies); other shapes return VD_ERR_SHAPE (callers use vd_gemm_bias_act
+ * with the downsample output as the residual). */
+int vd_gemm_dual_bias_act(const float *A1, int K1, const float *A2, int K2, int M, const float *W,
+                          int N, const float *bias, int relu, float *D, void *stream);
+
 /* ---------------------------------------------------------------------------
  * NMS with the semantics of the NMS the reference executes,
  * utils.boxes.nms -> cython_nms.nms (lib/utils/boxes.py:329-333,

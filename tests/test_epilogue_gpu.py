@@ -103,6 +103,26 @@ def test_gemm1x1_mfma_vs_torch(monkeypatch, K, N, M):
             assert float((got - ref).abs().max()) <= tol, (M, K, N, res is not None, relu)
 
 
+@pytest.mark.parametrize("M", [4096, 1003, 1])
+def test_gemm_dual_vs_torch(M):
+    """vd_gemm_dual_bias_act (conv3 + stride-1 downsample as one two-operand MFMA
+    GEMM) vs torch fp32: relu(a1 @ w[:, :64].T + a2 @ w[:, 64:].T + b); shapes the
+    kernel does not serve return None (the caller falls back)."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(M)
+    a1 = torch.randn(M, 64, device="cuda", generator=g)
+    a2 = torch.randn(M, 64, device="cuda", generator=g)
+    w = torch.randn(256, 128, device="cuda", generator=g) / 128 ** .5
+    b = torch.randn(256, device="cuda", generator=g)
+    for relu in (True, False):
+        ref = a1 @ w[:, :64].t() + a2 @ w[:, 64:].t() + b
+        if relu:
+            ref = torch.relu(ref)
+        got = ops.gemm_dual_bias_act(a1, a2, w, b, relu=relu)
+        assert float((got - ref).abs().max()) <= 2e-5 * max(1., float(ref.abs().max()))
+    assert ops.gemm_dual_bias_act(a1, a2[:, :32].contiguous(), w[:, :96].contiguous(), b) is None
+
+
 def test_bottleneck_gemm_path_matches_conv_path(monkeypatch):
     """A folded Bottleneck on channels_last input: the GEMM-epilogue path equals
     the MIOpen conv + vd_bias_act path within fp32 accumulation-order noise

@@ -63,6 +63,29 @@ def main():
         print(json.dumps(row), flush=True)
         del a, w, b, r, d, outs
         torch.cuda.empty_cache()
+    # res2 block 0 tail: MIOpen downsample conv + GEMM with that residual vs the
+    # two-operand MFMA GEMM (conv3 + downsample summed in the accumulators)
+    import torch.nn.functional as F
+    M = 16 * 200 * 336
+    h = torch.randn(M, 64, device="cuda", generator=g)
+    x = torch.randn(16, 64, 200, 336, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    x2 = x.permute(0, 2, 3, 1).reshape(M, 64)
+    w3 = torch.randn(256, 64, device="cuda", generator=g) / 8
+    wd = torch.randn(256, 64, device="cuda", generator=g) / 8
+    b = torch.randn(256, device="cuda", generator=g)
+    wcat = torch.cat([w3, wd], 1).contiguous()
+    d = torch.empty(M, 256, device="cuda")
+
+    def two_step():
+        r = F.conv2d(x, wd.view(256, 64, 1, 1)).permute(0, 2, 3, 1).reshape(M, 256)
+        ops.gemm_bias_act(h, w3, b, residual=r, relu=True, out=d)
+    row = {"what": "res2 block-0 tail (16 frames)", "downsample_conv_plus_gemm_us":
+           round(timed(two_step), 1),
+           "dual_mfma_us": round(timed(lambda: ops.gemm_dual_bias_act(h, x2, wcat, b, out=d)),
+                                 1)}
+    print(json.dumps(row), flush=True)
+    rows.append(row)
     if len(sys.argv) > 1:
         json.dump(rows, open(sys.argv[1], "w"), indent=1)
 

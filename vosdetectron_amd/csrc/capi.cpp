@@ -100,6 +100,13 @@ int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const 
                                 workspace_bytes, VD_STREAM(stream));
 }
 
+int vd_gemm_dual_bias_act(const float *A1, int K1, const float *A2, int K2, int M, const float *W,
+                          int N, const float *bias, int relu, float *D, void *stream) {
+    if (M < 0 || K1 < 1 || K2 < 1 || N < 1 || !W || !bias || !D || (M > 0 && (!A1 || !A2)))
+        return VD_ERR_ARG;
+    return launch_gemm1x1_dual(A1, K1, A2, K2, M, W, N, bias, relu, D, VD_STREAM(stream));
+}
+
 int vd_roi_align_legacy_forward(int ah, int aw, float spatial_scale, const float *features,
                                 int B, int C, int H, int W, const float *rois, int num_rois,
                                 float *output, void *stream) {

@@ -46,8 +46,15 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 // (block b runs on XCD b % 8; the S splits of a pixel range are blocks
 // 8 (S w + s) + xcd), each staging an N / S-channel weight slice, so the
 // slices fit LDS and the pixel rows they share are read from one L2.
-template <int K, int NFULL, int S, bool RES, bool RELU>
+//
+// K2 > 0: a second input operand A2 [M][K2] contributes the last K2 of the K
+// input channels (W = [W1 | W2], K = K1 + K2): the ResNet stage's first block
+// as ONE kernel, conv3 and the stride-1 downsample of the block input summed
+// in the accumulators -- relu(h W3^T + x Wd^T + b3 + bd) -- instead of the
+// downsample conv's output written and read back as the residual.
+template <int K, int K2, int NFULL, int S, bool RES, bool RELU>
 __global__ __launch_bounds__(512, 4) void gemm1x1_mfma_kernel(const float *__restrict__ A,
+                                                           const float *__restrict__ A2,
                                                            const float *__restrict__ W,
                                                            const float *__restrict__ bias,
                                                            const float *__restrict__ R,
@@ -71,11 +78,15 @@ __global__ __launch_bounds__(512, 4) void gemm1x1_mfma_kernel(const float *__res
     const int64_t nblk = (M + 15) / 16;
     const int64_t nw = nworkers * num_waves();
     // the next block's inputs are loaded while this block's groups run
+    constexpr int K1 = K - K2, KB1 = K1 / 16;
     auto load_x = [&](int64_t blk, float4 (&x)[KB]) {
         const int64_t p = min(blk * 16 + pj, M - 1);
-        const float *ap = A + p * K + 4 * q;
+        const float *ap = A + p * K1 + 4 * q;
+        const float *ap2 = A2 + p * K2 + 4 * q;
 #pragma unroll
-        for (int kb = 0; kb < KB; ++kb) x[kb] = *reinterpret_cast<const float4 *>(ap + 16 * kb);
+        for (int kb = 0; kb < KB; ++kb)
+            x[kb] = kb < KB1 ? *reinterpret_cast<const float4 *>(ap + 16 * kb)
+                             : *reinterpret_cast<const float4 *>(ap2 + 16 * (kb - KB1));
     };
     int64_t blk = worker * num_waves() + wave_id();
     float4 x[KB];
@@ -145,6 +156,7 @@ __global__ __launch_bounds__(512, 4) void gemm1x1_mfma_kernel(const float *__res
 // run -- a flattened (block, chunk) loop, so the prefetch crosses blocks.
 template <int K, int N, bool RES, bool RELU>
 __global__ __launch_bounds__(512) void gemm1x1_mfma_chunk_kernel(const float *__restrict__ A,
+                                                                 const float *__restrict__,
                                                                  const float *__restrict__ W,
                                                                  const float *__restrict__ bias,
                                                                  const float *__restrict__ R,
@@ -229,17 +241,18 @@ __global__ __launch_bounds__(512) void gemm1x1_mfma_chunk_kernel(const float *__
     }
 }
 
-template <int K, int N, int S, bool RES, bool RELU>
+template <int K, int N, int S, bool RES, bool RELU, int K2 = 0>
 int launch_shape(const float *A, int64_t M, const float *W, const float *bias, const float *R,
-                 float *D, hipStream_t s) {
+                 float *D, hipStream_t s, const float *A2 = nullptr) {
     constexpr size_t lds = (size_t)(N / S) * K * 4 + (size_t)(N / S) * 4;
     static_assert(lds <= 80 * 1024, "two workgroups per CU");
-    constexpr bool chunked = K >= 128 && S == 1;
-    void (*kern)(const float *, const float *, const float *, const float *, float *, int64_t);
+    constexpr bool chunked = K >= 128 && S == 1 && K2 == 0;
+    void (*kern)(const float *, const float *, const float *, const float *, const float *,
+                 float *, int64_t);
     if constexpr (chunked)
         kern = gemm1x1_mfma_chunk_kernel<K, N, RES, RELU>;
     else
-        kern = gemm1x1_mfma_kernel<K, N, S, RES, RELU>;
+        kern = gemm1x1_mfma_kernel<K, K2, N, S, RES, RELU>;
     static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  (int)lds) == hipSuccess;
@@ -251,7 +264,7 @@ int launch_shape(const float *A, int64_t M, const float *W, const float *bias, c
     const int64_t need = (blocks16 + 7) / 8 * S;
     if (grid > need) grid = need;
     grid = (grid + 8 * S - 1) / (8 * S) * (8 * S);
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), lds, s, A, W, bias, R, D, M);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), lds, s, A, A2, W, bias, R, D, M);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
@@ -277,6 +290,16 @@ int launch_gemm1x1_mfma(const float *A, int M, int K, const float *W, int N, con
     VD_G1(128, 512, 4)
 #undef VD_G1
     return VD_ERR_SHAPE;
+}
+
+bool gemm1x1_dual_supported(int K1, int K2, int N) { return K1 == 64 && K2 == 64 && N == 256; }
+
+int launch_gemm1x1_dual(const float *A1, int K1, const float *A2, int K2, int M, const float *W,
+                        int N, const float *bias, int relu, float *D, hipStream_t s) {
+    if (M == 0) return VD_OK;
+    if (!gemm1x1_dual_supported(K1, K2, N)) return VD_ERR_SHAPE;
+    return relu ? launch_shape<128, 256, 2, false, true, 64>(A1, M, W, bias, nullptr, D, s, A2)
+                : launch_shape<128, 256, 2, false, false, 64>(A1, M, W, bias, nullptr, D, s, A2);
 }
 
 }  // namespace vd

@@ -113,6 +113,12 @@ class Bottleneck(nn.Module):
             out = _conv_epi(self.f1, x)
         out = _conv_epi(self.f2, out)
         if self.downsample is not None:
+            if self.fd.stride == (1, 1) and x.is_contiguous(memory_format=torch.channels_last):
+                # conv3 and the stride-1 downsample as one two-operand MFMA GEMM
+                N, _, H, W = out.shape
+                y = ops.gemm_dual_bias_act(_nhwc2d(out), _nhwc2d(x), self.w3d, self.b3d)
+                if y is not None:
+                    return y.view(N, H, W, -1).permute(0, 3, 1, 2)
             return _gemm_conv1x1(out, self.w3, self.b3d, relu=True, res=_conv_nb(self.fd, x))
         return _gemm_conv1x1(out, self.w3, self.f3.bias, relu=True, res=x)
 
@@ -739,6 +745,9 @@ def prepare_bottlenecks(blocks, epilogue: bool = True):
             # 2-D weights of the 1x1 convs for the GEMM epilogue path
             blk.w1 = blk.f1.weight.reshape(blk.f1.out_channels, -1).contiguous()
             blk.w3 = blk.f3.weight.reshape(blk.f3.out_channels, -1).contiguous()
+            if blk.downsample is not None:  # [W3 | Wd] for the two-operand GEMM
+                blk.w3d = torch.cat([blk.w3, blk.fd.weight.reshape(blk.fd.out_channels, -1)],
+                                    1).contiguous()
             blk.fused = True
         blk.epilogue = epilogue
 

@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import check, lib
+from ._lib import VD_ERR_SHAPE, check, lib
 
 
 def _stream() -> int:
@@ -441,6 +441,31 @@ def gemm_bias_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
                                  r_.data_ptr() if r_ is not None else None, int(relu),
                                  out.data_ptr(), ws.data_ptr(), ws.numel(), _stream()),
           "vd_gemm_bias_act")
+    return out
+
+
+def gemm_dual_bias_act(a1: torch.Tensor, a2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
+                       relu: bool = True, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """act(a1 @ w[:, :K1].T + a2 @ w[:, K1:].T + bias) in one MFMA kernel
+    (vd_gemm_dual_bias_act): a1 [M,K1], a2 [M,K2], w [N,K1+K2], bias [N].
+    Returns None for a shape the kernel does not serve (the caller falls back)."""
+    a1_, a2_ = _need(a1, "a1"), _need(a2, "a2")
+    w_, b_ = _need(w, "w"), _need(bias, "bias")
+    M, K1 = a1_.shape
+    K2 = a2_.shape[1]
+    N = w_.shape[0]
+    if a2_.shape[0] != M or w_.shape[1] != K1 + K2 or b_.numel() != N:
+        raise ValueError("gemm_dual_bias_act: a1 %s, a2 %s, w %s, bias %s"
+                         % (tuple(a1_.shape), tuple(a2_.shape), tuple(w_.shape), tuple(b_.shape)))
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a1_.device)
+    elif tuple(out.shape) != (M, N) or not out.is_contiguous():
+        raise ValueError("out must be a contiguous %s tensor" % ((M, N),))
+    st = lib().vd_gemm_dual_bias_act(a1_.data_ptr(), K1, a2_.data_ptr(), K2, M, w_.data_ptr(), N,
+                                     b_.data_ptr(), int(relu), out.data_ptr(), _stream())
+    if st == VD_ERR_SHAPE:
+        return None
+    check(st, "vd_gemm_dual_bias_act")
     return out
 
 
