@@ -5,10 +5,11 @@ the reference CPU path timed on the host.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch F]
 
-One process per GPU (torchrun for N>1, RCCL).  A step = every rank runs the full
-per-frame hot path on its own F frames (already resident in HBM as u8), then one
-all_gather of the fixed-size padded detections + masks collects every rank's
-results (weak scaling: per-GPU work is fixed).  Rank 0 prints ONE JSON line.
+One process per GPU (torchrun for N>1, RCCL).  A step = every rank uploads its own
+F u8 frames from pinned host memory (side stream, inside the timed region) and runs
+the full per-frame hot path on them, then one all_gather of the packed detections +
+masks collects every rank's results (weak scaling: per-GPU work is fixed).  Rank 0
+prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -638,13 +639,15 @@ def main():
         roof = measure_roialign_roofline(dev)
         if not vos and cfg.FPN.FPN_ON:
             roof["engine_launch"] = measure_pipeline_roialign(pipe, any_frames)
+    if not args.no_roofline and rank == 0 and world == 1:  # N=1 line only (no ranks waiting)
         extra["hbm_copy"] = measure_hbm_copy(dev)
         nthr = torch.get_num_threads()
         torch.set_num_threads(cpu_share()[0])
         flops, dets_cpu = frame_flops(sd, cfg)
         torch.set_num_threads(nthr)
         extra["step_roofline"] = step_roofline(
-            flops, dets_cpu, F, dt / args.steps * 1e3, roof.get("engine_launch"), (fh, fw),
+            flops, dets_cpu, F, dt / args.steps * 1e3, roof.get("engine_launch") if roof else None,
+            (fh, fw),
             (getattr(pipe, "Hp", fh), getattr(pipe, "Wp", fw)))
     cpu = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:

@@ -14,6 +14,11 @@ timeout -k 10 600 python -u bench.py > $O/bench_default.json 2> $O/bench_default
 tail -c 300 $O/bench_default.json; echo
 exit 0
 fi
+if [ "${PART}" = 3 ]; then  # N-rank rehearsal on the one-GPU box (gloo collectives)
+timeout -k 10 600 python -u bench.py --gpus 2 --share-gpu --steps 4 --warmup 2 --no-cpu-baseline > $O/bench_share2.json 2> $O/bench_share2.err || { echo share2 failed; tail -5 $O/bench_share2.err; exit 1; }
+tail -c 400 $O/bench_share2.json; echo
+exit 0
+fi
 for c in e2e_mask_rcnn_R-101-FPN_2x e2e_mask_rcnn_X-101-32x8d-FPN_1x e2e_mask_rcnn_R-50-C4_1x vos_R-101-FPN_3x_gn_dynamic_davis; do
   timeout -k 10 400 python -u bench.py --config $c --batch 8 --steps 5 --no-cpu-baseline --no-roofline > $O/bench_$c.json 2> $O/bench_$c.err || { echo "bench $c failed"; tail -3 $O/bench_$c.err; exit 1; }
   python3 -c "import json,sys; d=json.loads(open('$O/bench_$c.json').read().strip().splitlines()[-1]); print('$c', d['value'], d['ms_per_step'])"
