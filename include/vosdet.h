@@ -127,6 +127,17 @@ int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const 
                      const float *residual, int relu, float *D, void *workspace,
                      size_t workspace_bytes, void *stream);
 
+/* 3x3 stride-1 pad-1 convolution of a channels_last (NHWC) fp32 tensor with
+ * the bias (+ ReLU) epilogue fused, one hand-written MFMA implicit-GEMM kernel:
+ * Y[n][y][x][co] = act(sum_{ky,kx,ci} X[n][y+ky-1][x+kx-1][ci] W2[co][ky][kx][ci]
+ * + bias[co]), out-of-image taps zero.  W2 is the PyTorch weight [Cout][Cin][3][3]
+ * permuted to [Cout][3][3][Cin].  bias may be NULL.  The FPN posthoc convs
+ * (lib/modeling/FPN.py:227-258), the RPN conv (FPN.py:376-422) and the mask head
+ * convs (mask_rcnn_heads.py:178-188) run in PyTorch in the reference.
+ * Requires Cin % 64 == 0 and Cout % 128 == 0 (VD_ERR_SHAPE otherwise). */
+int vd_conv3x3_bias_act(const float *X, int N, int H, int W, int C, const float *W2, int Cout,
+                        const float *bias, int relu, float *Y, void *stream);
+
 /* Two 1x1 convolutions of two channels_last inputs summed, with the epilogue:
  * D[M][N] = act(A1[M][K1] . W[:, :K1]^T + A2[M][K2] . W[:, K1:]^T + bias[N]),
  * W = [W1 | W2] as N x (K1 + K2) row-major.  With A1 = the bottleneck's conv2

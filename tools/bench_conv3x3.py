@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""A/B of the 256 -> 256 3x3 convolutions of a 16-frame R-50-FPN step: the
+hand-written MFMA implicit GEMM with the bias (+ReLU) epilogue (csrc/conv3x3.hip)
+vs what the engine runs today (MIOpen conv without bias + vd_bias_act).  HIP
+events; fraction of the 157.3 TF/s fp32 matrix peak.  usage: tools/bench_conv3x3.py [out.json]"""
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vosdetectron_amd import ops  # noqa: E402
+
+PEAK = 157.3e12
+SHAPES = [(16, 256, 200, 336), (16, 256, 100, 168), (16, 256, 50, 84), (1600, 256, 14, 14),
+          (16, 256, 25, 42)]
+
+
+def timed(fn, iters=10):
+    s = torch.cuda.current_stream()
+    for _ in range(2):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        fn()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3
+
+
+def main():
+    torch.backends.cudnn.benchmark = True
+    rows = []
+    for N, C, H, W in SHAPES:
+        x = torch.randn(N, C, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
+        w = (torch.randn(C, C, 3, 3, device="cuda") / (9 * C) ** .5).contiguous(
+            memory_format=torch.channels_last)
+        b = torch.randn(C, device="cuda")
+        w2 = ops.conv3x3_weight(w)
+        y = torch.empty_like(x)
+        flops = 2 * N * H * W * C * C * 9
+        t_ref = timed(lambda: ops.bias_act_(F.conv2d(x, w, None, padding=1), b, relu=True))
+        t_own = timed(lambda: ops.conv3x3_bias_act(x, w2, b, relu=True, out=y))
+        ref = ops.bias_act_(F.conv2d(x, w, None, padding=1), b, relu=True)
+        row = {"shape": [N, C, H, W], "miopen_plus_bias_act_us": round(t_ref, 1),
+               "mfma_us": round(t_own, 1), "mfma_frac": round(flops / (t_own * 1e-6) / PEAK, 3),
+               "miopen_frac": round(flops / (t_ref * 1e-6) / PEAK, 3),
+               "maxdiff": float((y - ref).abs().max())}
+        print(json.dumps(row), flush=True)
+        rows.append(row)
+        del x, y, ref
+        torch.cuda.empty_cache()
+    if len(sys.argv) > 1:
+        json.dump(rows, open(sys.argv[1], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,228 @@
+// 3x3 stride-1 pad-1 convolution on NHWC fp32 as an MFMA implicit GEMM with the
+// bias (+ ReLU) epilogue fused.
+//
+// The 256 -> 256 3x3 convolutions are half of a Mask R-CNN step: FPN posthoc
+// (lib/modeling/FPN.py:227-258, conv + bias), the RPN conv (FPN.py:376-422),
+// the mask head's four convs (mask_rcnn_heads.py:178-188, conv + bias + ReLU)
+// and res4's conv2.  Implicit GEMM:
+//   D[m][co] = sum_{t = (ky,kx), ci} X[pixel m shifted by (ky-1, kx-1)][ci] . W2[co][t][ci]
+// with out-of-image taps reading zero; W2 = the weight permuted to
+// [Cout][3][3][Cin] once on the host side (k = 9 taps x Cin contiguous per co).
+//
+// Tiling: a workgroup (4 waves, one per SIMD) computes 128 pixels x 128 output
+// channels; wave w owns 64 x 64 (pixels (w & 1) * 64, channels (w >> 1) * 64)
+// as 4 x 4 tiles of v_mfma_f32_16x16x4_f32 in the transposed orientation (MFMA
+// A operand = weights, B operand = pixels), so each lane's accumulators are 4
+// consecutive output channels of one pixel and the epilogue stores float4s.
+// The K axis (9 x Cin) is walked in chunks of 64 input channels of one tap:
+// the chunk's pixel rows (128 x 256 B) and weight rows (128 x 256 B) are
+// staged in LDS, 16-byte chunk c of row r at c ^ (r & 15) so every fragment
+// read (lane = row, 4 lanes per 64 contiguous bytes) is a conflict-free
+// ds_read_b128; the next chunk's global loads are in flight while the current
+// chunk's 256 MFMAs per wave run; one LDS stage per workgroup and two
+// workgroups per CU, so one's store phase overlaps the other's MFMAs.
+// Per 16 input channels (kb) a lane holds channels 16 kb + 4 q .. + 3 (q = lane
+// / 16) of its row in both operands: a K permutation shared by A and B.
+#include <stdlib.h>
+
+#include "common.hpp"
+#include "vosdet_internal.hpp"
+
+namespace vd {
+
+namespace {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+constexpr int kTM = 128, kTN = 128, kKC = 64;  // tile: pixels x channels, K chunk
+constexpr int kRowF4 = kKC / 4;                // float4s per staged row (16)
+constexpr int kStageF4 = (kTM + kTN) * kRowF4; // float4s per LDS stage
+
+template <bool RELU>
+__global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
+    const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ W2,
+    int Cout, const float *__restrict__ bias, float *__restrict__ Y, int mtiles) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds[];  // [kTM + kTN][16]
+    const int64_t M = (int64_t)N * H * W;
+    const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
+    const int j = lane & 15, q = lane >> 4;
+    // the Cout / 128 channel tiles of a pixel tile are blocks b, b + 8, ... --
+    // the same XCD (block b runs on XCD b % 8), so its pixel rows come from one L2
+    const int ntiles = Cout / kTN;
+    const int r16 = blockIdx.x % (8 * ntiles);
+    const int nt = r16 / 8, mt = (blockIdx.x / (8 * ntiles)) * 8 + (r16 & 7);
+    if (mt >= mtiles) return;
+    const int64_t m0 = (int64_t)mt * kTM;
+    const int n0 = nt * kTN;
+    // staging: thread t moves float4 c = t % 16 of rows r = t / 16 + 16 i (i < 8)
+    const int sc = tid & 15, sr0 = tid >> 4;
+    int py[8], px[8], pix[8];  // pixel row / column / linear index (M < 2^31 / C)
+    bool pv[8];
+    const int HW = H * W;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int m = (int)m0 + sr0 + 16 * i;
+        pv[i] = m < M;
+        pix[i] = pv[i] ? m : 0;
+        const int rem = pix[i] % HW;
+        py[i] = rem / W;
+        px[i] = rem - py[i] * W;
+    }
+    const int K9 = 9 * C;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(X), (short)0, (int)(M * C * 4), 0x00020000);
+    const int cblocks = C / kKC, nchunks = 9 * cblocks;
+    // weight rows n0 + sr0 + 16 i, float4 sc of the chunk's 64 k (buffer offsets)
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(W2), (short)0, Cout * K9 * 4, 0x00020000);
+    const int wrow0 = (n0 + sr0) * K9 + 4 * sc;
+    float4 *const st_a = lds + sr0 * kRowF4 + sc;  // + buf stage, + 16 i rows (swizzle below)
+    f4v acc[4][4];
+#pragma unroll
+    for (int tc = 0; tc < 4; ++tc)
+#pragma unroll
+        for (int tp = 0; tp < 4; ++tp) acc[tc][tp] = f4v{0.f, 0.f, 0.f, 0.f};
+    const int pw0 = (wave & 1) * 64, cw0 = (wave >> 1) * 64;
+    // chunk ch = (tap, channel block): its pixel / weight float4s in registers
+#define VD_LOAD_CHUNK(CH)                                                                   \
+    {                                                                                       \
+        const int tap_ = (CH) / cblocks, cb_ = (CH) - tap_ * cblocks;                       \
+        const int dy_ = tap_ / 3 - 1, dx_ = tap_ % 3 - 1;                                   \
+        const int koff_ = tap_ * C + cb_ * kKC;                                             \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                     \
+            const int y_ = py[i] + dy_, x_ = px[i] + dx_;                                   \
+            const bool ok_ = pv[i] & ((unsigned)y_ < (unsigned)H) & ((unsigned)x_ < (unsigned)W); \
+            /* out-of-image taps read past the buffer's range: zeros, no branch */         \
+            const int off_ = ok_ ? ((pix[i] + dy_ * W + dx_) * C + cb_ * kKC + 4 * sc) * 4   \
+                                 : 0x7ffffff0;                                              \
+            ra[i] = __builtin_bit_cast(float4,                                              \
+                                       __builtin_amdgcn_raw_buffer_load_b128(xr, off_, 0, 0)); \
+            rb[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(             \
+                        wr, (wrow0 + 16 * i * K9 + koff_) * 4, 0, 0));                      \
+        }                                                                                   \
+    }
+#define VD_STORE_CHUNK(BUF)                                                                 \
+    {                                                                                       \
+        float4 *a_ = lds + (BUF) * kStageF4;                                                \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                     \
+            const int r_ = sr0 + 16 * i;                                                    \
+            a_[r_ * kRowF4 + (sc ^ (r_ & 15))] = ra[i];                                     \
+            a_[(kTM + r_) * kRowF4 + (sc ^ (r_ & 15))] = rb[i];                             \
+        }                                                                                   \
+    }
+    (void)st_a;
+    // one LDS stage per workgroup (64 KiB) and two workgroups per CU: while one
+    // workgroup stores its next chunk between its two barriers, the other's
+    // MFMAs keep the SIMDs busy
+    {
+        float4 ra[8], rb[8];
+        VD_LOAD_CHUNK(0)
+        VD_STORE_CHUNK(0)
+    }
+    __syncthreads();
+    const float4 *a = lds;
+    const float4 *b = lds + kTM * kRowF4;
+    for (int ch = 0; ch < nchunks; ++ch) {
+        const int nxt = ch + 1 < nchunks ? ch + 1 : ch;
+        float4 ra[8], rb[8];
+        VD_LOAD_CHUNK(nxt)
+        // keep the next chunk's loads here, a whole chunk of MFMAs ahead of their
+        // use (the scheduler would otherwise sink them next to the LDS stores)
+        __builtin_amdgcn_sched_barrier(0);
+        // fragments of block kb + 1 are read while block kb's MFMAs run
+        float4 pf[4], wf[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            pf[t] = a[(pw0 + 16 * t + j) * kRowF4 + (q ^ j)];
+            wf[t] = b[(cw0 + 16 * t + j) * kRowF4 + (q ^ j)];
+        }
+#pragma unroll
+        for (int kb = 0; kb < kKC / 16; ++kb) {
+            float4 pn[4], wn[4];
+            if (kb + 1 < kKC / 16) {
+                const int c = ((kb + 1) * 4 + q) ^ j;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    pn[t] = a[(pw0 + 16 * t + j) * kRowF4 + c];
+                    wn[t] = b[(cw0 + 16 * t + j) * kRowF4 + c];
+                }
+            }
+            // component-major: 16 independent accumulators between two uses of one
+#define VD_MF(COMP)                                                                         \
+    _Pragma("unroll") for (int tc = 0; tc < 4; ++tc)                                        \
+        _Pragma("unroll") for (int tp = 0; tp < 4; ++tp) acc[tc][tp] =                      \
+            __builtin_amdgcn_mfma_f32_16x16x4f32(wf[tc].COMP, pf[tp].COMP, acc[tc][tp], 0, 0, 0);
+            VD_MF(x)
+            VD_MF(y)
+            VD_MF(z)
+            VD_MF(w)
+#undef VD_MF
+            if (kb + 1 < kKC / 16) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    pf[t] = pn[t];
+                    wf[t] = wn[t];
+                }
+            }
+        }
+        __syncthreads();  // every wave is done reading the stage
+        VD_STORE_CHUNK(0)
+        __syncthreads();  // the next chunk is visible
+    }
+#undef VD_LOAD_CHUNK
+#undef VD_STORE_CHUNK
+    // epilogue: lane (j, q), tile (tc, tp) holds channels n0 + cw0 + 16 tc + 4 q .. + 3
+    // of pixel m0 + pw0 + 16 tp + j
+#pragma unroll
+    for (int tc = 0; tc < 4; ++tc) {
+        const int co = n0 + cw0 + 16 * tc + 4 * q;
+        const float4 bv = bias ? *reinterpret_cast<const float4 *>(bias + co)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int tp = 0; tp < 4; ++tp) {
+            const int64_t m = m0 + pw0 + 16 * tp + j;
+            if (m >= M) continue;
+            float4 o = make_float4(acc[tc][tp][0] + bv.x, acc[tc][tp][1] + bv.y,
+                                   acc[tc][tp][2] + bv.z, acc[tc][tp][3] + bv.w);
+            if (RELU) {
+                o.x = fmaxf(o.x, 0.f);
+                o.y = fmaxf(o.y, 0.f);
+                o.z = fmaxf(o.z, 0.f);
+                o.w = fmaxf(o.w, 0.f);
+            }
+            *reinterpret_cast<float4 *>(Y + m * Cout + co) = o;
+        }
+    }
+}
+
+}  // namespace
+
+bool conv3x3_mfma_supported(int C, int Cout) {
+    return C % kKC == 0 && C >= kKC && Cout % kTN == 0;
+}
+
+int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float *W2, int Cout,
+                        const float *bias, int relu, float *Y, hipStream_t s) {
+    const int64_t M = (int64_t)N * H * W;
+    if (M == 0) return VD_OK;
+    if (!conv3x3_mfma_supported(C, Cout)) return VD_ERR_SHAPE;
+    if (M * C * 4 >= 0x7ffffff0ll) return VD_ERR_SHAPE;  // 32-bit buffer offsets
+    const int64_t mtiles = (M + kTM - 1) / kTM;
+    const int64_t blocks = (mtiles + 7) / 8 * 8 * (Cout / kTN);
+    if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
+    const size_t lds = kStageF4 * sizeof(float4);  // 64 KiB: two workgroups per CU
+    auto kern = relu ? conv3x3_mfma_kernel<true> : conv3x3_mfma_kernel<false>;
+    static bool attr[2] = {false, false};
+    if (!attr[relu ? 1 : 0]) {
+        if (hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds) != hipSuccess)
+            return VD_ERR_LAUNCH;
+        attr[relu ? 1 : 0] = true;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, s, X, N, H, W, C, W2, Cout,
+                       bias, Y, (int)mtiles);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+}  // namespace vd

@@ -34,6 +34,9 @@ int launch_gemm_bias_act(const float *A, int M, int K, const float *W, int N, co
                          const float *R, int relu, float *D, void *ws, size_t ws_bytes,
                          hipStream_t s);
 bool gemm1x1_mfma_supported(int K, int N);
+bool conv3x3_mfma_supported(int C, int Cout);
+int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float *W2, int Cout,
+                        const float *bias, int relu, float *Y, hipStream_t s);
 bool gemm1x1_dual_supported(int K1, int K2, int N);
 int launch_gemm1x1_dual(const float *A1, int K1, const float *A2, int K2, int M, const float *W,
                         int N, const float *bias, int relu, float *D, hipStream_t s);

@@ -444,6 +444,43 @@ def gemm_bias_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
     return out
 
 
+def conv3x3_weight(w: torch.Tensor) -> torch.Tensor:
+    """PyTorch conv weight [Cout][Cin][3][3] -> the [Cout][3][3][Cin] layout
+    vd_conv3x3_bias_act reads (once per model, at prepare time)."""
+    return w.permute(0, 2, 3, 1).contiguous()
+
+
+def conv3x3_bias_act(x: torch.Tensor, w2: torch.Tensor, bias: Optional[torch.Tensor],
+                     relu: bool = False, out: Optional[torch.Tensor] = None):
+    """act(conv3x3(x, pad 1) + bias) on a channels_last fp32 tensor in one MFMA
+    implicit-GEMM kernel (vd_conv3x3_bias_act); w2 from conv3x3_weight.  Returns
+    None for a shape the kernel does not serve (the caller falls back)."""
+    if x.dim() != 4 or not x.is_cuda or x.dtype != torch.float32 or \
+            not x.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("conv3x3_bias_act: x must be a channels_last fp32 CUDA tensor")
+    N, C, H, W = x.shape
+    w_ = _need(w2, "w2")
+    Cout = w_.shape[0]
+    if tuple(w_.shape) != (Cout, 3, 3, C):
+        raise ValueError("w2 must be [Cout][3][3][Cin], got %s" % (tuple(w_.shape),))
+    b_ = _need(bias, "bias") if bias is not None else None
+    if b_ is not None and b_.numel() != Cout:
+        raise ValueError("bias must have %d elements" % Cout)
+    if out is None:
+        out = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device,
+                          memory_format=torch.channels_last)
+    elif tuple(out.shape) != (N, Cout, H, W) or \
+            not out.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("out must be a channels_last %s tensor" % ((N, Cout, H, W),))
+    st = lib().vd_conv3x3_bias_act(x.data_ptr(), N, H, W, C, w_.data_ptr(), Cout,
+                                   b_.data_ptr() if b_ is not None else None, int(relu),
+                                   out.data_ptr(), _stream())
+    if st == VD_ERR_SHAPE:
+        return None
+    check(st, "vd_conv3x3_bias_act")
+    return out
+
+
 def gemm_dual_bias_act(a1: torch.Tensor, a2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
                        relu: bool = True, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """act(a1 @ w[:, :K1].T + a2 @ w[:, K1:].T + bias) in one MFMA kernel
