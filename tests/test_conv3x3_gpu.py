@@ -12,8 +12,10 @@ pytestmark = pytest.mark.gpu
                                           (3, 128, 1, 1, 128), (1, 256, 25, 42, 256),
                                           (5, 256, 7, 7, 384)])
 @pytest.mark.parametrize("relu", [False, True])
-def test_conv3x3_vs_torch(N, C, H, W, Cout, relu):
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_conv3x3_vs_torch(monkeypatch, N, C, H, W, Cout, relu, variant):
     from vosdetectron_amd import ops
+    monkeypatch.setenv("VOSDET_CONV3X3_VARIANT", variant)
     g = torch.Generator(device="cpu").manual_seed(N * 1000 + C + H + Cout)
     x = torch.randn(N, C, H, W, generator=g).cuda().contiguous(memory_format=torch.channels_last)
     w = (torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** .5).cuda()

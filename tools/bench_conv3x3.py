@@ -43,12 +43,16 @@ def main():
         y = torch.empty_like(x)
         flops = 2 * N * H * W * C * C * 9
         t_ref = timed(lambda: ops.bias_act_(F.conv2d(x, w, None, padding=1), b, relu=True))
-        t_own = timed(lambda: ops.conv3x3_bias_act(x, w2, b, relu=True, out=y))
         ref = ops.bias_act_(F.conv2d(x, w, None, padding=1), b, relu=True)
         row = {"shape": [N, C, H, W], "miopen_plus_bias_act_us": round(t_ref, 1),
-               "mfma_us": round(t_own, 1), "mfma_frac": round(flops / (t_own * 1e-6) / PEAK, 3),
-               "miopen_frac": round(flops / (t_ref * 1e-6) / PEAK, 3),
-               "maxdiff": float((y - ref).abs().max())}
+               "miopen_frac": round(flops / (t_ref * 1e-6) / PEAK, 3)}
+        for v in os.environ.get("CONV3X3_VARIANTS", "1,2").split(","):
+            os.environ["VOSDET_CONV3X3_VARIANT"] = v
+            t_own = timed(lambda: ops.conv3x3_bias_act(x, w2, b, relu=True, out=y))
+            row["mfma_v%s_us" % v] = round(t_own, 1)
+            row["mfma_v%s_frac" % v] = round(flops / (t_own * 1e-6) / PEAK, 3)
+            row["maxdiff_v%s" % v] = float((y - ref).abs().max())
+        os.environ.pop("VOSDET_CONV3X3_VARIANT")
         print(json.dumps(row), flush=True)
         rows.append(row)
         del x, y, ref

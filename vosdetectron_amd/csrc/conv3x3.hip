@@ -34,15 +34,24 @@ namespace {
 
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-constexpr int kTM = 128, kTN = 128, kKC = 64;  // tile: pixels x channels, K chunk
-constexpr int kRowF4 = kKC / 4;                // float4s per staged row (16)
-constexpr int kStageF4 = (kTM + kTN) * kRowF4; // float4s per LDS stage
+constexpr int kTM = 128, kTN = 128;  // tile: pixels x output channels
 
-template <bool RELU>
+// KC input channels per K chunk, STAGES LDS stages per workgroup.  Row r of a
+// stage holds KC / 4 float4s, float4 c stored at c ^ swz(r): conflict-free
+// ds_read_b128 for 16 lanes reading 16 consecutive rows at one c.
+template <int KC>
+__device__ __forceinline__ int swz(int r) {
+    return KC == 64 ? (r & 15) : ((r >> 1) & 7);
+}
+
+template <bool RELU, int KC, int STAGES>
 __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ W2,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int mtiles) {
-    extern __shared__ __attribute__((aligned(16))) float4 lds[];  // [kTM + kTN][16]
+    constexpr int R4 = KC / 4;               // float4s per staged row
+    constexpr int STAGE = (kTM + kTN) * R4;  // float4s per stage
+    constexpr int RP = 256 / R4, NI = kTM / RP;  // rows per staging pass, passes
+    extern __shared__ __attribute__((aligned(16))) float4 lds[];  // [STAGES][kTM + kTN][R4]
     const int64_t M = (int64_t)N * H * W;
     const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
     const int j = lane & 15, q = lane >> 4;
@@ -54,14 +63,14 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
     if (mt >= mtiles) return;
     const int64_t m0 = (int64_t)mt * kTM;
     const int n0 = nt * kTN;
-    // staging: thread t moves float4 c = t % 16 of rows r = t / 16 + 16 i (i < 8)
-    const int sc = tid & 15, sr0 = tid >> 4;
-    int py[8], px[8], pix[8];  // pixel row / column / linear index (M < 2^31 / C)
-    bool pv[8];
+    // staging: thread t moves float4 sc = t % R4 of rows sr0 + RP i (i < NI)
+    const int sc = tid % R4, sr0 = tid / R4;
+    int py[NI], px[NI], pix[NI];  // pixel row / column / linear index (M * C < 2^29)
+    bool pv[NI];
     const int HW = H * W;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int m = (int)m0 + sr0 + 16 * i;
+    for (int i = 0; i < NI; ++i) {
+        const int m = (int)m0 + sr0 + RP * i;
         pv[i] = m < M;
         pix[i] = pv[i] ? m : 0;
         const int rem = pix[i] % HW;
@@ -71,12 +80,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
     const int K9 = 9 * C;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float *>(X), (short)0, (int)(M * C * 4), 0x00020000);
-    const int cblocks = C / kKC, nchunks = 9 * cblocks;
-    // weight rows n0 + sr0 + 16 i, float4 sc of the chunk's 64 k (buffer offsets)
+    const int cblocks = C / KC, nchunks = 9 * cblocks;
+    // weight rows n0 + sr0 + RP i, float4 sc of the chunk's KC k (buffer offsets)
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float *>(W2), (short)0, Cout * K9 * 4, 0x00020000);
     const int wrow0 = (n0 + sr0) * K9 + 4 * sc;
-    float4 *const st_a = lds + sr0 * kRowF4 + sc;  // + buf stage, + 16 i rows (swizzle below)
     f4v acc[4][4];
 #pragma unroll
     for (int tc = 0; tc < 4; ++tc)
@@ -88,63 +96,63 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
     {                                                                                       \
         const int tap_ = (CH) / cblocks, cb_ = (CH) - tap_ * cblocks;                       \
         const int dy_ = tap_ / 3 - 1, dx_ = tap_ % 3 - 1;                                   \
-        const int koff_ = tap_ * C + cb_ * kKC;                                             \
-        _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                     \
+        const int koff_ = tap_ * C + cb_ * KC;                                              \
+        _Pragma("unroll") for (int i = 0; i < NI; ++i) {                                    \
             const int y_ = py[i] + dy_, x_ = px[i] + dx_;                                   \
             const bool ok_ = pv[i] & ((unsigned)y_ < (unsigned)H) & ((unsigned)x_ < (unsigned)W); \
             /* out-of-image taps read past the buffer's range: zeros, no branch */         \
-            const int off_ = ok_ ? ((pix[i] + dy_ * W + dx_) * C + cb_ * kKC + 4 * sc) * 4   \
+            const int off_ = ok_ ? ((pix[i] + dy_ * W + dx_) * C + cb_ * KC + 4 * sc) * 4    \
                                  : 0x7ffffff0;                                              \
             ra[i] = __builtin_bit_cast(float4,                                              \
                                        __builtin_amdgcn_raw_buffer_load_b128(xr, off_, 0, 0)); \
             rb[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(             \
-                        wr, (wrow0 + 16 * i * K9 + koff_) * 4, 0, 0));                      \
+                        wr, (wrow0 + RP * i * K9 + koff_) * 4, 0, 0));                      \
         }                                                                                   \
     }
 #define VD_STORE_CHUNK(BUF)                                                                 \
     {                                                                                       \
-        float4 *a_ = lds + (BUF) * kStageF4;                                                \
-        _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                     \
-            const int r_ = sr0 + 16 * i;                                                    \
-            a_[r_ * kRowF4 + (sc ^ (r_ & 15))] = ra[i];                                     \
-            a_[(kTM + r_) * kRowF4 + (sc ^ (r_ & 15))] = rb[i];                             \
+        float4 *a_ = lds + (BUF) * STAGE;                                                   \
+        _Pragma("unroll") for (int i = 0; i < NI; ++i) {                                    \
+            const int r_ = sr0 + RP * i;                                                    \
+            a_[r_ * R4 + (sc ^ swz<KC>(r_))] = ra[i];                                       \
+            a_[(kTM + r_) * R4 + (sc ^ swz<KC>(r_))] = rb[i];                               \
         }                                                                                   \
     }
-    (void)st_a;
-    // one LDS stage per workgroup (64 KiB) and two workgroups per CU: while one
-    // workgroup stores its next chunk between its two barriers, the other's
-    // MFMAs keep the SIMDs busy
+    // STAGES == 1: one stage per workgroup, the next chunk stored between two
+    // barriers; STAGES == 2: double-buffered, one barrier per chunk.  Either way
+    // two workgroups share a CU, so one's store phase overlaps the other's MFMAs.
     {
-        float4 ra[8], rb[8];
+        float4 ra[NI], rb[NI];
         VD_LOAD_CHUNK(0)
         VD_STORE_CHUNK(0)
     }
     __syncthreads();
-    const float4 *a = lds;
-    const float4 *b = lds + kTM * kRowF4;
     for (int ch = 0; ch < nchunks; ++ch) {
+        const int buf = STAGES == 2 ? (ch & 1) : 0;
         const int nxt = ch + 1 < nchunks ? ch + 1 : ch;
-        float4 ra[8], rb[8];
+        float4 ra[NI], rb[NI];
         VD_LOAD_CHUNK(nxt)
         // keep the next chunk's loads here, a whole chunk of MFMAs ahead of their
         // use (the scheduler would otherwise sink them next to the LDS stores)
         __builtin_amdgcn_sched_barrier(0);
+        const float4 *a = lds + buf * STAGE;
+        const float4 *b = a + kTM * R4;
         // fragments of block kb + 1 are read while block kb's MFMAs run
         float4 pf[4], wf[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            pf[t] = a[(pw0 + 16 * t + j) * kRowF4 + (q ^ j)];
-            wf[t] = b[(cw0 + 16 * t + j) * kRowF4 + (q ^ j)];
+            pf[t] = a[(pw0 + 16 * t + j) * R4 + (q ^ swz<KC>(j))];
+            wf[t] = b[(cw0 + 16 * t + j) * R4 + (q ^ swz<KC>(j))];
         }
 #pragma unroll
-        for (int kb = 0; kb < kKC / 16; ++kb) {
+        for (int kb = 0; kb < KC / 16; ++kb) {
             float4 pn[4], wn[4];
-            if (kb + 1 < kKC / 16) {
-                const int c = ((kb + 1) * 4 + q) ^ j;
+            if (kb + 1 < KC / 16) {
+                const int c = ((kb + 1) * 4 + q) ^ swz<KC>(j);
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    pn[t] = a[(pw0 + 16 * t + j) * kRowF4 + c];
-                    wn[t] = b[(cw0 + 16 * t + j) * kRowF4 + c];
+                    pn[t] = a[(pw0 + 16 * t + j) * R4 + c];
+                    wn[t] = b[(cw0 + 16 * t + j) * R4 + c];
                 }
             }
             // component-major: 16 independent accumulators between two uses of one
@@ -157,7 +165,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
             VD_MF(z)
             VD_MF(w)
 #undef VD_MF
-            if (kb + 1 < kKC / 16) {
+            if (kb + 1 < KC / 16) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                     pf[t] = pn[t];
@@ -165,8 +173,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
                 }
             }
         }
-        __syncthreads();  // every wave is done reading the stage
-        VD_STORE_CHUNK(0)
+        if (STAGES == 1) __syncthreads();  // every wave is done reading the stage
+        VD_STORE_CHUNK(STAGES == 2 ? (buf ^ 1) : 0)
         __syncthreads();  // the next chunk is visible
     }
 #undef VD_LOAD_CHUNK
@@ -197,29 +205,35 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
 
 }  // namespace
 
-bool conv3x3_mfma_supported(int C, int Cout) {
-    return C % kKC == 0 && C >= kKC && Cout % kTN == 0;
-}
+bool conv3x3_mfma_supported(int C, int Cout) { return C % 64 == 0 && C >= 64 && Cout % kTN == 0; }
 
 int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float *W2, int Cout,
                         const float *bias, int relu, float *Y, hipStream_t s) {
     const int64_t M = (int64_t)N * H * W;
     if (M == 0) return VD_OK;
     if (!conv3x3_mfma_supported(C, Cout)) return VD_ERR_SHAPE;
-    if (M * C * 4 >= 0x7ffffff0ll) return VD_ERR_SHAPE;  // 32-bit buffer offsets
+    if (M * C * 4 >= 0x7ffffff0ll || (int64_t)Cout * 9 * C * 4 >= 0x7ffffff0ll)
+        return VD_ERR_SHAPE;  // 32-bit buffer offsets
     const int64_t mtiles = (M + kTM - 1) / kTM;
     const int64_t blocks = (mtiles + 7) / 8 * 8 * (Cout / kTN);
     if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
-    const size_t lds = kStageF4 * sizeof(float4);  // 64 KiB: two workgroups per CU
-    auto kern = relu ? conv3x3_mfma_kernel<true> : conv3x3_mfma_kernel<false>;
-    static bool attr[2] = {false, false};
-    if (!attr[relu ? 1 : 0]) {
-        if (hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds) != hipSuccess)
-            return VD_ERR_LAUNCH;
-        attr[relu ? 1 : 0] = true;
+    // variant: 1 = K chunk 64, one LDS stage (64 KiB); 2 = K chunk 32, two stages
+    // (64 KiB); both two workgroups per CU
+    const char *e = getenv("VOSDET_CONV3X3_VARIANT");
+    const int v = e ? atoi(e) : 1;
+    void (*kern)(const float *, int, int, int, int, const float *, int, const float *, float *,
+                 int);
+    size_t lds;
+    if (v == 2) {
+        kern = relu ? conv3x3_mfma_kernel<true, 32, 2> : conv3x3_mfma_kernel<false, 32, 2>;
+        lds = 2 * (size_t)(kTM + kTN) * 8 * sizeof(float4);
+    } else {
+        kern = relu ? conv3x3_mfma_kernel<true, 64, 1> : conv3x3_mfma_kernel<false, 64, 1>;
+        lds = (size_t)(kTM + kTN) * 16 * sizeof(float4);
     }
+    if (hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return VD_ERR_LAUNCH;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, s, X, N, H, W, C, W2, Cout,
                        bias, Y, (int)mtiles);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;

@@ -55,6 +55,30 @@ def _conv_epi(conv: nn.Conv2d, x, relu=True, res=None, res_bias=None, up=False):
                          upsample_residual=up)
 
 
+_CONV3X3_MIN_PIXELS = 1 << 18  # below this CK's kernels fill the chip better
+
+
+def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False):
+    """conv (3x3, stride 1, pad 1) of a channels_last fp32 tensor as the
+    hand-written MFMA implicit GEMM with the bias (+ ReLU) epilogue
+    (ops.conv3x3_bias_act), or None where it does not apply: other geometry,
+    fewer than 2^18 output pixels (P4-P6 of a 16-frame batch), or
+    VOSDET_CONV3X3_MFMA=0.  The permuted weight is cached on the module."""
+    if (os.environ.get("VOSDET_CONV3X3_MFMA", "1") == "0" or not x.is_cuda
+            or conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1)
+            or conv.dilation != (1, 1) or conv.groups != 1 or x.dtype != torch.float32
+            or x.shape[0] * x.shape[2] * x.shape[3] < _CONV3X3_MIN_PIXELS
+            or not x.is_contiguous(memory_format=torch.channels_last)):
+        return None
+    w = conv.weight
+    key = (w.data_ptr(), w._version)
+    if getattr(conv, "_vd_w2_key", None) != key:
+        conv._vd_w2 = ops.conv3x3_weight(w.detach())
+        conv._vd_w2_key = key
+    b = conv.bias.detach() if (bias and conv.bias is not None) else None
+    return ops.conv3x3_bias_act(x, conv._vd_w2, b, relu=relu)
+
+
 def _stage_counts(conv_body: str):
     return {"FPN.fpn_ResNet50_conv5_body": (3, 4, 6, 3),
             "FPN.fpn_ResNet101_conv5_body": (3, 4, 23, 3),
@@ -355,7 +379,10 @@ class FPNBody(nn.Module):
         if self.use_gn:
             outs = [self._gn_seq(self.posthoc_modules[i], inner[i]) for i in range(4)]
         else:
-            outs = [self.posthoc_modules[i](inner[i]) for i in range(4)]
+            outs = []
+            for i in range(4):
+                y = _conv3x3_mfma(self.posthoc_modules[i], inner[i]) if self.epilogue else None
+                outs.append(y if y is not None else self.posthoc_modules[i](inner[i]))
         outs.insert(0, F.max_pool2d(outs[0], kernel_size=1, stride=2, padding=0))  # P6
         return outs  # [P6, P5, P4, P3, P2]
 
@@ -389,7 +416,9 @@ class FPNRPNOutputs(nn.Module):
         if (self.fused is not None and x.is_cuda and _gemm_ok(x) and 5 * A <= 16
                 and x.shape[1] % 64 == 0 and os.environ.get("VOSDET_RPN_HEAD", "1") != "0"):
             # conv without bias, then bias + ReLU + both 1x1s + sigmoid in one pass
-            h = _conv_nb(self.FPN_RPN_conv, x)
+            h = _conv3x3_mfma(self.FPN_RPN_conv, x, bias=False)
+            if h is None:
+                h = _conv_nb(self.FPN_RPN_conv, x)
             if not h.is_contiguous(memory_format=torch.channels_last):
                 h = h.contiguous(memory_format=torch.channels_last)
             return ops.rpn_head(h, self.FPN_RPN_conv.bias.detach(), self.fused_w2d,
@@ -566,7 +595,8 @@ class MaskHeadV1upXconvs(nn.Module):
     def _convs_nhwc(self, x):
         for m in self.conv_fcn:
             if isinstance(m, nn.Conv2d):
-                x = _conv_epi(m, x)
+                y = _conv3x3_mfma(m, x, relu=True)
+                x = y if y is not None else _conv_epi(m, x)
         return x
 
     def forward(self, x, rpn_ret):
