@@ -14,8 +14,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vosdetectron_amd import ops  # noqa: E402
 
 PEAK = 157.3e12
-SHAPES = [(16, 256, 200, 336), (16, 256, 100, 168), (16, 256, 50, 84), (1600, 256, 14, 14),
-          (16, 256, 25, 42)]
+SHAPES = [(16, 256, 200, 336, 256), (16, 256, 100, 168, 256), (16, 256, 50, 84, 256),
+          (1600, 256, 14, 14, 256), (16, 256, 25, 42, 256), (16, 128, 100, 168, 128)]
 
 
 def timed(fn, iters=10):
@@ -34,17 +34,17 @@ def timed(fn, iters=10):
 def main():
     torch.backends.cudnn.benchmark = True
     rows = []
-    for N, C, H, W in SHAPES:
+    for N, C, H, W, Co in SHAPES:
         x = torch.randn(N, C, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
-        w = (torch.randn(C, C, 3, 3, device="cuda") / (9 * C) ** .5).contiguous(
+        w = (torch.randn(Co, C, 3, 3, device="cuda") / (9 * C) ** .5).contiguous(
             memory_format=torch.channels_last)
-        b = torch.randn(C, device="cuda")
+        b = torch.randn(Co, device="cuda")
         w2 = ops.conv3x3_weight(w)
-        y = torch.empty_like(x)
-        flops = 2 * N * H * W * C * C * 9
+        y = torch.empty(N, Co, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
+        flops = 2 * N * H * W * C * Co * 9
         t_ref = timed(lambda: ops.bias_act_(F.conv2d(x, w, None, padding=1), b, relu=True))
         ref = ops.bias_act_(F.conv2d(x, w, None, padding=1), b, relu=True)
-        row = {"shape": [N, C, H, W], "miopen_plus_bias_act_us": round(t_ref, 1),
+        row = {"shape": [N, C, H, W, Co], "miopen_plus_bias_act_us": round(t_ref, 1),
                "miopen_frac": round(flops / (t_ref * 1e-6) / PEAK, 3)}
         for v in os.environ.get("CONV3X3_VARIANTS", "1,2").split(","):
             os.environ["VOSDET_CONV3X3_VARIANT"] = v
