@@ -218,7 +218,8 @@ int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float 
     const int64_t blocks = (mtiles + 7) / 8 * 8 * (Cout / kTN);
     if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
     // variant: 1 = K chunk 64, one LDS stage (64 KiB); 2 = K chunk 32, two stages
-    // (64 KiB); both two workgroups per CU
+    // (64 KiB); both two workgroups per CU.  Measured equal within 1 %; raising the
+    // wave priority over the MFMA phase (s_setprio) cost 1-4 % (profiles/r02c/README.md)
     const char *e = getenv("VOSDET_CONV3X3_VARIANT");
     const int v = e ? atoi(e) : 1;
     void (*kern)(const float *, int, int, int, int, const float *, int, const float *, float *,
