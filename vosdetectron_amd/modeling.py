@@ -43,7 +43,11 @@ class AffineChannel2d(nn.Module):
 
 
 def _conv_nb(conv: nn.Conv2d, x):
-    """The convolution of `conv` without its bias (added by the fused epilogue)."""
+    """The convolution of `conv` without its bias (added by the fused epilogue):
+    the MFMA 3x3 kernel where it applies (_conv3x3_mfma), else MIOpen."""
+    y = _conv3x3_mfma(conv, x, bias=False)
+    if y is not None:
+        return y
     return F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
 
 
