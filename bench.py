@@ -152,9 +152,16 @@ def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=Non
             and os.path.exists(pmc):
         traffic = int(json.load(open(pmc))["traffic_bytes"])
         tsrc = os.path.relpath(pmc, os.path.dirname(os.path.abspath(__file__)))
+    extra = {}
+    if traffic:
+        # the bytes the launch really moves through the fabric (PMC) per second:
+        # beside the algorithmic rate, what the memory system delivers to it
+        extra = {"traffic_over_algorithmic": round(traffic / nbytes, 3),
+                 "traffic_GBs": round(traffic / t / 1e9, 1),
+                 "traffic_frac": round(traffic / t / 1e9 / HBM_PEAK_GBS, 4)}
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "traffic_source": tsrc,
+            "traffic_source": tsrc, **extra,
             "kernel": ROIALIGN_KERNEL.get(variant,
                                           "vd::roi_align_fpn_nhwc_kernel")
                       + (" (XCD-ordered)" if use_order else "") + ", out " + out_layout,
