@@ -134,7 +134,7 @@ int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const 
  * permuted to [Cout][3][3][Cin].  bias may be NULL.  The FPN posthoc convs
  * (lib/modeling/FPN.py:227-258), the RPN conv (FPN.py:376-422) and the mask head
  * convs (mask_rcnn_heads.py:178-188) run in PyTorch in the reference.
- * Requires Cin % 64 == 0 and Cout % 128 == 0 (VD_ERR_SHAPE otherwise). */
+ * Requires Cin % 64 == 0 and Cout % 128 == 0 or Cout == 64 (VD_ERR_SHAPE otherwise). */
 int vd_conv3x3_bias_act(const float *X, int N, int H, int W, int C, const float *W2, int Cout,
                         const float *bias, int relu, float *Y, void *stream);
 

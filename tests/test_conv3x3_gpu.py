@@ -10,7 +10,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("N,C,H,W,Cout", [(2, 64, 9, 13, 128), (1, 256, 14, 14, 256),
                                           (3, 128, 1, 1, 128), (1, 256, 25, 42, 256),
-                                          (5, 256, 7, 7, 384)])
+                                          (5, 256, 7, 7, 384), (2, 64, 30, 41, 64),
+                                          (1, 128, 5, 3, 64)])
 @pytest.mark.parametrize("relu", [False, True])
 @pytest.mark.parametrize("variant", ["1", "2"])
 def test_conv3x3_vs_torch(monkeypatch, N, C, H, W, Cout, relu, variant):
@@ -36,5 +37,5 @@ def test_conv3x3_no_bias_and_unsupported_shape():
     got = ops.conv3x3_bias_act(x, ops.conv3x3_weight(w), None)
     ref = F.conv2d(x, w, None, padding=1)
     assert float((got - ref).abs().max()) <= 2e-5 * max(1., float(ref.abs().max()))
-    w2 = torch.randn(64, 64, 3, 3, device="cuda")  # Cout % 128 != 0: not served
+    w2 = torch.randn(96, 64, 3, 3, device="cuda")  # Cout neither 64 nor a multiple of 128
     assert ops.conv3x3_bias_act(x, ops.conv3x3_weight(w2), None) is None

@@ -16,7 +16,8 @@ from vosdetectron_amd import ops  # noqa: E402
 PEAK = 157.3e12
 SHAPES = [(int(v) for v in t.split("x")) for t in os.environ["CONV3X3_SHAPES"].split(",")] \
     if os.environ.get("CONV3X3_SHAPES") else [(16, 256, 200, 336, 256), (16, 256, 100, 168, 256), (16, 256, 50, 84, 256),
-          (1600, 256, 14, 14, 256), (16, 256, 25, 42, 256), (16, 128, 100, 168, 128)]
+          (1600, 256, 14, 14, 256), (16, 256, 25, 42, 256), (16, 128, 100, 168, 128),
+          (16, 64, 200, 336, 64)]
 
 
 def timed(fn, iters=10):

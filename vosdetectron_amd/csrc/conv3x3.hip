@@ -44,25 +44,29 @@ __device__ __forceinline__ int swz(int r) {
     return KC == 64 ? (r & 15) : ((r >> 1) & 7);
 }
 
-template <bool RELU, int KC, int STAGES>
+// TM x TN: the workgroup tile (pixels x output channels), 4 waves of 64 x 64:
+// 128 x 128 (2 x 2 waves) or 256 x 64 (4 x 1, for Cout = 64).
+template <bool RELU, int KC, int STAGES, int TM = kTM, int TN = kTN>
 __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ W2,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int mtiles) {
     constexpr int R4 = KC / 4;               // float4s per staged row
-    constexpr int STAGE = (kTM + kTN) * R4;  // float4s per stage
-    constexpr int RP = 256 / R4, NI = kTM / RP;  // rows per staging pass, passes
-    extern __shared__ __attribute__((aligned(16))) float4 lds[];  // [STAGES][kTM + kTN][R4]
+    constexpr int STAGE = (TM + TN) * R4;    // float4s per stage
+    constexpr int RP = 256 / R4;             // rows per staging pass
+    constexpr int NI = TM / RP, NB = TN / RP;  // passes for pixel / weight rows
+    constexpr int WPX = TM / 64;             // waves along the pixels
+    extern __shared__ __attribute__((aligned(16))) float4 lds[];  // [STAGES][TM + TN][R4]
     const int64_t M = (int64_t)N * H * W;
     const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
     const int j = lane & 15, q = lane >> 4;
-    // the Cout / 128 channel tiles of a pixel tile are blocks b, b + 8, ... --
+    // the Cout / TN channel tiles of a pixel tile are blocks b, b + 8, ... --
     // the same XCD (block b runs on XCD b % 8), so its pixel rows come from one L2
-    const int ntiles = Cout / kTN;
+    const int ntiles = Cout / TN;
     const int r16 = blockIdx.x % (8 * ntiles);
     const int nt = r16 / 8, mt = (blockIdx.x / (8 * ntiles)) * 8 + (r16 & 7);
     if (mt >= mtiles) return;
-    const int64_t m0 = (int64_t)mt * kTM;
-    const int n0 = nt * kTN;
+    const int64_t m0 = (int64_t)mt * TM;
+    const int n0 = nt * TN;
     // staging: thread t moves float4 sc = t % R4 of rows sr0 + RP i (i < NI)
     const int sc = tid % R4, sr0 = tid / R4;
     int py[NI], px[NI], pix[NI];  // pixel row / column / linear index (M * C < 2^29)
@@ -90,7 +94,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
     for (int tc = 0; tc < 4; ++tc)
 #pragma unroll
         for (int tp = 0; tp < 4; ++tp) acc[tc][tp] = f4v{0.f, 0.f, 0.f, 0.f};
-    const int pw0 = (wave & 1) * 64, cw0 = (wave >> 1) * 64;
+    const int pw0 = (wave % WPX) * 64, cw0 = (wave / WPX) * 64;
     // chunk ch = (tap, channel block): its pixel / weight float4s in registers
 #define VD_LOAD_CHUNK(CH)                                                                   \
     {                                                                                       \
@@ -105,9 +109,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
                                  : 0x7ffffff0;                                              \
             ra[i] = __builtin_bit_cast(float4,                                              \
                                        __builtin_amdgcn_raw_buffer_load_b128(xr, off_, 0, 0)); \
+        }                                                                                   \
+        _Pragma("unroll") for (int i = 0; i < NB; ++i)                                      \
             rb[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(             \
                         wr, (wrow0 + RP * i * K9 + koff_) * 4, 0, 0));                      \
-        }                                                                                   \
     }
 #define VD_STORE_CHUNK(BUF)                                                                 \
     {                                                                                       \
@@ -115,14 +120,17 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
         _Pragma("unroll") for (int i = 0; i < NI; ++i) {                                    \
             const int r_ = sr0 + RP * i;                                                    \
             a_[r_ * R4 + (sc ^ swz<KC>(r_))] = ra[i];                                       \
-            a_[(kTM + r_) * R4 + (sc ^ swz<KC>(r_))] = rb[i];                               \
+        }                                                                                   \
+        _Pragma("unroll") for (int i = 0; i < NB; ++i) {                                    \
+            const int r_ = sr0 + RP * i;                                                    \
+            a_[(TM + r_) * R4 + (sc ^ swz<KC>(r_))] = rb[i];                                \
         }                                                                                   \
     }
     // STAGES == 1: one stage per workgroup, the next chunk stored between two
     // barriers; STAGES == 2: double-buffered, one barrier per chunk.  Either way
     // two workgroups share a CU, so one's store phase overlaps the other's MFMAs.
     {
-        float4 ra[NI], rb[NI];
+        float4 ra[NI], rb[NB];
         VD_LOAD_CHUNK(0)
         VD_STORE_CHUNK(0)
     }
@@ -130,13 +138,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
     for (int ch = 0; ch < nchunks; ++ch) {
         const int buf = STAGES == 2 ? (ch & 1) : 0;
         const int nxt = ch + 1 < nchunks ? ch + 1 : ch;
-        float4 ra[NI], rb[NI];
+        float4 ra[NI], rb[NB];
         VD_LOAD_CHUNK(nxt)
         // keep the next chunk's loads here, a whole chunk of MFMAs ahead of their
         // use (the scheduler would otherwise sink them next to the LDS stores)
         __builtin_amdgcn_sched_barrier(0);
         const float4 *a = lds + buf * STAGE;
-        const float4 *b = a + kTM * R4;
+        const float4 *b = a + TM * R4;
         // fragments of block kb + 1 are read while block kb's MFMAs run
         float4 pf[4], wf[4];
 #pragma unroll
@@ -205,7 +213,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
 
 }  // namespace
 
-bool conv3x3_mfma_supported(int C, int Cout) { return C % 64 == 0 && C >= 64 && Cout % kTN == 0; }
+bool conv3x3_mfma_supported(int C, int Cout) {
+    return C % 64 == 0 && C >= 64 && (Cout % kTN == 0 || Cout == 64);
+}
 
 int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float *W2, int Cout,
                         const float *bias, int relu, float *Y, hipStream_t s) {
@@ -214,8 +224,10 @@ int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float 
     if (!conv3x3_mfma_supported(C, Cout)) return VD_ERR_SHAPE;
     if (M * C * 4 >= 0x7ffffff0ll || (int64_t)Cout * 9 * C * 4 >= 0x7ffffff0ll)
         return VD_ERR_SHAPE;  // 32-bit buffer offsets
-    const int64_t mtiles = (M + kTM - 1) / kTM;
-    const int64_t blocks = (mtiles + 7) / 8 * 8 * (Cout / kTN);
+    const bool narrow = Cout == 64;  // 256 x 64 tiles (res2's 64-channel conv2)
+    const int tm = narrow ? 256 : kTM, tn = narrow ? 64 : kTN;
+    const int64_t mtiles = (M + tm - 1) / tm;
+    const int64_t blocks = (mtiles + 7) / 8 * 8 * (Cout / tn);
     if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
     // variant: 1 = K chunk 64, one LDS stage (64 KiB); 2 = K chunk 32, two stages
     // (64 KiB); both two workgroups per CU.  Measured equal within 1 %; raising the
@@ -225,7 +237,11 @@ int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float 
     void (*kern)(const float *, int, int, int, int, const float *, int, const float *, float *,
                  int);
     size_t lds;
-    if (v == 2) {
+    if (narrow) {
+        kern = relu ? conv3x3_mfma_kernel<true, 64, 1, 256, 64>
+                    : conv3x3_mfma_kernel<false, 64, 1, 256, 64>;
+        lds = (size_t)(256 + 64) * 16 * sizeof(float4);  // 80 KiB
+    } else if (v == 2) {
         kern = relu ? conv3x3_mfma_kernel<true, 32, 2> : conv3x3_mfma_kernel<false, 32, 2>;
         lds = 2 * (size_t)(kTM + kTN) * 8 * sizeof(float4);
     } else {

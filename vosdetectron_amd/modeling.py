@@ -139,7 +139,7 @@ class Bottleneck(nn.Module):
             out = _gemm_conv1x1(x, self.w1, self.f1.bias, relu=True)
         else:
             out = _conv_epi(self.f1, x)
-        y = _conv3x3_mfma(self.f2, out, relu=True)  # res3's 128-channel 3x3 (>= 2^18 px)
+        y = _conv3x3_mfma(self.f2, out, relu=True)  # res2 / res3 3x3s (>= 2^18 px)
         out = y if y is not None else _conv_epi(self.f2, out)
         if self.downsample is not None:
             if self.fd.stride == (1, 1) and x.is_contiguous(memory_format=torch.channels_last):
