@@ -46,15 +46,20 @@ __device__ __forceinline__ int swz(int r) {
 
 // TM x TN: the workgroup tile (pixels x output channels), 4 waves of 64 x 64:
 // 128 x 128 (2 x 2 waves) or 256 x 64 (4 x 1, for Cout = 64).
-template <bool RELU, int KC, int STAGES, int TM = kTM, int TN = kTN>
-__global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
+// WTP x WTC: a wave's 16 x 16 MFMA tiles along pixels x channels (4 x 4 = 64 x 64;
+// 2 x 4 = 32 x 64 for the 64 x 128 workgroup tile of the mid-size shapes, which
+// runs three workgroups per CU).
+template <bool RELU, int KC, int STAGES, int TM = kTM, int TN = kTN, int WTP = 4, int WTC = 4,
+          int WGS = 2>
+__global__ __launch_bounds__(256, WGS) void conv3x3_mfma_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ W2,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int mtiles) {
     constexpr int R4 = KC / 4;               // float4s per staged row
     constexpr int STAGE = (TM + TN) * R4;    // float4s per stage
     constexpr int RP = 256 / R4;             // rows per staging pass
     constexpr int NI = TM / RP, NB = TN / RP;  // passes for pixel / weight rows
-    constexpr int WPX = TM / 64;             // waves along the pixels
+    constexpr int WPX = TM / (16 * WTP);     // waves along the pixels
+    static_assert(WPX * (TN / (16 * WTC)) == 4, "four waves per workgroup");
     extern __shared__ __attribute__((aligned(16))) float4 lds[];  // [STAGES][TM + TN][R4]
     const int64_t M = (int64_t)N * H * W;
     const int tid = threadIdx.x, lane = lane_id(), wave = wave_id();
@@ -89,12 +94,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float *>(W2), (short)0, Cout * K9 * 4, 0x00020000);
     const int wrow0 = (n0 + sr0) * K9 + 4 * sc;
-    f4v acc[4][4];
+    f4v acc[WTC][WTP];
 #pragma unroll
-    for (int tc = 0; tc < 4; ++tc)
+    for (int tc = 0; tc < WTC; ++tc)
 #pragma unroll
-        for (int tp = 0; tp < 4; ++tp) acc[tc][tp] = f4v{0.f, 0.f, 0.f, 0.f};
-    const int pw0 = (wave % WPX) * 64, cw0 = (wave / WPX) * 64;
+        for (int tp = 0; tp < WTP; ++tp) acc[tc][tp] = f4v{0.f, 0.f, 0.f, 0.f};
+    const int pw0 = (wave % WPX) * 16 * WTP, cw0 = (wave / WPX) * 16 * WTC;
     // chunk ch = (tap, channel block): its pixel / weight float4s in registers
 #define VD_LOAD_CHUNK(CH)                                                                   \
     {                                                                                       \
@@ -146,27 +151,25 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
         const float4 *a = lds + buf * STAGE;
         const float4 *b = a + TM * R4;
         // fragments of block kb + 1 are read while block kb's MFMAs run
-        float4 pf[4], wf[4];
+        float4 pf[WTP], wf[WTC];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            pf[t] = a[(pw0 + 16 * t + j) * R4 + (q ^ swz<KC>(j))];
-            wf[t] = b[(cw0 + 16 * t + j) * R4 + (q ^ swz<KC>(j))];
-        }
+        for (int t = 0; t < WTP; ++t) pf[t] = a[(pw0 + 16 * t + j) * R4 + (q ^ swz<KC>(j))];
+#pragma unroll
+        for (int t = 0; t < WTC; ++t) wf[t] = b[(cw0 + 16 * t + j) * R4 + (q ^ swz<KC>(j))];
 #pragma unroll
         for (int kb = 0; kb < KC / 16; ++kb) {
-            float4 pn[4], wn[4];
+            float4 pn[WTP], wn[WTC];
             if (kb + 1 < KC / 16) {
                 const int c = ((kb + 1) * 4 + q) ^ swz<KC>(j);
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    pn[t] = a[(pw0 + 16 * t + j) * R4 + c];
-                    wn[t] = b[(cw0 + 16 * t + j) * R4 + c];
-                }
+                for (int t = 0; t < WTP; ++t) pn[t] = a[(pw0 + 16 * t + j) * R4 + c];
+#pragma unroll
+                for (int t = 0; t < WTC; ++t) wn[t] = b[(cw0 + 16 * t + j) * R4 + c];
             }
             // component-major: 16 independent accumulators between two uses of one
 #define VD_MF(COMP)                                                                         \
-    _Pragma("unroll") for (int tc = 0; tc < 4; ++tc)                                        \
-        _Pragma("unroll") for (int tp = 0; tp < 4; ++tp) acc[tc][tp] =                      \
+    _Pragma("unroll") for (int tc = 0; tc < WTC; ++tc)                                      \
+        _Pragma("unroll") for (int tp = 0; tp < WTP; ++tp) acc[tc][tp] =                    \
             __builtin_amdgcn_mfma_f32_16x16x4f32(wf[tc].COMP, pf[tp].COMP, acc[tc][tp], 0, 0, 0);
             VD_MF(x)
             VD_MF(y)
@@ -175,10 +178,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
 #undef VD_MF
             if (kb + 1 < KC / 16) {
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    pf[t] = pn[t];
-                    wf[t] = wn[t];
-                }
+                for (int t = 0; t < WTP; ++t) pf[t] = pn[t];
+#pragma unroll
+                for (int t = 0; t < WTC; ++t) wf[t] = wn[t];
             }
         }
         if (STAGES == 1) __syncthreads();  // every wave is done reading the stage
@@ -190,12 +192,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_kernel(
     // epilogue: lane (j, q), tile (tc, tp) holds channels n0 + cw0 + 16 tc + 4 q .. + 3
     // of pixel m0 + pw0 + 16 tp + j
 #pragma unroll
-    for (int tc = 0; tc < 4; ++tc) {
+    for (int tc = 0; tc < WTC; ++tc) {
         const int co = n0 + cw0 + 16 * tc + 4 * q;
         const float4 bv = bias ? *reinterpret_cast<const float4 *>(bias + co)
                                : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int tp = 0; tp < 4; ++tp) {
+        for (int tp = 0; tp < WTP; ++tp) {
             const int64_t m = m0 + pw0 + 16 * tp + j;
             if (m >= M) continue;
             float4 o = make_float4(acc[tc][tp][0] + bv.x, acc[tc][tp][1] + bv.y,
@@ -225,7 +227,12 @@ int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float 
     if (M * C * 4 >= 0x7ffffff0ll || (int64_t)Cout * 9 * C * 4 >= 0x7ffffff0ll)
         return VD_ERR_SHAPE;  // 32-bit buffer offsets
     const bool narrow = Cout == 64;  // 256 x 64 tiles (res2's 64-channel conv2)
-    const int tm = narrow ? 256 : kTM, tn = narrow ? 64 : kTN;
+    // mid-size shapes (fewer than 8 rounds of 128 x 128 tiles over 512 slots):
+    // 64 x 128 tiles, three workgroups per CU
+    const char *em = getenv("VOSDET_CONV3X3_MID");
+    const int64_t big_tiles = (M + kTM - 1) / kTM * (Cout / kTN);
+    const bool mid = !narrow && (em ? atoi(em) != 0 : big_tiles < 4096);
+    const int tm = narrow ? 256 : (mid ? 64 : kTM), tn = narrow ? 64 : kTN;
     const int64_t mtiles = (M + tm - 1) / tm;
     const int64_t blocks = (mtiles + 7) / 8 * 8 * (Cout / tn);
     if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
@@ -241,6 +248,10 @@ int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float 
         kern = relu ? conv3x3_mfma_kernel<true, 64, 1, 256, 64>
                     : conv3x3_mfma_kernel<false, 64, 1, 256, 64>;
         lds = (size_t)(256 + 64) * 16 * sizeof(float4);  // 80 KiB
+    } else if (mid) {
+        kern = relu ? conv3x3_mfma_kernel<true, 64, 1, 64, 128, 2, 4, 3>
+                    : conv3x3_mfma_kernel<false, 64, 1, 64, 128, 2, 4, 3>;
+        lds = (size_t)(64 + 128) * 16 * sizeof(float4);  // 48 KiB: three per CU
     } else if (v == 2) {
         kern = relu ? conv3x3_mfma_kernel<true, 32, 2> : conv3x3_mfma_kernel<false, 32, 2>;
         lds = 2 * (size_t)(kTM + kTN) * 8 * sizeof(float4);
