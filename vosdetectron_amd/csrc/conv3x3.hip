@@ -231,7 +231,7 @@ int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float 
     // 64 x 128 tiles, three workgroups per CU
     const char *em = getenv("VOSDET_CONV3X3_MID");
     const int64_t big_tiles = (M + kTM - 1) / kTM * (Cout / kTN);
-    const bool mid = !narrow && (em ? atoi(em) != 0 : big_tiles < 4096);
+    const bool mid = !narrow && em && atoi(em) != 0 && big_tiles < 4096;  // opt-in (A/B)
     const int tm = narrow ? 256 : (mid ? 64 : kTM), tn = narrow ? 64 : kTN;
     const int64_t mtiles = (M + tm - 1) / tm;
     const int64_t blocks = (mtiles + 7) / 8 * 8 * (Cout / tn);
