@@ -1,0 +1,37 @@
+"""bench.py's measurement arithmetic on the CPU (no GPU): the SURVEY 8(d) step
+roofline, the RoIAlign algorithmic-byte formula and the CPU-share probe."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+
+def test_step_roofline_sums_stage_bounds():
+    r = bench.step_roofline(528e9, 100, 16, 72.0, {"algorithmic_bytes_per_launch": 2.0e9},
+                            (800, 1333), (800, 1344))
+    mfma_ms = 528e9 * 16 / 157.3e12 * 1e3
+    blob = 16 * (800 * 1333 * 3 + 3 * 4 * 800 * 1344)
+    hbm_ms = (blob + 2.0e9) / 8e12 * 1e3
+    assert abs(r["mfma_bound_ms"] - round(mfma_ms, 3)) < 1e-6
+    assert abs(r["hbm_bound_ms"] - round(hbm_ms, 3)) < 1e-6
+    assert abs(r["frac"] - round((mfma_ms + hbm_ms) / 72.0, 4)) < 1e-9
+    assert r["frac"] < 1.0
+
+
+def test_roi_align_algorithmic_bytes_counts_union_once():
+    # two identical RoIs on level 0 (P2): the footprint is counted once, outputs twice
+    rois = np.array([[0, 8, 8, 40, 40], [0, 8, 8, 40, 40]], np.float32)
+    lv = np.zeros(2, np.int32)
+    C, P = 4, 7
+    got = bench.roi_align_algorithmic_bytes(rois, lv, [(200, 336), (1, 1), (1, 1), (1, 1)], C, P)
+    # scale 1/4: [2, 10] x [2, 10] -> rows/cols floor(2)..floor(10)+1 = 2..11 inclusive
+    touched = 10 * 10
+    assert got == 4 * C * touched + 2 * 4 * C * P * P + 2 * 20
+
+
+def test_cpu_share_is_positive():
+    n, caps = bench.cpu_share()
+    assert n >= 1 and "affinity" in caps
