@@ -25,6 +25,9 @@
 // / 16) of its row in both operands: a K permutation shared by A and B.
 #include <stdlib.h>
 
+#include <mutex>
+#include <set>
+
 #include "common.hpp"
 #include "vosdet_internal.hpp"
 
@@ -213,6 +216,19 @@ __global__ __launch_bounds__(256, WGS) void conv3x3_mfma_kernel(
     }
 }
 
+// The dynamic-LDS opt-in (> 64 KiB) once per kernel instance, not per launch.
+bool allow_lds(const void *kern, size_t lds) {
+    static std::mutex mu;
+    static std::set<const void *> done;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.count(kern)) return true;
+    if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+        hipSuccess)
+        return false;
+    done.insert(kern);
+    return true;
+}
+
 }  // namespace
 
 bool conv3x3_mfma_supported(int C, int Cout) {
@@ -259,9 +275,7 @@ int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float 
         kern = relu ? conv3x3_mfma_kernel<true, 64, 1> : conv3x3_mfma_kernel<false, 64, 1>;
         lds = (size_t)(kTM + kTN) * 16 * sizeof(float4);
     }
-    if (hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-        return VD_ERR_LAUNCH;
+    if (!allow_lds(reinterpret_cast<const void *>(kern), lds)) return VD_ERR_LAUNCH;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, s, X, N, H, W, C, W2, Cout,
                        bias, Y, (int)mtiles);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
