@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
                                           (5, 256, 7, 7, 384), (2, 64, 30, 41, 64),
                                           (1, 128, 5, 3, 64)])
 @pytest.mark.parametrize("relu", [False, True])
-@pytest.mark.parametrize("variant", ["1", "2"])
+@pytest.mark.parametrize("variant", ["1", "2", "6"])
 def test_conv3x3_vs_torch(monkeypatch, N, C, H, W, Cout, relu, variant):
     from vosdetectron_amd import ops
     monkeypatch.setenv("VOSDET_CONV3X3_VARIANT", variant)

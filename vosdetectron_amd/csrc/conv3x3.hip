@@ -252,11 +252,14 @@ int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float 
     const int64_t mtiles = (M + tm - 1) / tm;
     const int64_t blocks = (mtiles + 7) / 8 * 8 * (Cout / tn);
     if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
-    // variant: 1 = K chunk 64, one LDS stage (64 KiB); 2 = K chunk 32, two stages
-    // (64 KiB); both two workgroups per CU.  Measured equal within 1 %; raising the
-    // wave priority over the MFMA phase (s_setprio) cost 1-4 % (profiles/r02c/README.md)
+    // variant (profiles/r02c/README.md): 6 (default) = K chunk 32, one 32 KiB stage,
+    // THREE workgroups per CU -- while one stores its next chunk between its two
+    // barriers, two others keep the MFMA pipes fed (0.87 of peak at P2); 1 = K chunk
+    // 64, one 64 KiB stage, two per CU (0.84); 2 = K chunk 32 double-buffered, two
+    // per CU (0.84).  Four per CU spills (0.69); one double-buffered per CU 0.73;
+    // s_setprio over the MFMA phase cost 1-4 %.
     const char *e = getenv("VOSDET_CONV3X3_VARIANT");
-    const int v = e ? atoi(e) : 1;
+    const int v = e ? atoi(e) : 6;
     void (*kern)(const float *, int, int, int, int, const float *, int, const float *, float *,
                  int);
     size_t lds;
@@ -268,6 +271,10 @@ int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float 
         kern = relu ? conv3x3_mfma_kernel<true, 64, 1, 64, 128, 2, 4, 3>
                     : conv3x3_mfma_kernel<false, 64, 1, 64, 128, 2, 4, 3>;
         lds = (size_t)(64 + 128) * 16 * sizeof(float4);  // 48 KiB: three per CU
+    } else if (v == 6) {  // K chunk 32, one 32 KiB stage, three workgroups per CU
+        kern = relu ? conv3x3_mfma_kernel<true, 32, 1, kTM, kTN, 4, 4, 3>
+                    : conv3x3_mfma_kernel<false, 32, 1, kTM, kTN, 4, 4, 3>;
+        lds = (size_t)(kTM + kTN) * 8 * sizeof(float4);
     } else if (v == 2) {
         kern = relu ? conv3x3_mfma_kernel<true, 32, 2> : conv3x3_mfma_kernel<false, 32, 2>;
         lds = 2 * (size_t)(kTM + kTN) * 8 * sizeof(float4);
