@@ -42,3 +42,35 @@ def test_config_matches_reference_yaml(name):
         if isinstance(a, (list, tuple)):
             a, b = tuple(a), tuple(b)
         assert a == b, (name, k, a, b)
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree absent")
+@pytest.mark.parametrize("yml,keys", [
+    ("configs/baselines/e2e_mask_rcnn_X-152-32x8d-FPN-IN5k_1.44x.yaml",
+     ["TEST.BBOX_VOTE.ENABLED", "TEST.BBOX_AUG.ENABLED", "TEST.MASK_AUG.ENABLED"]),
+    ("lib_vos/tools/R-101-FPN_3x_gn_train_online.yaml", ["TEST.NMS_WITH_MASK_IOU"]),
+])
+def test_unsupported_options_raise(yml, keys):
+    """A reference YAML that enables an inference option this path does not build
+    (box voting, TTA, mask-IoU NMS, ...) raises and names the keys, through both
+    load_cfg and merge_cfg_from_file; the global cfg is left unchanged."""
+    path = os.path.join(REF, yml)
+    with pytest.raises(NotImplementedError) as e:
+        vcfg.load_cfg(path)
+    for k in keys:
+        assert k in str(e.value), (k, str(e.value))
+    before = vcfg.copy.deepcopy(vcfg.cfg)
+    with pytest.raises(NotImplementedError):
+        vcfg.merge_cfg_from_file(path)
+    assert vcfg.cfg == before
+
+
+def test_unsupported_overrides_raise():
+    for key, val in (("TEST.SOFT_NMS.ENABLED", True), ("TEST.NMS_SMALL_BOX_IOU", 0.5),
+                     ("MODEL.USE_DELTA_FLOW", True), ("TEST.KPS_AUG.ENABLED", True)):
+        with pytest.raises(NotImplementedError, match=key.replace(".", r"\.")):
+            vcfg.load_cfg(overrides={key: val})
+    with pytest.raises(NotImplementedError, match="NMS_WITH_MASK_IOU"):
+        vcfg.merge_cfg_from_list(["TEST.NMS_WITH_MASK_IOU", "1.0"])
+    # disabled values are accepted
+    vcfg.load_cfg(overrides={"TEST.NMS_SMALL_BOX_IOU": 0., "TEST.BBOX_VOTE.ENABLED": False})

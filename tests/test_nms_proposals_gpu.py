@@ -43,6 +43,24 @@ def test_nms_edge_cases():
     assert ops.nms(torch.from_numpy(d).to(DEV), 0.5).cpu().tolist() == [0]
 
 
+def test_nms_vs_executed_reference(golden):
+    """vd_nms (ops.nms) and the ndarray drop-in boxes.nms against the EXECUTED
+    reference cython_nms.nms (tests/golden/nms.npz, tools/ref_cython_nms.py):
+    tie-free sets at N in {1, 64, 65, 1000, 4381, 5000} x {0.3, 0.5, 0.7},
+    exact-threshold IoU pairs, and tie sets given the reference's processing
+    order.  Bit-exact index selection (north_star)."""
+    from tests.test_oracle_golden import _nms_cases
+    from vosdetectron_amd import boxes, ops
+    g = golden("nms")
+    n_cases = 0
+    for kind, d, thr, keep in _nms_cases(g):
+        out = ops.nms(torch.from_numpy(d).to(DEV), thr).cpu().numpy()
+        assert np.array_equal(out, keep), (kind, len(d), thr)
+        assert np.array_equal(np.asarray(boxes.nms(d, thr), np.int64), keep), (kind, len(d))
+        n_cases += 1
+    assert n_cases == int(g["count"])
+
+
 def test_fpn_levels_golden(golden):
     from vosdetectron_amd import ops
     g = golden("fpn_levels")

@@ -118,3 +118,40 @@ def test_tie_study_fixture(golden):
             assert np.array_equal(key(r), key(ref)), tag
             checked += 1
     assert checked >= 2
+
+
+def _nms_cases(g):
+    """(dets, thresh, expected keep, rescored dets) per case of tests/golden/nms.npz.
+
+    Tie cases carry the reference's own processing order (numpy's argsort on the
+    generating host); rescoring each row by its rank in that order makes the
+    order tie-free without changing the boxes, so an NMS with any tie rule must
+    then reproduce the reference's keep exactly."""
+    for i in range(int(g["count"])):
+        d, thr, keep = g["dets_%d" % i], float(g["thresh_%d" % i]), g["keep_%d" % i]
+        kind = str(g["kind_%d" % i])
+        if kind == "ties":
+            order = g["order_%d" % i]
+            n = len(d)
+            rank = np.empty(n, np.float64)
+            rank[order] = np.arange(n)[::-1]
+            d = d.copy()
+            d[:, 4] = ((rank + 1) / n).astype(np.float32)
+        yield kind, d, thr, keep
+
+
+def test_nms_vs_executed_reference(golden):
+    """The oracle's NMS (oracle/roi_ops.c) against the executed reference
+    cython_nms.nms (tools/ref_cython_nms.py -> tests/golden/nms.npz): tie-free
+    sets up to 5000 boxes, exact-threshold IoU pairs, and tie sets given the
+    reference's processing order.  Bit-exact index selection."""
+    g = golden("nms")
+    kinds = set()
+    for kind, d, thr, keep in _nms_cases(g):
+        assert np.array_equal(orc.nms(d, thr), keep), (kind, len(d), thr)
+        kinds.add(kind)
+    assert kinds == {"tie_free", "exact_threshold", "ties"}
+    # exact threshold: IoU == fl32(thr) suppresses, a hair below keeps
+    for i in range(int(g["count"])):
+        if str(g["kind_%d" % i]) == "exact_threshold":
+            assert g["keep_%d" % i].tolist() == [0, 2, 3, 4]

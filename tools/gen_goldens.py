@@ -10,12 +10,15 @@ Runtime-only import shims (nothing under /root/reference is modified):
   * ``np.float`` / ``np.int`` aliases (removed in numpy >= 1.24; used by
     generate_anchors.py:63,72, core/test.py:904-905);
   * ``torch._six`` stub (lib/nn/parallel/scatter_gather.py:7);
-  * ``utils.cython_nms`` / ``utils.cython_bbox``: the vendored Cython does not
-    build against numpy 2, so ``nms`` is bound to the oracle's C restatement
-    (oracle/roi_ops.c).  Fixtures that run through NMS therefore pin everything
-    around the NMS call (top-k, decode, clip, filter, keep[:post]) to the
-    reference, and the NMS itself to the oracle.  This is recorded in
-    DESIGN.md ("Parity").
+  * ``utils.cython_nms``: the REFERENCE's own ``lib/utils/cython_nms.pyx``,
+    compiled by tools/ref_cython_nms.py from a /tmp scratch copy with the
+    two-token dtype substitution of SURVEY Appendix A (``np.int_t`` ->
+    ``np.intp_t``, ``dtype=np.int)`` -> ``dtype=np.intp)``: the same 64-bit
+    integer on Linux; numpy 2's .pxd dropped the old spelling).  Every fixture
+    that runs through NMS (proposals, C4 proposals, collect/distribute, the
+    fork's post-filter) therefore runs the executed reference NMS, and
+    ``nms.npz`` pins it directly.  ``utils.cython_bbox`` is not on the
+    inference path and stays a stub.
   * ``cv2`` / ``pycocotools`` stubs (imported at module level by core/test.py,
     never called on the functions used here).
 
@@ -44,10 +47,9 @@ def install_shims():
     import torch.utils.data.dataloader as dl
     if not hasattr(dl, "numpy_type_map"):
         dl.numpy_type_map = {}
-    from oracle import oracle as orc
-    cy_nms = types.ModuleType("utils.cython_nms")
-    cy_nms.nms = lambda dets, thresh: orc.nms(dets, thresh)
-    sys.modules["utils.cython_nms"] = cy_nms
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from ref_cython_nms import load as load_ref_nms
+    sys.modules["utils.cython_nms"] = load_ref_nms()
     cy_bbox = types.ModuleType("utils.cython_bbox")
     cy_bbox.bbox_overlaps = None  # not on the inference path
     sys.modules["utils.cython_bbox"] = cy_bbox
@@ -235,7 +237,85 @@ def main():
     cfg.TEST.NMS_CROSS_CLASS, cfg.TEST.NUM_DET_PER_CLASS_PRE = 0., 0
     np.savez(os.path.join(OUT, "detections_postfilter.npz"), **post)
 
+    gen_nms_fixture(sys.modules["utils.cython_nms"])
     print("wrote", sorted(os.listdir(OUT)))
+
+
+def _clustered_dets(rng, n, span=1300.):
+    """RPN / class-NMS-like boxes: jittered copies around n/8+1 centres (heavy
+    overlap) mixed with free boxes; 1-2 px boxes and exact duplicates included."""
+    k = max(1, n // 8)
+    centres = np.hstack([rng.uniform(0, span, (k, 2)), rng.uniform(4, 300, (k, 2))])
+    pick = rng.integers(0, k, n)
+    c = centres[pick]
+    jit = rng.normal(0, 1, (n, 4)) * (0.08 * c[:, 2:4].repeat(2, 1))
+    x1 = c[:, 0] - c[:, 2] / 2 + jit[:, 0]
+    y1 = c[:, 1] - c[:, 3] / 2 + jit[:, 1]
+    x2 = c[:, 0] + c[:, 2] / 2 + jit[:, 2]
+    y2 = c[:, 1] + c[:, 3] / 2 + jit[:, 3]
+    free = rng.uniform(0, 1, n) < 0.25
+    fxy = rng.uniform(0, span, (n, 2))
+    fwh = rng.uniform(0, 150, (n, 2))
+    x1 = np.where(free, fxy[:, 0], x1)
+    y1 = np.where(free, fxy[:, 1], y1)
+    x2 = np.where(free, fxy[:, 0] + fwh[:, 0], np.maximum(x2, x1))
+    y2 = np.where(free, fxy[:, 1] + fwh[:, 1], np.maximum(y2, y1))
+    d = np.stack([x1, y1, x2, y2, np.zeros(n)], 1).astype(np.float32)
+    if n >= 8:
+        d[1] = d[0]                        # exact duplicate box
+        d[2, 2:4] = d[2, 0:2]              # 1x1 box (+1 convention)
+    return d
+
+
+def gen_nms_fixture(cy):
+    """tests/golden/nms.npz: the executed reference ``cython_nms.nms``
+    (lib/utils/cython_nms.pyx:37-87) on
+      * tie-free sets at N in {1, 64, 65, 1000, 4381, 5000} x thresh {0.3, 0.5, 0.7};
+      * exact-threshold IoU pairs (IoU == fl32(thresh) suppresses, one ulp
+        below does not) at each threshold;
+      * tie-bearing sets (scores quantised to 1/8): the reference's keep AND its
+        processing order ``scores.argsort()[::-1]`` as numpy computed it on the
+        generating host.  Tie order is host-dependent (numpy's unstable SIMD
+        argsort), so the tests pin the NMS given that
+        order: rescoring the rows by their rank in ``order`` must reproduce
+        ``keep`` bit for bit."""
+    rng = np.random.default_rng(20261017)
+    out, i = {}, 0
+    for n in (1, 64, 65, 1000, 4381, 5000):
+        for thr in (0.3, 0.5, 0.7):
+            d = _clustered_dets(rng, n)
+            d[:, 4] = distinct_scores(rng, n) if n > 1 else np.float32(0.5)
+            out["dets_%d" % i] = d
+            out["thresh_%d" % i] = np.float32(thr)
+            out["keep_%d" % i] = np.asarray(cy.nms(d, np.float32(thr)), np.int64)
+            out["kind_%d" % i] = np.array("tie_free")
+            i += 1
+    # exact-threshold pairs: a 10x10 box against 10 x h boxes inside it,
+    # IoU = 10h / 100 exactly representable as fl32(h / 10)
+    for thr, h in ((0.3, 3), (0.5, 5), (0.7, 7)):
+        rows = [[0, 0, 9, 9, 0.9],
+                [0, 0, 9, h - 1, 0.8],          # IoU == fl32(thr): suppressed
+                [40, 0, 49, 9, 0.7],
+                [40, 0, 49, h - 1 - 1e-3, 0.6],  # IoU a hair below: kept
+                [80, 0, 89, 9, 0.5],
+                [80, 0, 89, h - 1 + 1e-3, 0.4]]  # a hair above: suppressed
+        d = np.array(rows, np.float32)
+        out["dets_%d" % i] = d
+        out["thresh_%d" % i] = np.float32(thr)
+        out["keep_%d" % i] = np.asarray(cy.nms(d, np.float32(thr)), np.int64)
+        out["kind_%d" % i] = np.array("exact_threshold")
+        i += 1
+    for n, thr in ((5, 0.5), (16, 0.5), (17, 0.7), (300, 0.3), (1000, 0.7), (3000, 0.5)):
+        d = _clustered_dets(rng, n)
+        d[:, 4] = np.round(rng.uniform(0, 1, n) * 8) / 8
+        out["dets_%d" % i] = d
+        out["thresh_%d" % i] = np.float32(thr)
+        out["keep_%d" % i] = np.asarray(cy.nms(d, np.float32(thr)), np.int64)
+        out["order_%d" % i] = d[:, 4].argsort()[::-1].astype(np.int64)
+        out["kind_%d" % i] = np.array("ties")
+        i += 1
+    out["count"] = np.int64(i)
+    np.savez_compressed(os.path.join(OUT, "nms.npz"), **out)
 
 
 if __name__ == "__main__":

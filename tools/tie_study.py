@@ -9,8 +9,8 @@ record what numpy's unstable sorts do on this host.
 
 Writes tests/golden/proposals_ties.npz (inputs + reference outputs) and
 tests/golden/proposals_ties.json (summary).  Container-only: imports the
-reference through tools/gen_goldens.py's runtime shims (NMS bound to the oracle's
-C NMS, as for the other proposal fixtures).
+reference through tools/gen_goldens.py's runtime shims (NMS = the reference's own
+cython_nms.pyx, built by tools/ref_cython_nms.py, as for the other fixtures).
 
 Usage: python tools/tie_study.py
 """

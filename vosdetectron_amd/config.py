@@ -1,8 +1,11 @@
 """Configuration: the subset of the reference's global ``cfg`` (lib/core/config.py)
 that the per-frame inference hot path reads, with the reference's defaults, and
 a YAML merge that accepts the reference's own config files unchanged
-(merge_cfg_from_file, config.py:1107-1113; unknown keys are ignored here
-because the training/dataset keys are out of scope).
+(merge_cfg_from_file, config.py:1107-1113).  Unknown keys are ignored (the
+training / dataset keys are out of scope), but a config that ENABLES an
+inference option this path does not implement raises NotImplementedError
+naming the keys (``UNSUPPORTED`` below) instead of silently running different
+semantics.
 """
 from __future__ import annotations
 
@@ -69,7 +72,12 @@ def default_cfg() -> AttrDict:
             SCALE=600, MAX_SIZE=1000, NMS=0.3, BBOX_REG=True, RPN_NMS_THRESH=0.7,
             RPN_PRE_NMS_TOP_N=12000, RPN_POST_NMS_TOP_N=2000, RPN_MIN_SIZE=0,
             DETECTIONS_PER_IM=100, SCORE_THRESH=0.05, NUM_DET_PER_CLASS_PRE=0,
-            NUM_DET_PER_CLASS_POST=0, NMS_CROSS_CLASS=0.),
+            NUM_DET_PER_CLASS_POST=0, NMS_CROSS_CLASS=0.,
+            # inference options read only to be rejected when enabled (UNSUPPORTED)
+            SOFT_NMS=_d(ENABLED=False), BBOX_VOTE=_d(ENABLED=False),  # config.py:356-383
+            BBOX_AUG=_d(ENABLED=False), MASK_AUG=_d(ENABLED=False),  # config.py:246-316
+            KPS_AUG=_d(ENABLED=False),  # config.py:322-351
+            NMS_WITH_MASK_IOU=0., NMS_SMALL_BOX_IOU=0.),  # config.py:951-952
         PIXEL_MEANS=(102.9801, 115.9465, 122.7717),  # config.py:1015
         BBOX_XFORM_CLIP=math.log(1000. / 16.),  # config.py:1009
         CROP_RESIZE_WITH_MAX_POOL=True,  # config.py:1058
@@ -100,8 +108,47 @@ def _merge(a, b):
             b[k] = v
 
 
+# Inference options of the reference that change detections and are not built
+# here: (dotted key, "enabled" predicate, where the reference implements it).
+UNSUPPORTED = (
+    ("TEST.SOFT_NMS.ENABLED", bool, "soft-NMS, lib/utils/cython_nms.pyx:98-203, lib/core/test.py:755-766"),
+    ("TEST.BBOX_VOTE.ENABLED", bool, "box voting, lib/core/test.py:769-776, lib/utils/boxes.py:277-326"),
+    ("TEST.BBOX_AUG.ENABLED", bool, "box test-time augmentation, lib/core/test.py:193-727"),
+    ("TEST.MASK_AUG.ENABLED", bool, "mask test-time augmentation, lib/core/test.py:405-480"),
+    ("TEST.KPS_AUG.ENABLED", bool, "keypoint test-time augmentation (keypoint heads out of scope)"),
+    ("TEST.NMS_WITH_MASK_IOU", lambda v: float(v) > 0,
+     "mask-IoU NMS, lib_vos/tools/vos_test.py:113-118"),
+    ("TEST.NMS_SMALL_BOX_IOU", lambda v: float(v) > 0,
+     "small-box NMS against the previous frame, lib_vos/tools/vos_test.py:845-860"),
+    ("MODEL.USE_DELTA_FLOW", bool, "delta-flow VOS head, lib_vos/vos_modeling/vos_model_builder.py"),
+    ("MODEL.KEYPOINTS_ON", bool, "keypoint heads (out of scope)"),
+)
+
+
+def _get(cfg, key):
+    for p in key.split("."):
+        cfg = cfg[p]
+    return cfg
+
+
+def check_supported(cfg) -> None:
+    """Raise NotImplementedError naming every enabled option of ``UNSUPPORTED``."""
+    bad = []
+    for key, enabled, where in UNSUPPORTED:
+        try:
+            v = _get(cfg, key)
+        except (KeyError, TypeError):
+            continue
+        if enabled(v):
+            bad.append("%s=%r (%s)" % (key, v, where))
+    if bad:
+        raise NotImplementedError("inference options not implemented by vosdetectron_amd: "
+                                  + "; ".join(bad))
+
+
 def load_cfg(path: str | None = None, overrides: dict | None = None) -> AttrDict:
-    """Defaults, then a reference YAML (safe loader), then dotted overrides."""
+    """Defaults, then a reference YAML (safe loader), then dotted overrides.
+    Raises NotImplementedError if the result enables an ``UNSUPPORTED`` option."""
     cfg = default_cfg()
     if path:
         with open(path) as f:
@@ -112,6 +159,7 @@ def load_cfg(path: str | None = None, overrides: dict | None = None) -> AttrDict
         for p in parts[:-1]:
             d = d[p]
         d[parts[-1]] = val
+    check_supported(cfg)
     return cfg
 
 
@@ -224,9 +272,14 @@ cfg = e2e_mask_rcnn_R_50_FPN_1x()
 
 
 def merge_cfg_from_file(path: str) -> None:
-    """config.py:1107-1111: merge a reference YAML into the global cfg in place."""
+    """config.py:1107-1111: merge a reference YAML into the global cfg in place.
+    An ``UNSUPPORTED`` option raises and leaves the global cfg unchanged."""
     with open(path) as f:
-        _merge(yaml.safe_load(f) or {}, cfg)
+        new = copy.deepcopy(cfg)
+        _merge(yaml.safe_load(f) or {}, new)
+    check_supported(new)
+    cfg.clear()
+    cfg.update(new)
 
 
 cfg_from_file = merge_cfg_from_file  # config.py:1113
@@ -236,14 +289,18 @@ def merge_cfg_from_list(cfg_list) -> None:
     """config.py:1121-1144: ['TEST.NMS', '0.4', ...] key/value pairs."""
     if len(cfg_list) % 2:
         raise ValueError("cfg_list must hold key/value pairs")
+    new = copy.deepcopy(cfg)
     for key, val in zip(cfg_list[0::2], cfg_list[1::2]):
-        d = cfg
+        d = new
         parts = key.split(".")
         for p in parts[:-1]:
             d = d[p]
         if parts[-1] not in d:
             raise KeyError("Non-existent config key: %s" % key)
         d[parts[-1]] = _decode(val)
+    check_supported(new)
+    cfg.clear()
+    cfg.update(new)
 
 
 def use(name: str) -> AttrDict:
