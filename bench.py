@@ -397,6 +397,39 @@ def measure_segm(pipe, out, frames=16):
     return round((time.perf_counter() - t0) / k * 1e3, 3)
 
 
+def capture_graphs(pipe, slots, graphs, note):
+    """Capture one hipGraph of the whole step per frame slot (sync=False: no host
+    read inside).  Eager execution stays in place if capture fails."""
+    try:
+        for x in slots[:2]:
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                pipe.run(x, sync=False)  # warm on the capture stream
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g):
+                gout = pipe.run(x, sync=False)
+            torch.cuda.synchronize()
+            graphs[x.data_ptr()] = (g, gout)
+        note[0] = "captured"
+    except Exception as e:  # noqa: BLE001 -- report and run eagerly
+        graphs.clear()
+        note[0] = "capture failed: %s" % (str(e).splitlines()[0][:200],)
+        print("bench: hipGraph %s; running eagerly" % note[0], file=sys.stderr, flush=True)
+        torch.cuda.synchronize()
+
+
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
 def spawn_ranks(n):
     """`python bench.py --gpus N` without a launcher: start N ranks through
     torch.distributed.run (one process per GPU, like the reference's per-GPU
@@ -486,6 +519,11 @@ def main():
                          "timed region (SURVEY §8d)")
     ap.add_argument("--seq-len", type=int, default=50,
                     help="VOS configs: frames per synthetic sequence (hidden states reset)")
+    ap.add_argument("--no-graph", dest="graph", action="store_false",
+                    help="launch every step eagerly instead of replaying a captured hipGraph")
+    ap.add_argument("--rccl-gather", action="store_true",
+                    help="issue the per-step all-gather even at world 1 (forms a 1-rank "
+                         "RCCL group), so the collective is inside the timed step")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo rehearsal of the N-rank launch and gather (no GPU)")
     ap.add_argument("--share-gpu", action="store_true",
@@ -512,9 +550,13 @@ def main():
         return dry_run(args, dist.get_world_size(), rank)
     if args.share_gpu:
         local = 0
-    if world > 1:
+    if world > 1 or args.rccl_gather:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:  # a one-rank RCCL group (--rccl-gather): no launcher env
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local)
         if args.share_gpu:  # RCCL refuses two ranks on one device: gloo carries the rehearsal
             dist.init_process_group("gloo")
@@ -559,10 +601,19 @@ def main():
     any_frames = resident[0] if args.resident else uploader.dev[0]  # post-run measurements
     step_no = [0]
 
+    # FPN engines queue a step without any host read (sync=False): the mask
+    # batch has pipe.mask_rows(F) rows and the gather ships exactly those
+    asynchronous = hasattr(pipe, "mask_rows")
+    mask_rows = (pipe.mask_rows(F) if asynchronous
+                 else F * max(100, int(cfg.TEST.DETECTIONS_PER_IM)) + 64)
     gatherer = ResultGatherer(F, pipe.det_cap, cfg.MRCNN.RESOLUTION, world, dev,
-                              mask_rows=F * max(100, int(cfg.TEST.DETECTIONS_PER_IM)) + 64)
+                              mask_rows=mask_rows)
+    graphs = {}  # uploader slot -> (CUDAGraph, static output dict)
+    graph_note = [None]
+    use_graph = args.graph and asynchronous and not vos
 
     pending = [None]
+    prev_out = [None]
 
     def drain():  # the previous step's gather has landed (stream-ordered)
         if pending[0] is not None:
@@ -575,10 +626,22 @@ def main():
         if vos and t % args.seq_len == 0:
             pipe.reset()
         frames = resident[t % n_host] if args.resident else uploader.get(t, prefetch)
-        out = pipe.run(frames)
+        key = frames.data_ptr()
+        if key in graphs:  # replay the captured step (hipGraph: one launch, no host work)
+            g, gout = graphs[key]
+            g.replay()
+            out = dict(gout)
+        else:
+            out = pipe.run(frames, sync=not asynchronous)
         if not args.resident:
             uploader.release(t)
-        if world > 1:
+        if asynchronous:
+            # the previous step's one host read (counts, capacity, rare overflow
+            # masks) while this step runs on the GPU
+            if prev_out[0] is not None:
+                pipe.complete(prev_out[0])
+            prev_out[0] = out
+        if gatherer.collective:
             # ONE packed all_gather per step over RCCL (runner.py), left in flight
             # on RCCL's stream while the next step computes; at most one in flight
             drain()
@@ -606,6 +669,10 @@ def main():
                   file=sys.stderr, flush=True)
     drain()
     torch.cuda.synchronize()
+    if use_graph:
+        capture_graphs(pipe, uploader.dev if not args.resident else resident, graphs,
+                       graph_note)
+        step_no[0] = 0  # restart the upload cycle at slot 0 for the timed region
     warm_done.set()
     if world > 1:
         dist.barrier()
@@ -623,6 +690,9 @@ def main():
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    if asynchronous:
+        pipe.complete(prev_out[0])
+        out = prev_out[0]
     dets_per_frame = float(np.mean(out["counts_host"]))
 
     stages = None
@@ -683,7 +753,10 @@ def main():
                        "frames_per_gpu_step": F, "global_batch": world * F,
                        "parallelism": "frame-sharded dp%d + RCCL all_gather" % world,
                        "layout": args.layout, "dets_per_frame": dets_per_frame, "h2d": h2d,
-                       "gather_bytes_per_rank": gatherer.bytes_per_rank if world > 1 else 0},
+                       "gather_bytes_per_rank": gatherer.bytes_per_rank
+                       if gatherer.collective else 0,
+                       "launch": "hipGraph replay per step" if graphs else
+                       ("eager (%s)" % graph_note[0] if graph_note[0] else "eager")},
             "roofline": roof, "cpu_baseline": cpu,
         }
         if args.share_gpu:

@@ -173,6 +173,22 @@ int vd_map_rois_to_fpn_levels(const float *rois, int roi_stride, int col0, int R
                               int k_max, float canonical_scale, float canonical_level,
                               int32_t *lvl_out, void *stream);
 
+/* The mask-head batch of im_detect_mask for all frames of a step, sized
+ * without a host read of the detection counts (lib/core/test.py:366-402:
+ * _get_rois_blob :877-906 -- box * im_scale as a float64 product stored as
+ * float32 -- and _add_multilevel_rois_for_test :909-927).  Detection j of
+ * frame f (j < counts[f], vd_box_detections' outputs) is global row
+ * prefix(counts)[f] + j, frame-major; rows [row0, row0 + rows) are written:
+ * rois_out [rows][5] = (f, x1, y1, x2, y2), lvl_out = FPN level - k_min,
+ * cls_out = its class.  Output rows past the total are padding (zero box,
+ * level 0, class 1).  total_out[0] = sum(counts) (may exceed row0 + rows: the
+ * caller runs a second batch from row0 = rows for those).  im_scale: F doubles. */
+int vd_mask_rois(const float *dets, const int32_t *classes, const int32_t *counts,
+                 int num_images, int det_cap, const double *im_scale, int row0, int rows,
+                 int k_min, int k_max, float canonical_scale, float canonical_level,
+                 float *rois_out, int32_t *lvl_out, int32_t *cls_out, int32_t *total_out,
+                 void *stream);
+
 /* ---------------------------------------------------------------------------
  * RPN proposals for all FPN levels and images in one launch: per (image,
  * level) GenerateProposalsOp.forward / proposals_for_one_image

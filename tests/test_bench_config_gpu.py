@@ -1,0 +1,125 @@
+"""The configuration bench.py measures, tested as benched.
+
+bench.py runs e2e_mask_rcnn_R-50-FPN_1x at 16 synthetic 800x1333 frames per
+step on the channels_last engine.  At that batch the P2/P3 convolutions cross
+the 2^18-pixel routing threshold (modeling._conv3x3_mfma) and run on the
+hand-written MFMA implicit GEMM (csrc/conv3x3.hip) and the 1x1 GEMMs run at
+M = 1,075,200 pixels; batch-1 pipeline tests never reach those routes.  Here:
+
+* FramePipeline(batch=16) on 16 distinct frames (bench.synthetic_frames, the
+  bench's own seeds and routes): stage-wise parity on frames 0, 7 and 15
+  (proposals + collect and detections bit-exact, box / mask RoIAlign within
+  1e-4 of the oracle's operator API) and e2e vs the independent CPU pipeline on
+  frames 0 and 15;
+* the MFMA 3x3 conv alone at the benched shapes (16,256,200,336),
+  (16,256,100,168) and the mask head's (1600,256,14,14), bias and no bias, vs
+  torch fp32;
+* the 1x1 GEMM epilogue path and the dual GEMM at M = 1,075,200.
+Reference: lib/core/test.py:50-111 (im_detect_all)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tests.engine_checks import e2e_vs_cpu, stagewise
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+BATCH = 16
+
+
+@pytest.fixture(scope="module")
+def bench_setup():
+    from bench import synthetic_frames
+    from vosdetectron_amd import config as vcfg
+    from vosdetectron_amd.engine import FramePipeline
+    from vosdetectron_amd.weights import build_model
+    cfg = vcfg.get("e2e_mask_rcnn_R-50-FPN_1x")
+    model, sd = build_model(cfg, seed=0, device=DEV, channels_last=True)
+    frames = synthetic_frames(BATCH, 1, 800, 1333)  # bench.py's first host batch
+    pipe = FramePipeline(model, cfg, batch=BATCH, channels_last=True, device=DEV)
+    out = pipe.run(torch.from_numpy(frames).to(DEV), keep_intermediates=True)
+    torch.cuda.synchronize()
+    return cfg, sd, pipe, frames, out
+
+
+def test_bench_batch_routes(bench_setup):
+    """The benched shapes take the hand-written routes (not a silent fallback)."""
+    from vosdetectron_amd import modeling
+    cfg, sd, pipe, frames, out = bench_setup
+    p2 = out["feats"][-1]
+    assert p2.shape == (BATCH, 256, 200, 336)
+    assert p2.is_contiguous(memory_format=torch.channels_last)
+    assert BATCH * 200 * 336 >= modeling._CONV3X3_MIN_PIXELS
+    assert all(int(c) > 0 for c in out["counts_host"])
+
+
+@pytest.mark.parametrize("f", [0, 7, 15])
+def test_bench_batch_stagewise(bench_setup, f):
+    cfg, sd, pipe, frames, out = bench_setup
+    rois, _ = stagewise(cfg, pipe, out, frames[f], f=f)
+    assert len(rois) == 1000
+
+
+@pytest.mark.parametrize("f", [0, 15])
+def test_bench_batch_e2e_vs_cpu(bench_setup, f):
+    from oracle.pipeline import RefCPUPipeline
+    cfg, sd, pipe, frames, out = bench_setup
+    torch.set_num_threads(16)
+    ref_out = RefCPUPipeline(sd)(frames[f])
+    e2e_vs_cpu(out, ref_out, f=f)
+
+
+@pytest.mark.parametrize("N,H,W", [(16, 200, 336), (16, 100, 168), (1600, 14, 14)])
+@pytest.mark.parametrize("bias", [True, False])
+def test_conv3x3_benched_shapes(N, H, W, bias):
+    """vd_conv3x3_bias_act (default variant) at the benched sizes vs torch fp32;
+    (16,256,200,336) is 1,075,200 pixels, half of the kernel's 32-bit offset guard."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(N + H)
+    x = torch.randn(N, 256, H, W, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    w = torch.randn(256, 256, 3, 3, device="cuda", generator=g) / 48.
+    b = torch.randn(256, device="cuda", generator=g) if bias else None
+    got = ops.conv3x3_bias_act(x, ops.conv3x3_weight(w), b, relu=bias)
+    assert got is not None, "benched shape fell off the MFMA route"
+    ref = F.conv2d(x, w, b, padding=1)
+    if bias:
+        ref = F.relu(ref)
+    torch.cuda.synchronize()
+    err = float((got - ref).abs().max())
+    assert err <= 2e-5 * max(1., float(ref.abs().max())), err
+
+
+@pytest.mark.parametrize("K,N,res", [(64, 256, True), (256, 64, False), (64, 64, False),
+                                     (256, 256, False)])
+def test_gemm1x1_benched_M(K, N, res):
+    """The 1x1-conv GEMM epilogue (default search: hipBLASLt or the MFMA kernel,
+    whichever the per-shape timing picks) at M = 16 x 200 x 336 vs torch fp32."""
+    from vosdetectron_amd import ops
+    M = BATCH * 200 * 336
+    g = torch.Generator(device="cuda").manual_seed(K + N)
+    a = torch.randn(M, K, device="cuda", generator=g)
+    w = torch.randn(N, K, device="cuda", generator=g) / K ** .5
+    b = torch.randn(N, device="cuda", generator=g)
+    r = torch.randn(M, N, device="cuda", generator=g) if res else None
+    got = ops.gemm_bias_act(a, w, b, residual=r, relu=True)
+    ref = torch.relu(a @ w.t() + b + (r if res else 0.))
+    err = float((got - ref).abs().max())
+    assert err <= 2e-5 * max(1., float(ref.abs().max())), err
+
+
+def test_gemm_dual_benched_M():
+    """res2's first block tail as one two-operand GEMM at M = 1,075,200."""
+    from vosdetectron_amd import ops
+    M = BATCH * 200 * 336
+    g = torch.Generator(device="cuda").manual_seed(5)
+    a1 = torch.randn(M, 64, device="cuda", generator=g)
+    a2 = torch.randn(M, 64, device="cuda", generator=g)
+    w = torch.randn(256, 128, device="cuda", generator=g) / 128 ** .5
+    b = torch.randn(256, device="cuda", generator=g)
+    got = ops.gemm_dual_bias_act(a1, a2, w, b, relu=True)
+    assert got is not None
+    ref = torch.relu(a1 @ w[:, :64].t() + a2 @ w[:, 64:].t() + b)
+    err = float((got - ref).abs().max())
+    assert err <= 2e-5 * max(1., float(ref.abs().max())), err

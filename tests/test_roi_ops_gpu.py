@@ -235,3 +235,45 @@ def test_roi_align_fpn_schedules_and_edges(P):
     feats = [p[0:1].permute(0, 3, 1, 2).cpu().numpy() for p in pyr]
     oref = orc.roi_feature_transform(feats[::-1], d, "rois", P, scales[::-1], 2)
     np.testing.assert_allclose(ref[sel].transpose(0, 3, 1, 2), oref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("P", [7, 14])
+def test_roi_align_lds_bit_exact(P):
+    """The LDS-staged kernel (variant 20, roi_align_lds.hip) computes every output
+    with the reference's arithmetic: bit-identical to the reference-order row
+    kernel (variant 3) and to the oracle's per-level loop, for any RoI schedule,
+    on 3 frames of the 800x1333 pyramid incl. RoIs off the map, degenerate, at the
+    border, split into several bands, and wide enough for the direct path."""
+    import os
+    from vosdetectron_amd import ops
+    from bench import fpn_levels_np, synthetic_rois
+    C, F = 256, 3
+    g = torch.Generator(device=DEV).manual_seed(11)
+    sizes = [(200, 336), (100, 168), (50, 84), (25, 42)]
+    pyr = [torch.randn((F, h, w, C), generator=g, device=DEV) for h, w in sizes]
+    rois = np.concatenate([synthetic_rois(f + 5, 400, batch_idx=f) for f in range(F)])
+    rois[:8, 1:5] = [[-30, -20, 40, 30], [1300, 780, 1400, 900], [0, 0, 0.5, 0.5],
+                     [1320, 790, 1332.9, 799.9], [0, 400, 1332, 420],  # 167 px wide at P3: direct
+                     [-200, 100, 1500, 140], [10, 10, 450, 890],  # tall: several bands
+                     [600, -50, 620, 1000]]
+    lv = fpn_levels_np(rois) - 2
+    rt, lt = torch.from_numpy(rois).to(DEV), torch.from_numpy(lv).to(DEV)
+    scales = [1. / 4, 1. / 8, 1. / 16, 1. / 32]
+
+    def run(variant, order=None):
+        os.environ["VOSDET_ROIALIGN_VARIANT"] = variant
+        try:
+            return ops.roi_align_fpn(pyr, scales, rt, lt, P, 2, roi_order=order,
+                                     out_layout="nhwc").cpu().numpy()
+        finally:
+            del os.environ["VOSDET_ROIALIGN_VARIANT"]
+    ref = run("3")
+    for order in (None, ops.xcd_roi_order(rt, lt), ops.xcd_roi_order(rt, lt, n_xcd=1),
+                  ops.xcd_roi_order(rt, lt, window=400)):
+        got = run("20", order)
+        assert np.array_equal(got, ref)
+    sel = rois[:, 0] == 0
+    d = orc.distribute(rois[sel].copy())
+    feats = [p[0:1].permute(0, 3, 1, 2).cpu().numpy() for p in pyr]
+    oref = orc.roi_feature_transform(feats[::-1], d, "rois", P, scales[::-1], 2)
+    assert np.array_equal(ref[sel].transpose(0, 3, 1, 2), oref)

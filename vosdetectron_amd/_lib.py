@@ -54,6 +54,7 @@ SIGNATURES = {
     "vd_nms_workspace_size": (_S, [_I]),
     "vd_nms": (_I, [_P, _I, _I, _F, _P, _P, _P, _S, _P]),
     "vd_map_rois_to_fpn_levels": (_I, [_P, _I, _I, _I, _I, _I, _F, _F, _P, _P]),
+    "vd_mask_rois": (_I, [_P, _P, _P, _I, _I, _P, _I, _I, _I, _I, _F, _F, _P, _P, _P, _P, _P]),
     "vd_generate_proposals_workspace_size": (_S, [ctypes.POINTER(VdRpnLevel), _I, _I, _I]),
     "vd_generate_proposals": (_I, [ctypes.POINTER(VdRpnLevel), _I, _I, _P, _I, _I, _F, _F, _P,
                                    _P, _P, _P, _S, _P]),

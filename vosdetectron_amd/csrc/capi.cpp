@@ -168,6 +168,20 @@ int vd_map_rois_to_fpn_levels(const float *rois, int roi_stride, int col0, int R
                              canonical_level, lvl_out, VD_STREAM(stream));
 }
 
+int vd_mask_rois(const float *dets, const int32_t *classes, const int32_t *counts,
+                 int num_images, int det_cap, const double *im_scale, int row0, int rows,
+                 int k_min, int k_max, float canonical_scale, float canonical_level,
+                 float *rois_out, int32_t *lvl_out, int32_t *cls_out, int32_t *total_out,
+                 void *stream) {
+    if (num_images == 0 || (rows == 0 && !total_out)) return VD_OK;
+    if (!dets || !classes || !counts || !im_scale || num_images < 0 || det_cap < 1 || row0 < 0 ||
+        rows < 0 || k_min > k_max || (rows > 0 && (!rois_out || !lvl_out || !cls_out)))
+        return VD_ERR_ARG;
+    return launch_mask_rois(dets, classes, counts, num_images, det_cap, im_scale, row0, rows,
+                            k_min, k_max, canonical_scale, canonical_level, rois_out, lvl_out,
+                            cls_out, total_out, VD_STREAM(stream));
+}
+
 size_t vd_generate_proposals_workspace_size(const VdRpnLevel *levels, int num_levels,
                                             int num_images, int pre_nms_topN) {
     return rpn_workspace_bytes(levels, num_levels, num_images, pre_nms_topN);

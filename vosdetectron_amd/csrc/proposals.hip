@@ -663,6 +663,64 @@ __global__ void map_levels_kernel(const float *__restrict__ rois, int stride, in
     out[r] = fpn_level(b[0], b[1], b[2], b[3], k_min, k_max, s0, lvl0);
 }
 
+// --------------------------------------------------------------------------
+// mask-head batch without a host read (im_detect_mask's _get_rois_blob +
+// _add_multilevel_rois_for_test, lib/core/test.py:877-927): block f writes
+// frame f's detections at global rows prefix(counts)[f] + j; rows [row0,
+// row0 + rows) land in the outputs, the rest of them is padding.
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void mask_rois_kernel(
+    const float *__restrict__ dets, const int32_t *__restrict__ classes,
+    const int32_t *__restrict__ counts, int F, int det_cap, const double *__restrict__ im_scale,
+    int row0, int rows, int k_min, int k_max, float s0, float lvl0, float *__restrict__ rois_out,
+    int32_t *__restrict__ lvl_out, int32_t *__restrict__ cls_out, int32_t *__restrict__ total_out) {
+    const int f = blockIdx.x;
+    int pre = 0, total = 0;
+    for (int i = 0; i < F; ++i) {  // F is small (frames per step); negative = failed frame
+        const int c = counts[i] > 0 ? min(counts[i], det_cap) : 0;
+        pre += i < f ? c : 0;
+        total += c;
+    }
+    const int n = counts[f] > 0 ? min(counts[f], det_cap) : 0;
+    const double sc = im_scale[f];
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+        const int o = pre + j - row0;
+        if (o < 0 || o >= rows) continue;
+        const float *d = dets + ((int64_t)f * det_cap + j) * 5;
+        // float64 product, float32 store (_project_im_rois, test.py:893-906)
+        const float x1 = (float)((double)d[0] * sc), y1 = (float)((double)d[1] * sc);
+        const float x2 = (float)((double)d[2] * sc), y2 = (float)((double)d[3] * sc);
+        float *r = rois_out + (int64_t)o * 5;
+        r[0] = (float)f;
+        r[1] = x1;
+        r[2] = y1;
+        r[3] = x2;
+        r[4] = y2;
+        lvl_out[o] = fpn_level(x1, y1, x2, y2, k_min, k_max, s0, lvl0) - k_min;
+        cls_out[o] = classes[(int64_t)f * det_cap + j];
+    }
+    const int pad0 = max(total - row0, 0);
+    for (int o = pad0 + f * blockDim.x + threadIdx.x; o < rows; o += F * blockDim.x) {
+        float *r = rois_out + (int64_t)o * 5;
+        r[0] = 0.f;
+        r[1] = r[2] = r[3] = r[4] = 0.f;
+        lvl_out[o] = 0;
+        cls_out[o] = 1;
+    }
+    if (f == 0 && threadIdx.x == 0 && total_out) total_out[0] = total;
+}
+
+int launch_mask_rois(const float *dets, const int32_t *classes, const int32_t *counts, int F,
+                     int det_cap, const double *im_scale, int row0, int rows, int k_min,
+                     int k_max, float s0, float lvl0, float *rois_out, int32_t *lvl_out,
+                     int32_t *cls_out, int32_t *total_out, hipStream_t s) {
+    if (F <= 0) return VD_OK;
+    hipLaunchKernelGGL(mask_rois_kernel, dim3(F), dim3(256), 0, s, dets, classes, counts, F,
+                       det_cap, im_scale, row0, rows, k_min, k_max, s0, lvl0, rois_out, lvl_out,
+                       cls_out, total_out);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
 int launch_map_levels(const float *rois, int roi_stride, int col0, int R, int k_min, int k_max,
                       float s0, float lvl0, int32_t *lvl_out, hipStream_t s) {
     if (R <= 0) return VD_OK;

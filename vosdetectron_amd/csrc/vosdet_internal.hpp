@@ -28,6 +28,8 @@ int launch_roi_align_bwd_nchw(const float *top_diff, int B, int C, int H, int W,
 int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, const int *lvl,
                               const int *order, int R, int PH, int PW, int sr, int out_nhwc,
                               float *out, hipStream_t s);
+int launch_roi_align_fpn_lds(const FpnLevels &fa, int C, const float *rois, const int *lvl,
+                             const int *order, int R, int P, int sr, float *out, hipStream_t s);
 
 size_t gemm_epi_workspace_bytes();
 int launch_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,
@@ -58,6 +60,11 @@ size_t nms_workspace_bytes(int n);
 
 int launch_map_levels(const float *rois, int roi_stride, int col0, int R, int k_min, int k_max,
                       float s0, float lvl0, int32_t *lvl_out, hipStream_t s);
+
+int launch_mask_rois(const float *dets, const int32_t *classes, const int32_t *counts, int F,
+                     int det_cap, const double *im_scale, int row0, int rows, int k_min,
+                     int k_max, float s0, float lvl0, float *rois_out, int32_t *lvl_out,
+                     int32_t *cls_out, int32_t *total_out, hipStream_t s);
 
 int launch_rpn_proposals(const VdRpnLevel *levels, int num_levels, int num_images,
                          const float *im_info, int pre_nms_topN, int post_nms_topN,

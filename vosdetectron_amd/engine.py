@@ -8,12 +8,13 @@ im_detect_mask (:366-402), for a batch of F frames already resident in HBM:
   --PyTorch RPN convs--> vd_generate_proposals (all levels, all frames)
   --> vd_collect_distribute --> vd_roi_align_fpn (one launch, NHWC pyramid)
   --> PyTorch fc6/fc7/cls/bbox --> vd_box_detections (decode, clip, class NMS,
-  top-100) --> [one D2H of the detection counts] --> mask rois + level map
-  --> vd_roi_align_fpn 14x14 --> PyTorch mask head --> class-selected 28x28.
+  top-100) --> vd_mask_rois (mask batch of F x DETECTIONS_PER_IM rows from the
+  device counts) --> vd_roi_align_fpn 14x14 --> PyTorch mask head -->
+  class-selected 28x28.
 
 The reference crosses host<->device 5+5 times in proposals alone and twice per
-roi_feature_transform; here the only host read is the per-frame detection
-count that sizes the mask-head batch.  Outputs match the reference's
+roi_feature_transform; here nothing inside the step reads the host: the
+detection counts are read once after the step is queued (complete()).  Outputs match the reference's
 `cls_boxes` rows (class-major, proposal order) and the class-selected masks
 that segm_results consumes; `frame_segms` runs segm_results' paste + RLE on
 the device (segm.py).
@@ -68,6 +69,7 @@ class FramePipeline:
         self.im_info = torch.tensor([[self.Hp, self.Wp, scale]] * F, dtype=torch.float32,
                                     device=self.device)
         self.im_scale_t = torch.full((F,), scale, dtype=torch.float32, device=self.device)
+        self.im_scale_d = torch.full((F,), scale, dtype=torch.float64, device=self.device)
         self.im_hw = torch.tensor([[self.H, self.W]] * F, dtype=torch.int32, device=self.device)
         if cfg.FPN.FPN_ON:
             k_min, k_max = cfg.FPN.RPN_MIN_LEVEL, cfg.FPN.RPN_MAX_LEVEL
@@ -134,23 +136,25 @@ class FramePipeline:
         return out
 
     @torch.no_grad()
-    def run(self, frames: torch.Tensor, keep_intermediates: bool = False):
+    def run(self, frames: torch.Tensor, keep_intermediates: bool = False, sync: bool = True):
         """frames: F x H x W x 3 uint8 BGR on the device.  Returns a dict of device
-        tensors: dets [F,cap,5] (x1,y1,x2,y2,score), classes [F,cap], counts [F]
-        (host list too), masks [M,28,28] for the M = sum(counts) detections in
-        (frame, class, proposal) order.  Stage marks (enable_timers): conv_body,
-        proposals, box_head (together the reference's im_detect_bbox), misc_bbox,
-        im_detect_mask."""
+        tensors: dets [F,cap,5] (x1,y1,x2,y2,score), classes [F,cap], counts [F],
+        masks [M,28,28] for the M = sum(counts) detections in (frame, class,
+        proposal) order, and counts_host.  sync=False queues the step without
+        any host read (graph-capturable): masks then has mask_rows(F) rows of
+        which the first M are real, and complete(out) later reads the counts and
+        trims.  Stage marks (enable_timers): conv_body, proposals, box_head
+        (together the reference's im_detect_bbox), misc_bbox, im_detect_mask."""
         if self.timers is not None:
             self._marks = []
             self._mark("start")
         try:
-            return self._run(frames, keep_intermediates)
+            return self._run(frames, keep_intermediates, sync)
         finally:
             if self.timers is not None:
                 self._collect_marks()
 
-    def _run(self, frames: torch.Tensor, keep_intermediates: bool = False):
+    def _run(self, frames: torch.Tensor, keep_intermediates: bool = False, sync: bool = True):
         cfg = self.cfg
         F = frames.shape[0]
         feats = self.backbone(frames)
@@ -188,56 +192,73 @@ class FramePipeline:
             self.im_scale_t[:F], self.im_hw[:F], tst.SCORE_THRESH, tst.NMS,
             tst.DETECTIONS_PER_IM, cfg.MODEL.BBOX_REG_WEIGHTS, self.det_cap,
             nms_cross_class=tst.NMS_CROSS_CLASS, num_det_per_class_pre=tst.NUM_DET_PER_CLASS_PRE)
-        counts = dcnt.cpu().tolist()  # the one host read: sizes the mask batch
-        ops.raise_on_failed_counts(counts)
         self._mark("misc_bbox")
-        if max(counts) > self.det_cap:
-            raise RuntimeError("detections exceed det_cap=%d: %s" % (self.det_cap, counts))
-        out = {"dets": dets, "classes": dcls, "counts": dcnt, "counts_host": counts,
-               "rois": rois, "roi_counts": rcnt, "cls_prob": cls_prob, "bbox_pred": bbox_pred}
+        out = {"dets": dets, "classes": dcls, "counts": dcnt, "rois": rois, "roi_counts": rcnt,
+               "cls_prob": cls_prob, "bbox_pred": bbox_pred}
         if keep_intermediates:  # for stage-wise parity tests
             out.update(feats=feats, rpn_probs=probs, rpn_deltas=deltas, pyramid=pyr)
-        M = sum(counts)
-        R = cfg.MRCNN.RESOLUTION
-        if M == 0:
-            out["masks"] = torch.zeros((0, R, R), device=self.device)
-            return out
-        # pad the mask batch to a multiple of 64 rows: a handful of stable shapes
-        # for the convolution algorithm search (padding rows are zero RoIs whose
-        # outputs are dropped)
-        Mp = -(-M // 64) * 64
-        sel = torch.cat([torch.arange(c, device=self.device) + f * self.det_cap
-                         for f, c in enumerate(counts)])
-        flat = dets.view(-1, 5).index_select(0, sel)
-        bidx = torch.cat([torch.full((c,), f, dtype=torch.float32, device=self.device)
-                          for f, c in enumerate(counts)])
-        # _get_rois_blob (test.py:877-906): float64 product, float32 store
-        boxes = (flat[:, :4].double() * self.im_scale).float()
-        mrois = torch.cat([bidx[:, None], boxes], 1).contiguous()
-        mlvl = ops.map_rois_to_fpn_levels(mrois, cfg.FPN.ROI_MIN_LEVEL, cfg.FPN.ROI_MAX_LEVEL)
-        mlvl = (mlvl - cfg.FPN.ROI_MIN_LEVEL).contiguous()
-        mc = cfg.MRCNN
-        mcls = dcls.view(-1).index_select(0, sel)
-        out["mask_rois"] = mrois
+        # the mask batch: F x DETECTIONS_PER_IM rows (padded to 64), built on the
+        # device from the device counts -- no host read inside the step
+        # (box_results_with_nms_and_limit keeps <= DETECTIONS_PER_IM per frame
+        # barring exact score ties at the limit; complete() runs the rest)
+        cap = self.mask_rows(F)
+        mrois, mlvl, mcls, mtotal = ops.mask_rois(
+            dets, dcls, dcnt, self.im_scale_d[:F], cap, cfg.FPN.ROI_MIN_LEVEL,
+            cfg.FPN.ROI_MAX_LEVEL)
+        out["masks"], out["mask_feat"] = self._mask_batch(pyr, mrois, mlvl, mcls, fast)
+        out["mask_rois"], out["mask_total"] = mrois, mtotal
+        out["_pyr"], out["_fast"] = pyr, fast
+        self._mark("im_detect_mask")
+        if sync:
+            self.complete(out)
+        return out
+
+    def mask_rows(self, F: int) -> int:
+        """Rows of the step's mask batch: F x DETECTIONS_PER_IM, a multiple of 64
+        (a handful of stable shapes for the convolution algorithm search)."""
+        return -(-F * int(self.cfg.TEST.DETECTIONS_PER_IM) // 64) * 64
+
+    def _mask_batch(self, pyr, mrois, mlvl, mcls, fast):
+        """Mask RoIAlign + mask head + class-selected masks for a padded batch
+        (padding rows are zero boxes whose outputs are never read)."""
+        mc = self.cfg.MRCNN
         if fast and getattr(self.model.Mask_Head, "nhwc_ready", False):
-            if Mp > M:
-                mrois = torch.cat([mrois, mrois.new_zeros((Mp - M, 5))])
-                mlvl = torch.cat([mlvl, mlvl.new_zeros((Mp - M,))])
-                mcls = torch.cat([mcls, mcls.new_ones((Mp - M,))])
-            mfeat = ops.roi_align_fpn(pyr, self.roi_scales, mrois, mlvl,
-                                      mc.ROI_XFORM_RESOLUTION, mc.ROI_XFORM_SAMPLING_RATIO,
-                                      out_layout="nhwc")
+            mfeat = ops.roi_align_fpn(pyr, self.roi_scales, mrois, mlvl, mc.ROI_XFORM_RESOLUTION,
+                                      mc.ROI_XFORM_SAMPLING_RATIO, out_layout="nhwc")
             up = self.model.Mask_Head.head_nhwc(mfeat)
-            out["masks"] = self.model.Mask_Outs.selected_from_up(up, mcls)[:M]
-            out["mask_feat"] = mfeat[:M].permute(0, 3, 1, 2)
-            self._mark("im_detect_mask")
-            return out
+            return (self.model.Mask_Outs.selected_from_up(up, mcls),
+                    mfeat.permute(0, 3, 1, 2))
         mfeat = ops.roi_align_fpn(pyr, self.roi_scales, mrois, mlvl, mc.ROI_XFORM_RESOLUTION,
                                   mc.ROI_XFORM_SAMPLING_RATIO)
         mh = self.model.Mask_Head.head(mfeat)
-        out["masks"] = self.model.Mask_Outs.selected(mh, mcls)
-        out["mask_feat"] = mfeat
-        self._mark("im_detect_mask")
+        return self.model.Mask_Outs.selected(mh, mcls), mfeat
+
+    def complete(self, out: dict) -> dict:
+        """The step's one host read, after everything is queued: the detection
+        counts (failure / capacity checks), the masks of detections beyond the
+        padded batch (exact score ties at DETECTIONS_PER_IM), and the outputs
+        trimmed to the M = sum(counts) real detections.  Idempotent."""
+        if "counts_host" in out:
+            return out
+        counts = out["counts"].cpu().tolist()
+        ops.raise_on_failed_counts(counts)
+        if max(counts, default=0) > self.det_cap:
+            raise RuntimeError("detections exceed det_cap=%d: %s" % (self.det_cap, counts))
+        M, cap = sum(counts), out["masks"].shape[0]
+        if M > cap:  # rows [cap, M): a second, rare batch
+            extra = -(-(M - cap) // 64) * 64
+            F = len(counts)
+            r2, l2, c2, _ = ops.mask_rois(out["dets"], out["classes"], out["counts"],
+                                          self.im_scale_d[:F], extra, self.cfg.FPN.ROI_MIN_LEVEL,
+                                          self.cfg.FPN.ROI_MAX_LEVEL, row0=cap)
+            m2, f2 = self._mask_batch(out["_pyr"], r2, l2, c2, out["_fast"])
+            out["masks"] = torch.cat([out["masks"], m2])
+            out["mask_feat"] = torch.cat([out["mask_feat"], f2])
+            out["mask_rois"] = torch.cat([out["mask_rois"], r2])
+        out["masks"] = out["masks"][:M]
+        out["mask_feat"] = out["mask_feat"][:M]
+        out["mask_rois"] = out["mask_rois"][:M]
+        out["counts_host"] = counts
         return out
 
 

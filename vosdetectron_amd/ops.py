@@ -364,6 +364,32 @@ def map_rois_to_fpn_levels(rois: torch.Tensor, k_min: int, k_max: int, col0: int
     return out
 
 
+def mask_rois(dets: torch.Tensor, classes: torch.Tensor, counts: torch.Tensor,
+              im_scale: torch.Tensor, rows: int, k_min: int, k_max: int, row0: int = 0,
+              canonical_scale: float = 224., canonical_level: float = 4.):
+    """The mask-head batch of all frames without a host read (vd_mask_rois):
+    dets [F, D, 5], classes [F, D] int32, counts [F] int32, im_scale [F] float64
+    -> rois [rows, 5], levels [rows] (level - k_min), classes [rows] int32 and the
+    device total [1] int32; global rows [row0, row0 + rows), frame-major, padding
+    past the total."""
+    d, c, n = _need(dets, "dets"), _need(classes, "classes", torch.int32), \
+        _need(counts, "counts", torch.int32)
+    sc = _need(im_scale, "im_scale", torch.float64)
+    F, D = d.shape[0], d.shape[1]
+    if tuple(c.shape) != (F, D) or n.numel() != F or sc.numel() != F:
+        raise ValueError("mask_rois: dets %s classes %s counts %s im_scale %s"
+                         % (tuple(d.shape), tuple(c.shape), tuple(n.shape), tuple(sc.shape)))
+    rois = torch.empty((rows, 5), dtype=torch.float32, device=d.device)
+    lvl = torch.empty((rows,), dtype=torch.int32, device=d.device)
+    cls = torch.empty((rows,), dtype=torch.int32, device=d.device)
+    total = torch.empty((1,), dtype=torch.int32, device=d.device)
+    check(lib().vd_mask_rois(d.data_ptr(), c.data_ptr(), n.data_ptr(), F, D, sc.data_ptr(),
+                             int(row0), int(rows), k_min, k_max, float(canonical_scale),
+                             float(canonical_level), rois.data_ptr(), lvl.data_ptr(),
+                             cls.data_ptr(), total.data_ptr(), _stream()), "vd_mask_rois")
+    return rois, lvl, cls, total
+
+
 def nchw_to_nhwc(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     t = _need(x, "x")
     B, C, H, W = t.shape

@@ -31,10 +31,12 @@ class PendingGather:
     """An in-flight all_gather (async_op) of one buffer slot.
 
     The views `wait()` returns alias the gatherer's receive slot (the send slot
-    when world == 1).  Slots alternate, so a view stays valid until the
+    without a process group).  Slots alternate, so a view stays valid until the
     gather_async call after next; `wait(clone=True)` returns private copies for
-    callers that keep results longer.  A view read after its slot was reused
-    raises (generation check) instead of silently showing a later step's rows."""
+    callers that keep results longer.  A `wait()` on a slot that a later
+    gather_async has reused raises (generation check); views returned by an
+    earlier `wait()` are NOT guarded -- they alias the buffer and show the
+    later step's rows once it is reused."""
 
     def __init__(self, work, gatherer, rbuf, slot, gen):
         self.work, self.g, self.rbuf, self.slot, self.gen = work, gatherer, rbuf, slot, gen
@@ -76,7 +78,10 @@ class ResultGatherer:
 
     Two buffer slots alternate, so `gather_async` of step t can run on RCCL's
     stream while step t+1 computes; the caller keeps at most one gather in
-    flight (`wait()` before issuing the next)."""
+    flight (`wait()` before issuing the next).  The collective is issued
+    whenever a process group is initialised -- including a one-rank RCCL group,
+    so world 1 exercises the same all_gather_into_tensor -- and skipped (the
+    send slot is the result) only without one."""
 
     def __init__(self, frames_per_rank: int, det_cap: int, mask_res: int, world: int,
                  device, with_masks: bool = True, mask_rows: Optional[int] = None):
@@ -91,6 +96,10 @@ class ResultGatherer:
         self.recv = [torch.zeros((world, self.L), device=device) for _ in range(2)]
         self.slot = 0
         self.gen = [0, 0]
+        self.collective = dist.is_available() and dist.is_initialized()
+        if self.collective and dist.get_world_size() != world:
+            raise ValueError("ResultGatherer(world=%d) but the process group has %d ranks"
+                             % (world, dist.get_world_size()))
 
     @property
     def bytes_per_rank(self) -> int:
@@ -138,7 +147,7 @@ class ResultGatherer:
         self.slot ^= 1
         self.gen[s] += 1
         self._pack(self.send[s], dets, classes, counts, masks)
-        if self.world == 1:
+        if not self.collective:
             return PendingGather(None, self, self.send[s].view(1, -1), s, self.gen[s])
         work = dist.all_gather_into_tensor(self.recv[s].view(-1), self.send[s], async_op=True)
         return PendingGather(work, self, self.recv[s], s, self.gen[s])
@@ -149,10 +158,15 @@ class ResultGatherer:
 
 def frame_masks(views: Dict[str, torch.Tensor], frames_per_rank: int, frame: int
                 ) -> torch.Tensor:
-    """The gathered masks of global frame index `frame` (rank-major order)."""
+    """The gathered masks of global frame index `frame` (rank-major order).
+    Raises if the frame's rows lie past the gathered mask rows (a step with more
+    detections than the engine's padded mask batch, FramePipeline.complete)."""
     r, f = divmod(frame, frames_per_rank)
     o = int(views["mask_offsets"][r, f])
     k = int(views["counts"][frame])
+    if o + k > views["masks"].shape[1]:
+        raise RuntimeError("frame %d's masks (rows %d..%d) exceed the %d gathered mask rows"
+                           % (frame, o, o + k, views["masks"].shape[1]))
     return views["masks"][r, o:o + k]
 
 
