@@ -138,6 +138,15 @@ int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const 
 int vd_conv3x3_bias_act(const float *X, int N, int H, int W, int C, const float *W2, int Cout,
                         const float *bias, int relu, float *Y, void *stream);
 
+/* The same convolution by Winograd F(2x2, 3x3) on the MFMA pipes (2.25x fewer
+ * multiplies; the transforms add, subtract and halve): U from
+ * vd_conv3x3_wino_weight (16 x Cout x Cin fp32, once per model) replaces W2.
+ * Requires Cin % 8 == 0 and Cout % 64 == 0 (VD_ERR_SHAPE otherwise).  Results
+ * agree with the direct form within fp32 rounding (not bit for bit). */
+int vd_conv3x3_wino_weight(const float *w, int Cout, int Cin, float *U, void *stream);
+int vd_conv3x3_wino_bias_act(const float *X, int N, int H, int W, int C, const float *U,
+                             int Cout, const float *bias, int relu, float *Y, void *stream);
+
 /* Two 1x1 convolutions of two channels_last inputs summed, with the epilogue:
  * D[M][N] = act(A1[M][K1] . W[:, :K1]^T + A2[M][K2] . W[:, K1:]^T + bias[N]),
  * W = [W1 | W2] as N x (K1 + K2) row-major.  With A1 = the bottleneck's conv2

@@ -101,15 +101,24 @@ def match(gd, gc, gm, sc, bx, cl, masks, iou_min=0.95):
     return matched, mask_err
 
 
-def e2e_vs_cpu(out, ref_out, f=0, count_tol=0.05, mask_tol=1e-3):
+def e2e_vs_cpu(out, ref_out, f=0, count_tol=0.02, match_min=0.98, mask_tol=1e-3):
+    """Frame f of the GPU engine vs the independent CPU pipeline: detection
+    counts within 2 % (>= 2), >= 98 % of the CPU detections matched by class and
+    IoU > 0.95, median max-|mask diff| of the matched pairs < 1e-3.  The two
+    pipelines' convolutions (MIOpen / hand-written MFMA vs oneDNN, folded vs
+    unfolded AffineChannel) round differently, so a detection whose score sits
+    at the 0.05 threshold or the 100th place can flip; everything else must
+    agree (the stage-wise checks hold each HIP stage bit-exact / 1e-4)."""
     sc, bx, cl, masks, _ = ref_out
     k = out["counts_host"][f]
     o = int(sum(out["counts_host"][:f]))
     gd = out["dets"][f, :k].cpu().numpy()
     gc = out["classes"][f, :k].cpu().numpy()
     gm = out["masks"][o:o + k].cpu().numpy()
-    assert abs(k - len(sc)) <= max(3, count_tol * len(sc)), (k, len(sc))
+    assert abs(k - len(sc)) <= max(2, count_tol * len(sc)), (k, len(sc))
     matched, mask_err = match(gd, gc, gm, sc, bx, cl, masks)
-    assert matched >= 0.9 * len(sc), (matched, len(sc))
+    assert matched >= match_min * len(sc), (matched, len(sc))
     assert np.median(mask_err) < mask_tol, np.median(mask_err)
+    print("e2e frame %d: %d/%d CPU detections matched, GPU count %d, median mask err %.2e"
+          % (f, matched, len(sc), k, float(np.median(mask_err))))
     return matched

@@ -134,27 +134,6 @@ def test_c4_end_to_end_vs_independent_cpu(gpu_setup):
     torch.set_num_threads(16)
     sc, bx, cl, masks, _ = RefCPUPipelineC4(sd, post_nms=cfg.TEST.RPN_POST_NMS_TOP_N,
                                             test_scale=FRAME_HW[0])(frame)
-    k = out["counts_host"][0]
-    gd = out["dets"][0, :k].cpu().numpy()
-    gc = out["classes"][0, :k].cpu().numpy()
-    gm = out["masks"][:k].cpu().numpy()
     assert len(sc) > 0
-    assert abs(k - len(sc)) <= max(3, 0.05 * len(sc))
-    matched, mask_err = 0, []
-    for i in range(len(sc)):
-        same = np.where(gc == cl[i])[0]
-        if not len(same):
-            continue
-        b = gd[same, :4]
-        xx1 = np.maximum(b[:, 0], bx[i, 0]); yy1 = np.maximum(b[:, 1], bx[i, 1])
-        xx2 = np.minimum(b[:, 2], bx[i, 2]); yy2 = np.minimum(b[:, 3], bx[i, 3])
-        inter = np.maximum(0, xx2 - xx1 + 1) * np.maximum(0, yy2 - yy1 + 1)
-        a1 = (b[:, 2] - b[:, 0] + 1) * (b[:, 3] - b[:, 1] + 1)
-        a2 = (bx[i, 2] - bx[i, 0] + 1) * (bx[i, 3] - bx[i, 1] + 1)
-        iou = inter / (a1 + a2 - inter)
-        j = int(np.argmax(iou))
-        if iou[j] > 0.95:
-            matched += 1
-            mask_err.append(np.abs(gm[same[j]] - masks[i]).max())
-    assert matched >= 0.9 * len(sc), (matched, len(sc))
-    assert np.median(mask_err) < 1e-3
+    from tests.engine_checks import e2e_vs_cpu
+    e2e_vs_cpu(out, (sc, bx, cl, masks, None))

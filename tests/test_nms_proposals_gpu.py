@@ -73,9 +73,13 @@ def _anchors(lvl):
     return torch.from_numpy(orc.fpn_level_anchors(lvl)).to(DEV)
 
 
-def test_generate_proposals_golden(golden):
-    """Reference-executed GenerateProposalsOp per level (tests/golden/proposals.npz)."""
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_generate_proposals_golden(golden, split, monkeypatch):
+    """Reference-executed GenerateProposalsOp per level (tests/golden/proposals.npz),
+    through the split NMS (default) and the single-kernel small variant
+    (VOSDET_RPN_SPLIT=0)."""
     from vosdetectron_amd import ops
+    monkeypatch.setenv("VOSDET_RPN_SPLIT", split)
     g = golden("proposals")
     lv = list(range(2, 7))
     probs = [torch.from_numpy(g["probs_fpn%d" % l]).to(DEV) for l in lv]

@@ -129,10 +129,13 @@ def _edge_boxes(im_h, im_w):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("R,im_h,im_w", [(28, 800, 1333), (14, 480, 854), (28, 37, 53)])
+@pytest.mark.parametrize("R,im_h,im_w", [(28, 800, 1333), (14, 480, 854), (28, 37, 53),
+                                         (28, 24, 9000)])
 def test_segm_rle_fused_vs_oracle(R, im_h, im_w):
     """vd_segm_rle (paste + RLE without planes) and vd_rle_strings equal the
-    oracle's segm_results loop (paste, rleEncode, rleToString) bit for bit."""
+    oracle's segm_results loop (paste, rleEncode, rleToString) bit for bit; a
+    frame wider than the fused kernel's 8192-column table (9000) takes the
+    planes path (paste_masks + mask_rle) with the same results."""
     from vosdetectron_amd import ops, segm
     rng = np.random.default_rng(3 * R + im_w)
     masks, boxes = _cases(rng, 40, im_h, im_w, R)

@@ -187,13 +187,14 @@ def test_vos_sequence_vs_cpu_oracle(vos_setup):
             rel = float((a.cpu() - b).abs().max() / b.abs().max())
             assert rel < 2e-3, (t, rel)
         k = out["counts_host"][0]
-        assert abs(k - len(sc)) <= max(3, 0.05 * len(sc)), (t, k, len(sc))
+        assert abs(k - len(sc)) <= max(2, 0.02 * len(sc)), (t, k, len(sc))
         gd = out["dets"][0, :k].cpu().numpy()
         gc = out["classes"][0, :k].cpu().numpy()
         gm = out["masks"][:k].cpu().numpy()
         assert gm.shape[1:] == (56, 56)
         matched, mask_err = _match(gd, gc, gm, sc, bx, cl, masks)
-        assert matched >= 0.9 * len(sc), (t, matched, len(sc))
+        print("VOS frame %d: %d/%d matched, count %d" % (t, matched, len(sc), k))
+        assert matched >= 0.98 * len(sc), (t, matched, len(sc))
         assert np.median(mask_err) < 2e-3, (t, np.median(mask_err))
 
 

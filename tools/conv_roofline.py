@@ -4,7 +4,10 @@
 F.conv_transpose2d and F.linear are wrapped for one steady-state step: each
 call is bracketed by HIP events on the current stream and its FLOPs are
 2 * (output elements) * Cin/groups * kh * kw (2*M*N*K for linear).  The
-C-ABI GEMM-epilogue convs (ops.gemm_bias_act) are wrapped the same way.  Peak:
+C-ABI routes -- the GEMM-epilogue 1x1 convs (ops.gemm_bias_act: hipBLASLt or
+csrc/gemm1x1.hip), the two-operand GEMM (ops.gemm_dual_bias_act), the MFMA
+3x3 conv (ops.conv3x3_bias_act, csrc/conv3x3.hip) and the RPN head
+(ops.rpn_head) -- are wrapped the same way.  Peak:
 157.3 TFLOP/s fp32 MFMA (MI355X_MICROARCH.md; no xf32 on gfx950).
 
 usage: python tools/conv_roofline.py [out.json]"""
@@ -77,6 +80,29 @@ def main():
             return 2.0 * M * W.shape[0] * K, "gemm_bias_act M%d N%d K%d%s" % (
                 M, W.shape[0], K, " +res" if residual is not None else "")
         ops.gemm_bias_act = timed("gemm_epi", gl, gk)
+    cl = ops.conv3x3_bias_act
+
+    def ck(y, x, w2, bias, relu=False, out=None):
+        if y is None:
+            return 0.0, "conv3x3 (fell back)"
+        N, C, H, W = x.shape
+        return 2.0 * N * H * W * y.shape[1] * C * 9, "conv3x3_mfma x%s Cout%d%s" % (
+            list(x.shape), y.shape[1], " +bias" if bias is not None else "")
+    ops.conv3x3_bias_act = timed("conv3x3_mfma", cl, ck)
+    dl = ops.gemm_dual_bias_act
+
+    def dk(y, a1, a2, w, bias, relu=True, out=None):
+        M = a1.shape[0]
+        return 2.0 * M * w.shape[0] * w.shape[1], "gemm_dual M%d N%d K%d+%d" % (
+            M, w.shape[0], a1.shape[1], a2.shape[1])
+    ops.gemm_dual_bias_act = timed("gemm_dual", dl, dk)
+    rl = ops.rpn_head
+
+    def rk(y, x_raw, conv_bias, w, b, *a, **k):
+        N, C, H, W = x_raw.shape
+        return 2.0 * N * H * W * C * w.shape[0], "rpn_head x[%d,%d,%d,%d] 5A=%d" % (
+            N, C, H, W, w.shape[0])
+    ops.rpn_head = timed("rpn_head", rl, rk)
     try:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -87,6 +113,7 @@ def main():
         Fn.conv2d, Fn.conv_transpose2d, Fn.linear = orig[:3]
         if gl is not None:
             ops.gemm_bias_act = gl
+        ops.conv3x3_bias_act, ops.gemm_dual_bias_act, ops.rpn_head = cl, dl, rl
     step_ms = e0.elapsed_time(e1)
     agg = collections.OrderedDict()
     for kind, a, b, (fl, key) in recs:

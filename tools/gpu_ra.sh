@@ -4,7 +4,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/${TAG:-ra}; rm -rf $O; mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_roi_ops_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread ${TESTK:+-k "$TESTK"} > $O/tests.txt 2>&1
+timeout -k 10 300 python -u -m pytest ${TESTS:-tests/test_roi_ops_gpu.py} -m gpu -x -q --timeout 200 --timeout-method thread ${TESTK:+-k "$TESTK"} > $O/tests.txt 2>&1
 rc=$?; tail -3 $O/tests.txt; [ $rc -ne 0 ] && { grep -B5 -A40 "Error\|FAILED\|assert" $O/tests.txt | head -80; exit $rc; }
 for v in ${VARIANTS:-20 10}; do
   for P in 7 14; do
@@ -12,6 +12,10 @@ for v in ${VARIANTS:-20 10}; do
     python -c "import json;d=json.load(open('$O/v${v}_p$P.json'));print('v$v P$P', d['avg_launch_us'], d['frac'])"
   done
 done
+if [ -n "$PROBE" ]; then
+  timeout -k 10 300 python -u tools/probe_conv_algos.py > $O/probe.json 2> $O/probe.err || { echo probe failed; tail -20 $O/probe.err; exit 1; }
+  cat $O/probe.json
+fi
 [ -z "$PMC" ] && { echo done; exit 0; }
 v=$(echo ${VARIANTS:-20} | awk '{print $1}')
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null

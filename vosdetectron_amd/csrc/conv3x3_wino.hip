@@ -1,0 +1,333 @@
+// 3x3 stride-1 pad-1 convolution on NHWC fp32 by Winograd F(2x2, 3x3) on the
+// MFMA pipes, bias (+ ReLU) epilogue fused.
+//
+// Same operator as conv3x3.hip (FPN posthoc / RPN conv, lib/modeling/FPN.py:
+// 227-258, 376-422; mask head convs, mask_rcnn_heads.py:178-188), computed with
+// 2.25x fewer multiplies (Lavin & Gray, "Fast Algorithms for Convolutional Neural
+// Networks"): every 2x2 output tile is
+//   Y = A^T [ sum_ci (G g G^T) (.) (B^T d B) ] A
+// with d the tile's 4x4 input patch.  The sum over ci is 16 independent GEMMs,
+// M[pos][co][tile] = sum_ci U[pos][co][ci] V[pos][ci][tile] (pos = the 16
+// transform positions), run with v_mfma_f32_16x16x4_f32 (fp32 in, fp32 out: the
+// reference's precision; the transforms only add / subtract and scale by 0.5).
+//
+// Workgroup (8 waves, one per CU: 150 KiB of LDS): 64 tiles (4 tile rows x 16
+// tile columns = 8 x 32 output pixels of one image) x 64 output channels.
+// Wave w owns tile row w & 3 and 32 channels (w >> 2), i.e. ALL 16 positions of
+// its 16 tiles x 32 channels: 128 accumulator registers per lane, and a lane's
+// 16 position values of one (channel, tile) sit in the same register slot of its
+// 16 accumulators, so the output transform is lane-local.
+// K is walked in chunks of 8 input channels; per chunk the raw 10 x 34 pixel
+// patch and U's slice are staged in LDS, every thread transforms one (tile,
+// channel) of the NEXT chunk's patch into V while the MFMAs of this chunk run,
+// and the loads of the chunk after that are in flight: two LDS stages, two
+// barriers per chunk.  K permutation (both operands): lane group q at k-step s
+// holds channel 2q + s, so each fragment is one ds_read_b64.
+#include <stdlib.h>
+
+#include <mutex>
+#include <set>
+
+#include "common.hpp"
+#include "vosdet_internal.hpp"
+
+namespace vd {
+
+namespace {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+constexpr int kTiles = 64;                 // tiles per workgroup: TR x TC (4 x 16 or 8 x 8)
+constexpr int kCo = 64;                    // output channels per workgroup
+constexpr int kKC = 8;                     // input channels per chunk
+constexpr int kPatchMaxF4 = 680;           // the larger patch (10 x 34 pixels x 8 channels)
+constexpr int kVsF = 16 * kTiles * kKC;    // 8192 floats: V [pos][tile][8]
+constexpr int kUsF = 16 * kCo * kKC;       // 8192 floats: U [pos][co][8]
+constexpr int kPatchF = kPatchMaxF4 * 4;   // 2720 floats: patch [row][col][8]
+constexpr int kStageF = kVsF + kUsF + kPatchF;
+constexpr size_t kLdsBytes = 2 * (size_t)kStageF * 4;  // 152,832 B
+constexpr int kThreads = 512;
+
+// Row-half swizzle of the [.][8] rows: rows r and r + 8 of a 16-row MFMA block
+// put their two float4 halves in opposite order, so a ds_read_b64 fragment read
+// (lanes j = 0..15 x q = 0..1 per 32-lane group) touches 32 distinct banks.
+__device__ __forceinline__ int sw_half(int row) { return (row >> 3) & 1; }
+
+// TC tile columns x (64 / TC) tile rows per workgroup: 16 (8 x 32 output pixels)
+// for feature maps, 8 (16 x 16 pixels: one 14 x 14 mask-head RoI) for small ones.
+template <bool RELU, int TC>
+__global__ __launch_bounds__(kThreads, 1) void conv3x3_wino_kernel(
+    const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
+    int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx) {
+    constexpr int kTC = TC, kTR = kTiles / TC;
+    constexpr int kPR = 2 * kTR + 2, kPC = 2 * kTC + 2;  // input patch (pixels)
+    constexpr int kPatchF4 = kPR * kPC * kKC / 4;
+    static_assert(kPatchF4 <= kPatchMaxF4, "patch fits its LDS region");
+    extern __shared__ __attribute__((aligned(16))) float lds[];  // [2][kStageF]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 15, q = lane >> 4;
+    // the Cout / 64 channel blocks of one spatial block run on one XCD (blocks
+    // b, b + 8, ...): its input patches come from one L2
+    const int ncb = Cout / kCo;
+    const int r8 = blockIdx.x % (8 * ncb);
+    const int cb = r8 / 8;
+    const int sp = (blockIdx.x / (8 * ncb)) * 8 + (r8 & 7);
+    const int nsp = N * tby * tbx;
+    if (sp >= nsp) return;
+    const int n = sp / (tby * tbx);
+    const int rem = sp - n * tby * tbx;
+    const int tyb = rem / tbx, txb = rem - (rem / tbx) * tbx;
+    const int oy0 = 2 * kTR * tyb, ox0 = 2 * kTC * txb;  // first output pixel
+    const int iy0 = oy0 - 1, ix0 = ox0 - 1;              // first patch pixel
+    const int n0 = cb * kCo;
+    const int tg = wave & 3, cg = wave >> 2;  // wave: tiles 16 tg .. + 15, 32-channel group
+
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(X), (short)0, (int)((int64_t)N * H * W * C * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(U), (short)0, (int)((int64_t)16 * Cout * C * 4), 0x00020000);
+
+    // staging assignment: patch float4 f = tid + 512 i (i < 2, f < 680);
+    // U float4 f = tid + 512 i (i < 4): row f >> 1 = (pos, co), half f & 1
+    int poff[2], uoff[4], pdst[2], udst[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int f = tid + kThreads * i;
+        const int px = f >> 1, h = f & 1;
+        const int prow = px / kPC, pcol = px - (px / kPC) * kPC;
+        const int y = iy0 + prow, x = ix0 + pcol;
+        const bool ok = f < kPatchF4 && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+        // out-of-image taps read past the buffer's range: zeros
+        poff[i] = ok ? (((n * H + y) * W + x) * C + 4 * h) * 4 : 0x7ffffff0;
+        pdst[i] = f < kPatchF4 ? kVsF + kUsF + 4 * f : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int f = tid + kThreads * i;
+        const int row = f >> 1, h = f & 1;
+        const int pos = row >> 6, co = row & 63;
+        uoff[i] = ((pos * Cout + n0 + co) * C + 4 * h) * 4;
+        udst[i] = kVsF + row * kKC + 4 * (h ^ sw_half(co));
+    }
+    float4 pr[2], urg[4];
+#define VD_W_LOAD(CH)                                                                        \
+    {                                                                                        \
+        const int cb4_ = (CH) * kKC * 4;                                                     \
+        _Pragma("unroll") for (int i = 0; i < 2; ++i) pr[i] = __builtin_bit_cast(            \
+            float4, __builtin_amdgcn_raw_buffer_load_b128(                                   \
+                        xr, poff[i] == 0x7ffffff0 ? poff[i] : poff[i] + cb4_, 0, 0));        \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) urg[i] = __builtin_bit_cast(           \
+            float4, __builtin_amdgcn_raw_buffer_load_b128(ur, uoff[i] + cb4_, 0, 0));        \
+    }
+#define VD_W_STORE(STG)                                                                      \
+    {                                                                                        \
+        float *s_ = lds + (STG) * kStageF;                                                   \
+        _Pragma("unroll") for (int i = 0; i < 2; ++i) if (pdst[i] >= 0)                      \
+            *reinterpret_cast<float4 *>(s_ + pdst[i]) = pr[i];                               \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i)                                        \
+            *reinterpret_cast<float4 *>(s_ + udst[i]) = urg[i];                              \
+    }
+    // input transform of one (tile, channel) of stage STG's patch into its V:
+    // V = B^T d B, B^T = [1 0 -1 0; 0 1 1 0; 0 -1 1 0; 0 1 0 -1]
+    const int xt = tid >> 3, xc = tid & 7;  // tile, channel
+    const int xtr = xt / kTC, xtc = xt % kTC;
+    const int vdst = xt * kKC + 4 * ((xc >> 2) ^ sw_half(xt)) + (xc & 3);
+#define VD_W_XFORM(STG)                                                                      \
+    {                                                                                        \
+        const float *p_ = lds + (STG) * kStageF + kVsF + kUsF;                               \
+        float d_[4][4];                                                                      \
+        _Pragma("unroll") for (int a = 0; a < 4; ++a)                                        \
+            _Pragma("unroll") for (int c = 0; c < 4; ++c)                                    \
+                d_[a][c] = p_[((2 * xtr + a) * kPC + 2 * xtc + c) * kKC + xc];               \
+        float r_[4][4];                                                                      \
+        _Pragma("unroll") for (int c = 0; c < 4; ++c) {                                      \
+            r_[0][c] = d_[0][c] - d_[2][c];                                                  \
+            r_[1][c] = d_[1][c] + d_[2][c];                                                  \
+            r_[2][c] = d_[2][c] - d_[1][c];                                                  \
+            r_[3][c] = d_[1][c] - d_[3][c];                                                  \
+        }                                                                                    \
+        float *v_ = lds + (STG) * kStageF + vdst;                                            \
+        _Pragma("unroll") for (int a = 0; a < 4; ++a) {                                      \
+            v_[(4 * a + 0) * kTiles * kKC] = r_[a][0] - r_[a][2];                            \
+            v_[(4 * a + 1) * kTiles * kKC] = r_[a][1] + r_[a][2];                            \
+            v_[(4 * a + 2) * kTiles * kKC] = r_[a][2] - r_[a][1];                            \
+            v_[(4 * a + 3) * kTiles * kKC] = r_[a][1] - r_[a][3];                            \
+        }                                                                                    \
+    }
+    // fragment offsets (floats within a stage): V of tile tg*16 + j, U of channel
+    // cg*32 + 16 tc + j; channels 2q, 2q + 1 of the chunk
+    const int vt = tg * 16 + j;
+    const int vfo = vt * kKC + 4 * ((q >> 1) ^ sw_half(vt)) + 2 * (q & 1);
+    int ufo[2];
+#pragma unroll
+    for (int tc = 0; tc < 2; ++tc) {
+        const int co = cg * 32 + 16 * tc + j;
+        ufo[tc] = kVsF + co * kKC + 4 * ((q >> 1) ^ sw_half(co)) + 2 * (q & 1);
+    }
+    f4v acc[16][2];
+#pragma unroll
+    for (int p = 0; p < 16; ++p)
+#pragma unroll
+        for (int tc = 0; tc < 2; ++tc) acc[p][tc] = f4v{0.f, 0.f, 0.f, 0.f};
+
+    const int nch = C / kKC;
+    // prologue: chunk 0 staged and transformed, chunk 1 staged
+    VD_W_LOAD(0)
+    VD_W_STORE(0)
+    __syncthreads();
+    VD_W_XFORM(0)
+    if (nch > 1) {
+        VD_W_LOAD(1)
+        VD_W_STORE(1)
+    }
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+        const int s = ch & 1;
+        if (ch + 2 < nch) VD_W_LOAD(ch + 2)
+        const float *st = lds + s * kStageF;
+        // four positions at a time: 8 independent accumulators between the two
+        // k-steps of one (the 16x16x4 f32 MFMA's dependent latency is 40 cycles)
+#pragma unroll
+        for (int p0 = 0; p0 < 16; p0 += 4) {
+            f2v b[4], a[4][2];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                b[i] = *reinterpret_cast<const f2v *>(st + (p0 + i) * kTiles * kKC + vfo);
+                a[i][0] = *reinterpret_cast<const f2v *>(st + (p0 + i) * kCo * kKC + ufo[0]);
+                a[i][1] = *reinterpret_cast<const f2v *>(st + (p0 + i) * kCo * kKC + ufo[1]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int tc = 0; tc < 2; ++tc)
+                    acc[p0 + i][tc] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        a[i][tc].x, b[i].x, acc[p0 + i][tc], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int tc = 0; tc < 2; ++tc)
+                    acc[p0 + i][tc] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        a[i][tc].y, b[i].y, acc[p0 + i][tc], 0, 0, 0);
+        }
+        // the next chunk's patch -> its V (stage s ^ 1), beside this chunk's MFMAs
+        if (ch + 1 < nch) VD_W_XFORM(s ^ 1)
+        __syncthreads();  // stage s fully read; V of the next chunk written
+        if (ch + 2 < nch) VD_W_STORE(s)
+        __syncthreads();  // chunk ch + 2's patch / U visible
+    }
+#undef VD_W_LOAD
+#undef VD_W_STORE
+#undef VD_W_XFORM
+    // output transform (lane-local): A^T = [1 1 1 0; 0 1 -1 -1]; lane (j, q),
+    // accumulator slot r holds channel n0 + cg*32 + 16 tc + 4 q + r of tile (tg, j)
+    const int vtile = tg * 16 + j;
+    const int oy = oy0 + 2 * (vtile / kTC), ox = ox0 + 2 * (vtile % kTC);
+#pragma unroll
+    for (int tc = 0; tc < 2; ++tc) {
+        const int co = n0 + cg * 32 + 16 * tc + 4 * q;
+        const float4 bv = bias ? *reinterpret_cast<const float4 *>(bias + co)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+        float o[4][4];  // [output pixel dy*2+dx][slot r]
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float s0[4], s1[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                s0[c] = acc[c][tc][r] + acc[4 + c][tc][r] + acc[8 + c][tc][r];
+                s1[c] = acc[4 + c][tc][r] - acc[8 + c][tc][r] - acc[12 + c][tc][r];
+            }
+            o[0][r] = s0[0] + s0[1] + s0[2];
+            o[1][r] = s0[1] - s0[2] - s0[3];
+            o[2][r] = s1[0] + s1[1] + s1[2];
+            o[3][r] = s1[1] - s1[2] - s1[3];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int y = oy + (k >> 1), x = ox + (k & 1);
+            if (y >= H || x >= W) continue;
+            float4 v = make_float4(o[k][0] + bv.x, o[k][1] + bv.y, o[k][2] + bv.z,
+                                   o[k][3] + bv.w);
+            if (RELU) {
+                v.x = fmaxf(v.x, 0.f);
+                v.y = fmaxf(v.y, 0.f);
+                v.z = fmaxf(v.z, 0.f);
+                v.w = fmaxf(v.w, 0.f);
+            }
+            *reinterpret_cast<float4 *>(Y + ((int64_t)(n * H + y) * W + x) * Cout + co) = v;
+        }
+    }
+}
+
+// U[pos][co][ci] = (G g G^T)[pos / 4][pos % 4] of the PyTorch weight
+// w[co][ci][3][3]; G = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1]; float64, rounded once.
+__global__ void wino_weight_kernel(const float *__restrict__ w, int Cout, int C,
+                                   float *__restrict__ U) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)Cout * C) return;
+    const int co = (int)(i / C), ci = (int)(i - (int64_t)(i / C) * C);
+    const float *g = w + i * 9;
+    double t[4][3];  // G g
+    for (int c = 0; c < 3; ++c) {
+        const double g0 = g[c], g1 = g[3 + c], g2 = g[6 + c];
+        t[0][c] = g0;
+        t[1][c] = 0.5 * (g0 + g1 + g2);
+        t[2][c] = 0.5 * (g0 - g1 + g2);
+        t[3][c] = g2;
+    }
+    for (int a = 0; a < 4; ++a) {
+        const double u[4] = {t[a][0], 0.5 * (t[a][0] + t[a][1] + t[a][2]),
+                             0.5 * (t[a][0] - t[a][1] + t[a][2]), t[a][2]};
+        for (int b = 0; b < 4; ++b)
+            U[((int64_t)(4 * a + b) * Cout + co) * C + ci] = (float)u[b];
+    }
+}
+
+bool allow_lds_wino(const void *kern) {  // > 64 KiB of dynamic LDS, once per kernel
+    static std::mutex mu;
+    static std::set<const void *> done;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.count(kern)) return true;
+    if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes) !=
+        hipSuccess)
+        return false;
+    done.insert(kern);
+    return true;
+}
+
+}  // namespace
+
+bool conv3x3_wino_supported(int C, int Cout) {
+    return C % kKC == 0 && C >= kKC && Cout % kCo == 0 && Cout >= kCo;
+}
+
+int launch_conv3x3_wino_weight(const float *w, int Cout, int C, float *U, hipStream_t s) {
+    const int64_t n = (int64_t)Cout * C;
+    if (n == 0) return VD_OK;
+    hipLaunchKernelGGL(wino_weight_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w,
+                       Cout, C, U);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float *U, int Cout,
+                        const float *bias, int relu, float *Y, hipStream_t s) {
+    if ((int64_t)N * H * W == 0) return VD_OK;
+    if (!conv3x3_wino_supported(C, Cout)) return VD_ERR_SHAPE;
+    if ((int64_t)N * H * W * C * 4 >= 0x7ffffff0ll || (int64_t)16 * Cout * C * 4 >= 0x7ffffff0ll)
+        return VD_ERR_SHAPE;  // 32-bit buffer offsets
+    const bool sq = W <= 16;  // small maps (the 14 x 14 mask-head RoIs): 16 x 16-pixel blocks
+    const int tby = sq ? (H + 15) / 16 : (H + 7) / 8;  // else 8 x 32-pixel blocks
+    const int tbx = sq ? (W + 15) / 16 : (W + 31) / 32;
+    const int64_t nsp = (int64_t)N * tby * tbx;
+    const int64_t blocks = (nsp + 7) / 8 * 8 * (Cout / kCo);
+    if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
+    auto kern = sq ? (relu ? conv3x3_wino_kernel<true, 8> : conv3x3_wino_kernel<false, 8>)
+                   : (relu ? conv3x3_wino_kernel<true, 16> : conv3x3_wino_kernel<false, 16>);
+    if (!allow_lds_wino(reinterpret_cast<const void *>(kern))) return VD_ERR_LAUNCH;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kThreads), kLdsBytes, s, X, N, H, W, C,
+                       U, Cout, bias, Y, tby, tbx);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+}  // namespace vd

@@ -39,6 +39,10 @@ bool gemm1x1_mfma_supported(int K, int N);
 bool conv3x3_mfma_supported(int C, int Cout);
 int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float *W2, int Cout,
                         const float *bias, int relu, float *Y, hipStream_t s);
+bool conv3x3_wino_supported(int C, int Cout);
+int launch_conv3x3_wino_weight(const float *w, int Cout, int C, float *U, hipStream_t s);
+int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float *U, int Cout,
+                        const float *bias, int relu, float *Y, hipStream_t s);
 bool gemm1x1_dual_supported(int K1, int K2, int N);
 int launch_gemm1x1_dual(const float *A1, int K1, const float *A2, int K2, int M, const float *W,
                         int N, const float *bias, int relu, float *D, hipStream_t s);

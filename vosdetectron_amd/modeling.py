@@ -60,27 +60,42 @@ def _conv_epi(conv: nn.Conv2d, x, relu=True, res=None, res_bias=None, up=False):
 
 
 _CONV3X3_MIN_PIXELS = 1 << 18  # below this CK's kernels fill the chip better
+_WINO_MIN_PIXELS = 1 << 16
 
 
 def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False):
-    """conv (3x3, stride 1, pad 1) of a channels_last fp32 tensor as the
-    hand-written MFMA implicit GEMM with the bias (+ ReLU) epilogue
-    (ops.conv3x3_bias_act), or None where it does not apply: other geometry,
-    fewer than 2^18 output pixels (P4-P6 of a 16-frame batch), or
-    VOSDET_CONV3X3_MFMA=0.  The permuted weight is cached on the module."""
+    """conv (3x3, stride 1, pad 1) of a channels_last fp32 tensor on the
+    hand-written MFMA kernels with the bias (+ ReLU) epilogue, or None where
+    they do not apply (other geometry, VOSDET_CONV3X3_MFMA=0).  Algorithm
+    (VOSDET_CONV3X3_ALGO): 'wino' -- Winograd F(2x2,3x3), csrc/conv3x3_wino.hip,
+    from 2^16 output pixels -- else / below that the implicit GEMM
+    (csrc/conv3x3.hip) from 2^18 pixels (P4-P6 of a 16-frame batch stay on
+    MIOpen / CK).  The transformed weights are cached on the module."""
     if (os.environ.get("VOSDET_CONV3X3_MFMA", "1") == "0" or not x.is_cuda
             or conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1)
             or conv.dilation != (1, 1) or conv.groups != 1 or x.dtype != torch.float32
-            or x.shape[0] * x.shape[2] * x.shape[3] < _CONV3X3_MIN_PIXELS
             or not x.is_contiguous(memory_format=torch.channels_last)):
         return None
+    npx = x.shape[0] * x.shape[2] * x.shape[3]
     w = conv.weight
     key = (w.data_ptr(), w._version)
+    b = conv.bias.detach() if (bias and conv.bias is not None) else None
+    if os.environ.get("VOSDET_CONV3X3_ALGO", CONV3X3_ALGO) == "wino" and npx >= _WINO_MIN_PIXELS:
+        if getattr(conv, "_vd_u_key", None) != key:
+            conv._vd_u = ops.conv3x3_wino_weight(w.detach())
+            conv._vd_u_key = key
+        y = ops.conv3x3_wino_bias_act(x, conv._vd_u, b, relu=relu)
+        if y is not None:
+            return y
+    if npx < _CONV3X3_MIN_PIXELS:
+        return None
     if getattr(conv, "_vd_w2_key", None) != key:
         conv._vd_w2 = ops.conv3x3_weight(w.detach())
         conv._vd_w2_key = key
-    b = conv.bias.detach() if (bias and conv.bias is not None) else None
     return ops.conv3x3_bias_act(x, conv._vd_w2, b, relu=relu)
+
+
+CONV3X3_ALGO = "wino"  # the 3x3 algorithm the engine uses (VOSDET_CONV3X3_ALGO overrides)
 
 
 def _stage_counts(conv_body: str):
@@ -175,6 +190,11 @@ def _gemm_conv1x1(x, w2d, bias, relu=True, res=None):
             res = res.contiguous(memory_format=torch.channels_last)
         r = _nhwc2d(res)
     y = ops.gemm_bias_act(_nhwc2d(x), w2d, bias, residual=r, relu=relu)
+    if y is None:  # no GEMM algorithm for the shape: MIOpen's 1x1 conv + torch epilogue
+        y = F.conv2d(x, w2d.view(w2d.shape[0], C, 1, 1), bias)
+        if res is not None:
+            y = y + res
+        return F.relu(y) if relu else y
     return y.view(N, H, W, w2d.shape[0]).permute(0, 3, 1, 2)
 
 

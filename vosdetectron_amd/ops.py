@@ -441,7 +441,8 @@ def gemm_bias_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """act(a @ w.T + bias (+ residual)) in one GEMM launch (vd_gemm_bias_act: hipBLASLt
     with the epilogue fused, or the hand-written MFMA kernel where it is faster):
-    a [M,K], w [N,K], bias [N], residual / out [M,N], all fp32 contiguous."""
+    a [M,K], w [N,K], bias [N], residual / out [M,N], all fp32 contiguous.  Returns
+    None when neither serves the shape (the caller falls back)."""
     a_ = _need(a, "a")
     w_ = _need(w, "w")
     b_ = _need(bias, "bias")
@@ -463,10 +464,12 @@ def gemm_bias_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
     if ws is None:  # one stream-ordered workspace per device (single launch stream)
         ws = _ws(lib().vd_gemm_workspace_size(), a_.device)
         _GEMM_WS[a_.device] = ws
-    check(lib().vd_gemm_bias_act(a_.data_ptr(), M, K, w_.data_ptr(), N, b_.data_ptr(),
-                                 r_.data_ptr() if r_ is not None else None, int(relu),
-                                 out.data_ptr(), ws.data_ptr(), ws.numel(), _stream()),
-          "vd_gemm_bias_act")
+    st = lib().vd_gemm_bias_act(a_.data_ptr(), M, K, w_.data_ptr(), N, b_.data_ptr(),
+                                r_.data_ptr() if r_ is not None else None, int(relu),
+                                out.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+    if st == VD_ERR_SHAPE:  # no hipBLASLt algorithm and no MFMA kernel for the shape
+        return None
+    check(st, "vd_gemm_bias_act")
     return out
 
 
@@ -504,6 +507,45 @@ def conv3x3_bias_act(x: torch.Tensor, w2: torch.Tensor, bias: Optional[torch.Ten
     if st == VD_ERR_SHAPE:
         return None
     check(st, "vd_conv3x3_bias_act")
+    return out
+
+
+def conv3x3_wino_weight(w: torch.Tensor) -> torch.Tensor:
+    """PyTorch conv weight [Cout][Cin][3][3] -> the Winograd F(2x2,3x3) operand
+    U = G g G^T as [16][Cout][Cin] (vd_conv3x3_wino_weight; once per model)."""
+    w_ = _need(w, "w")
+    if w_.dim() != 4 or tuple(w_.shape[2:]) != (3, 3):
+        raise ValueError("conv3x3_wino_weight: weight %s" % (tuple(w_.shape),))
+    Cout, C = w_.shape[:2]
+    u = torch.empty((16, Cout, C), dtype=torch.float32, device=w_.device)
+    check(lib().vd_conv3x3_wino_weight(w_.data_ptr(), Cout, C, u.data_ptr(), _stream()),
+          "vd_conv3x3_wino_weight")
+    return u
+
+
+def conv3x3_wino_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch.Tensor],
+                          relu: bool = False, out: Optional[torch.Tensor] = None):
+    """act(conv3x3(x, pad 1) + bias) on a channels_last fp32 tensor by Winograd
+    F(2x2,3x3) on the MFMA pipes (vd_conv3x3_wino_bias_act); u from
+    conv3x3_wino_weight.  Returns None for a shape the kernel does not serve."""
+    if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 4 \
+            or not x.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("x must be a channels_last fp32 device tensor")
+    u_ = _need(u, "u")
+    N, C, H, W = x.shape
+    Cout = u_.shape[1]
+    if u_.dim() != 3 or u_.shape[0] != 16 or u_.shape[2] != C:
+        raise ValueError("u must be [16][Cout][%d], got %s" % (C, tuple(u_.shape)))
+    b_ = _need(bias, "bias") if bias is not None else None
+    if out is None:
+        out = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device,
+                          memory_format=torch.channels_last)
+    st = lib().vd_conv3x3_wino_bias_act(x.data_ptr(), N, H, W, C, u_.data_ptr(), Cout,
+                                        b_.data_ptr() if b_ is not None else None, int(relu),
+                                        out.data_ptr(), _stream())
+    if st == VD_ERR_SHAPE:
+        return None
+    check(st, "vd_conv3x3_wino_bias_act")
     return out
 
 
@@ -777,7 +819,9 @@ def rpn_head(x_raw: torch.Tensor, conv_bias: torch.Tensor, w: torch.Tensor, b: t
 def segm_rle_counts(masks: torch.Tensor, boxes: torch.Tensor, im_h: int, im_w: int,
                     thresh: float = 0.5, cap: Optional[int] = None):
     """paste_masks + mask_rle_counts fused (vd_segm_rle): the same counts and n
-    without materialising the M x im_h x im_w planes."""
+    without materialising the M x im_h x im_w planes.  Frames wider than the
+    fused kernel's LDS column table (VD_ERR_SHAPE) take the two-pass planes path
+    (paste_masks, then mask_rle_counts), which has no width limit."""
     m = _need(masks, "masks")
     b = _need(boxes, "boxes")
     M, R = m.shape[0], m.shape[-1]
@@ -787,9 +831,12 @@ def segm_rle_counts(masks: torch.Tensor, boxes: torch.Tensor, im_h: int, im_w: i
     while True:
         counts = torch.empty((M, cap), dtype=torch.int32, device=m.device)
         n = torch.empty((M,), dtype=torch.int32, device=m.device)
-        check(lib().vd_segm_rle(m.data_ptr(), M, R, b.data_ptr(), b.shape[1], int(im_h),
-                                int(im_w), float(np.float32(thresh)), counts.data_ptr(), cap,
-                                n.data_ptr(), _stream()), "vd_segm_rle")
+        st = lib().vd_segm_rle(m.data_ptr(), M, R, b.data_ptr(), b.shape[1], int(im_h),
+                               int(im_w), float(np.float32(thresh)), counts.data_ptr(), cap,
+                               n.data_ptr(), _stream())
+        if st == VD_ERR_SHAPE:
+            return mask_rle_counts(paste_masks(m, b, im_h, im_w, thresh))
+        check(st, "vd_segm_rle")
         need = int((-n).max().item()) if M else 0
         if need <= cap:
             return counts, n
