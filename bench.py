@@ -603,7 +603,7 @@ def main():
 
     # FPN engines queue a step without any host read (sync=False): the mask
     # batch has pipe.mask_rows(F) rows and the gather ships exactly those
-    asynchronous = hasattr(pipe, "mask_rows")
+    asynchronous = getattr(pipe, "ASYNC", False)
     mask_rows = (pipe.mask_rows(F) if asynchronous
                  else F * max(100, int(cfg.TEST.DETECTIONS_PER_IM)) + 64)
     gatherer = ResultGatherer(F, pipe.det_cap, cfg.MRCNN.RESOLUTION, world, dev,

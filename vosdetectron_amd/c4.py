@@ -179,6 +179,7 @@ class C4FramePipeline(FramePipeline):
       mask RoIAlign 14x14 --> shared res5 --> upconv5 + ReLU --> class-selected
       14x14 masks.
     """
+    ASYNC = False  # run() always reads the counts (the C4 mask batch is host-sized)
 
     def __init__(self, model, cfg, frame_hw=(800, 1333), batch=1, channels_last=False,
                  det_cap=256, device="cuda"):
@@ -199,7 +200,9 @@ class C4FramePipeline(FramePipeline):
                                 roi_order=order, out_layout="nhwc")
         return out.permute(0, 3, 1, 2)  # NCHW view, channels_last memory
 
-    def _run(self, frames: torch.Tensor, keep_intermediates: bool = False):
+    def _run(self, frames: torch.Tensor, keep_intermediates: bool = False, sync: bool = True):
+        # the C4 family sizes its mask batch from the host counts (one read after
+        # the box stage); sync is accepted for the FramePipeline interface
         cfg, tst = self.cfg, self.cfg.TEST
         F_ = frames.shape[0]
         res4 = self.backbone(frames)

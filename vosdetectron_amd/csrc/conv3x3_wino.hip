@@ -20,8 +20,8 @@
 // K is walked in chunks of 8 input channels; per chunk the raw 10 x 34 pixel
 // patch and U's slice are staged in LDS, every thread transforms one (tile,
 // channel) of the NEXT chunk's patch into V while the MFMAs of this chunk run,
-// and the loads of the chunk after that are in flight: two LDS stages, two
-// barriers per chunk.  K permutation (both operands): lane group q at k-step s
+// and the loads of the chunks after that are in flight: two LDS stages, one
+// barrier per chunk.  K permutation (both operands): lane group q at k-step s
 // holds channel 2q + s, so each fragment is one ds_read_b64.
 #include <stdlib.h>
 
@@ -44,9 +44,9 @@ constexpr int kKC = 8;                     // input channels per chunk
 constexpr int kPatchMaxF4 = 680;           // the larger patch (10 x 34 pixels x 8 channels)
 constexpr int kVsF = 16 * kTiles * kKC;    // 8192 floats: V [pos][tile][8]
 constexpr int kUsF = 16 * kCo * kKC;       // 8192 floats: U [pos][co][8]
-constexpr int kPatchF = kPatchMaxF4 * 4;   // 2720 floats: patch [row][col][8]
+constexpr int kPatchF = kPatchMaxF4 * 4 + 4;  // patch [row][col][8] + a 16-byte pad
 constexpr int kStageF = kVsF + kUsF + kPatchF;
-constexpr size_t kLdsBytes = 2 * (size_t)kStageF * 4;  // 152,832 B
+constexpr size_t kLdsBytes = 2 * (size_t)kStageF * 4;  // 152,864 B
 constexpr int kThreads = 512;
 
 // Row-half swizzle of the [.][8] rows: rows r and r + 8 of a 16-row MFMA block
@@ -101,7 +101,8 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_wino_kernel(
         const bool ok = f < kPatchF4 && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
         // out-of-image taps read past the buffer's range: zeros
         poff[i] = ok ? (((n * H + y) * W + x) * C + 4 * h) * 4 : 0x7ffffff0;
-        pdst[i] = f < kPatchF4 ? kVsF + kUsF + 4 * f : -1;
+        // lanes past the patch store into the region's pad (no branch)
+        pdst[i] = kVsF + kUsF + 4 * (f < kPatchF4 ? f : kPatchMaxF4);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -112,20 +113,28 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_wino_kernel(
         udst[i] = kVsF + row * kKC + 4 * (h ^ sw_half(co));
     }
     float4 pr[2], urg[4];
-#define VD_W_LOAD(CH)                                                                        \
+#define VD_W_LOADP(CH)                                                                       \
     {                                                                                        \
         const int cb4_ = (CH) * kKC * 4;                                                     \
         _Pragma("unroll") for (int i = 0; i < 2; ++i) pr[i] = __builtin_bit_cast(            \
             float4, __builtin_amdgcn_raw_buffer_load_b128(                                   \
                         xr, poff[i] == 0x7ffffff0 ? poff[i] : poff[i] + cb4_, 0, 0));        \
+    }
+#define VD_W_LOADU(CH)                                                                       \
+    {                                                                                        \
+        const int cb4_ = (CH) * kKC * 4;                                                     \
         _Pragma("unroll") for (int i = 0; i < 4; ++i) urg[i] = __builtin_bit_cast(           \
             float4, __builtin_amdgcn_raw_buffer_load_b128(ur, uoff[i] + cb4_, 0, 0));        \
     }
-#define VD_W_STORE(STG)                                                                      \
+#define VD_W_STOREP(STG)                                                                     \
     {                                                                                        \
         float *s_ = lds + (STG) * kStageF;                                                   \
-        _Pragma("unroll") for (int i = 0; i < 2; ++i) if (pdst[i] >= 0)                      \
+        _Pragma("unroll") for (int i = 0; i < 2; ++i)                                        \
             *reinterpret_cast<float4 *>(s_ + pdst[i]) = pr[i];                               \
+    }
+#define VD_W_STOREU(STG)                                                                     \
+    {                                                                                        \
+        float *s_ = lds + (STG) * kStageF;                                                   \
         _Pragma("unroll") for (int i = 0; i < 4; ++i)                                        \
             *reinterpret_cast<float4 *>(s_ + udst[i]) = urg[i];                              \
     }
@@ -173,19 +182,27 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_wino_kernel(
         for (int tc = 0; tc < 2; ++tc) acc[p][tc] = f4v{0.f, 0.f, 0.f, 0.f};
 
     const int nch = C / kKC;
-    // prologue: chunk 0 staged and transformed, chunk 1 staged
-    VD_W_LOAD(0)
-    VD_W_STORE(0)
+    // Before phase ch: V(ch), U(ch) in stage ch & 1, patch(ch + 1) in stage
+    // (ch + 1) & 1.  Phase ch reads V / U of stage s = ch & 1 and the patch of
+    // stage s ^ 1, and writes V and U of stage s ^ 1 (V(ch + 1), U(ch + 1)) and
+    // the patch of stage s (patch(ch + 2)): nothing it writes is read in the
+    // phase, so one barrier per chunk.  Loads / stores past the last chunk
+    // re-stage it harmlessly, keeping the body branch-free (one basic block,
+    // so the transform and the staging interleave with the MFMAs).
+    VD_W_LOADP(0)
+    VD_W_LOADU(0)
+    VD_W_STOREP(0)
+    VD_W_STOREU(0)
     __syncthreads();
     VD_W_XFORM(0)
-    if (nch > 1) {
-        VD_W_LOAD(1)
-        VD_W_STORE(1)
-    }
+    VD_W_LOADP(nch > 1 ? 1 : 0)
+    VD_W_STOREP(1)
     __syncthreads();
     for (int ch = 0; ch < nch; ++ch) {
         const int s = ch & 1;
-        if (ch + 2 < nch) VD_W_LOAD(ch + 2)
+        const int c1 = ch + 1 < nch ? ch + 1 : nch - 1, c2 = ch + 2 < nch ? ch + 2 : nch - 1;
+        VD_W_LOADU(c1)
+        VD_W_LOADP(c2)
         const float *st = lds + s * kStageF;
         // four positions at a time: 8 independent accumulators between the two
         // k-steps of one (the 16x16x4 f32 MFMA's dependent latency is 40 cycles)
@@ -211,14 +228,15 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_wino_kernel(
                     acc[p0 + i][tc] = __builtin_amdgcn_mfma_f32_16x16x4f32(
                         a[i][tc].y, b[i].y, acc[p0 + i][tc], 0, 0, 0);
         }
-        // the next chunk's patch -> its V (stage s ^ 1), beside this chunk's MFMAs
-        if (ch + 1 < nch) VD_W_XFORM(s ^ 1)
-        __syncthreads();  // stage s fully read; V of the next chunk written
-        if (ch + 2 < nch) VD_W_STORE(s)
-        __syncthreads();  // chunk ch + 2's patch / U visible
+        VD_W_XFORM(s ^ 1)  // patch(ch + 1) -> V(ch + 1)
+        VD_W_STOREU(s ^ 1)  // U(ch + 1)
+        VD_W_STOREP(s)      // patch(ch + 2)
+        __syncthreads();
     }
-#undef VD_W_LOAD
-#undef VD_W_STORE
+#undef VD_W_LOADP
+#undef VD_W_LOADU
+#undef VD_W_STOREP
+#undef VD_W_STOREU
 #undef VD_W_XFORM
     // output transform (lane-local): A^T = [1 1 1 0; 0 1 -1 -1]; lane (j, q),
     // accumulator slot r holds channel n0 + cg*32 + 16 tc + 4 q + r of tile (tg, j)

@@ -46,6 +46,7 @@ class StageTimer:
 
 
 class FramePipeline:
+    ASYNC = True  # run(sync=False) queues a step with no host read (see run())
     def __init__(self, model, cfg, frame_hw=(800, 1333), batch=1, channels_last=False,
                  det_cap=256, device="cuda"):
         self.model = model
