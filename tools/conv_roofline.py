@@ -6,7 +6,9 @@ call is bracketed by HIP events on the current stream and its FLOPs are
 2 * (output elements) * Cin/groups * kh * kw (2*M*N*K for linear).  The
 C-ABI routes -- the GEMM-epilogue 1x1 convs (ops.gemm_bias_act: hipBLASLt or
 csrc/gemm1x1.hip), the two-operand GEMM (ops.gemm_dual_bias_act), the MFMA
-3x3 conv (ops.conv3x3_bias_act, csrc/conv3x3.hip) and the RPN head
+3x3 conv (ops.conv3x3_bias_act, csrc/conv3x3.hip), the Winograd 3x3 conv
+(ops.conv3x3_wino_bias_act, csrc/conv3x3_wino.hip: FLOPs counted as the
+direct convolution's, so its TF/s can exceed the fp32 peak) and the RPN head
 (ops.rpn_head) -- are wrapped the same way.  Peak:
 157.3 TFLOP/s fp32 MFMA (MI355X_MICROARCH.md; no xf32 on gfx950).
 
@@ -89,6 +91,15 @@ def main():
         return 2.0 * N * H * W * y.shape[1] * C * 9, "conv3x3_mfma x%s Cout%d%s" % (
             list(x.shape), y.shape[1], " +bias" if bias is not None else "")
     ops.conv3x3_bias_act = timed("conv3x3_mfma", cl, ck)
+    wl = ops.conv3x3_wino_bias_act
+
+    def wk(y, x, u, bias, relu=False, out=None):
+        if y is None:
+            return 0.0, "conv3x3_wino (fell back)"
+        N, C, H, W = x.shape
+        return 2.0 * N * H * W * y.shape[1] * C * 9, "conv3x3_wino x%s Cout%d%s" % (
+            list(x.shape), y.shape[1], " +bias" if bias is not None else "")
+    ops.conv3x3_wino_bias_act = timed("conv3x3_wino", wl, wk)
     dl = ops.gemm_dual_bias_act
 
     def dk(y, a1, a2, w, bias, relu=True, out=None):
@@ -114,6 +125,7 @@ def main():
         if gl is not None:
             ops.gemm_bias_act = gl
         ops.conv3x3_bias_act, ops.gemm_dual_bias_act, ops.rpn_head = cl, dl, rl
+        ops.conv3x3_wino_bias_act = wl
     step_ms = e0.elapsed_time(e1)
     agg = collections.OrderedDict()
     for kind, a, b, (fl, key) in recs:

@@ -13,6 +13,10 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libvosdet.so")
+# pinned per-shape GEMM kernel choices (csrc/gemm_epi.cpp): the same file for
+# every process -- GPU tests, bench, all ranks -- so they compute the same numbers
+GEMM_PLANS = os.path.join(_HERE, "gemm_plans.txt")
+os.environ.setdefault("VOSDET_GEMM_PLANS", GEMM_PLANS)
 
 VD_OK, VD_ERR_ARG, VD_ERR_SHAPE, VD_ERR_LAUNCH, VD_ERR_WORKSPACE = range(5)
 VD_LAYOUT_NCHW, VD_LAYOUT_NHWC = 0, 1

@@ -44,9 +44,13 @@ constexpr int kKC = 8;                     // input channels per chunk
 constexpr int kPatchMaxF4 = 680;           // the larger patch (10 x 34 pixels x 8 channels)
 constexpr int kVsF = 16 * kTiles * kKC;    // 8192 floats: V [pos][tile][8]
 constexpr int kUsF = 16 * kCo * kKC;       // 8192 floats: U [pos][co][8]
-constexpr int kPatchF = kPatchMaxF4 * 4 + 4;  // patch [row][col][8] + a 16-byte pad
+// patch pixels are kPixF floats apart (8 channels + 4 pad): the transform's
+// ds_read_b32 lanes (4 tiles, 2 pixels apart, x 8 channels per 32-lane group)
+// then fall on 32 distinct banks (a stride of 8 would be 2-way)
+constexpr int kPixF = 12;
+constexpr int kPatchF = kPatchMaxF4 / 2 * kPixF + 4;  // patch [row][col][12] + a pad
 constexpr int kStageF = kVsF + kUsF + kPatchF;
-constexpr size_t kLdsBytes = 2 * (size_t)kStageF * 4;  // 152,864 B
+constexpr size_t kLdsBytes = 2 * (size_t)kStageF * 4;  // 163,744 B
 constexpr int kThreads = 512;
 
 // Row-half swizzle of the [.][8] rows: rows r and r + 8 of a 16-row MFMA block
@@ -56,7 +60,12 @@ __device__ __forceinline__ int sw_half(int row) { return (row >> 3) & 1; }
 
 // TC tile columns x (64 / TC) tile rows per workgroup: 16 (8 x 32 output pixels)
 // for feature maps, 8 (16 x 16 pixels: one 14 x 14 mask-head RoI) for small ones.
-template <bool RELU, int TC>
+// Schedule variants (VOSDET_WINO_VARIANT, A/B in one process): bit 0 = two
+// barriers per chunk (stores of chunk + 2 between them) instead of one; bit 1 =
+// opaque position stride (plain ds_read_b64 fragment reads, no read2 pairing);
+// bit 2 = sched_group_barrier interleave of transform / staging with the MFMAs;
+// bit 3 = four positions per MFMA group instead of two.
+template <bool RELU, int TC, int V>
 __global__ __launch_bounds__(kThreads, 1) void conv3x3_wino_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx) {
@@ -102,7 +111,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_wino_kernel(
         // out-of-image taps read past the buffer's range: zeros
         poff[i] = ok ? (((n * H + y) * W + x) * C + 4 * h) * 4 : 0x7ffffff0;
         // lanes past the patch store into the region's pad (no branch)
-        pdst[i] = kVsF + kUsF + 4 * (f < kPatchF4 ? f : kPatchMaxF4);
+        pdst[i] = kVsF + kUsF + (f < kPatchF4 ? px * kPixF + 4 * h : kPatchF - 4);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -149,7 +158,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_wino_kernel(
         float d_[4][4];                                                                      \
         _Pragma("unroll") for (int a = 0; a < 4; ++a)                                        \
             _Pragma("unroll") for (int c = 0; c < 4; ++c)                                    \
-                d_[a][c] = p_[((2 * xtr + a) * kPC + 2 * xtc + c) * kKC + xc];               \
+                d_[a][c] = p_[((2 * xtr + a) * kPC + 2 * xtc + c) * kPixF + xc];               \
         float r_[4][4];                                                                      \
         _Pragma("unroll") for (int c = 0; c < 4; ++c) {                                      \
             r_[0][c] = d_[0][c] - d_[2][c];                                                  \
@@ -189,48 +198,93 @@ __global__ __launch_bounds__(kThreads, 1) void conv3x3_wino_kernel(
     // phase, so one barrier per chunk.  Loads / stores past the last chunk
     // re-stage it harmlessly, keeping the body branch-free (one basic block,
     // so the transform and the staging interleave with the MFMAs).
-    VD_W_LOADP(0)
-    VD_W_LOADU(0)
-    VD_W_STOREP(0)
-    VD_W_STOREU(0)
-    __syncthreads();
-    VD_W_XFORM(0)
-    VD_W_LOADP(nch > 1 ? 1 : 0)
-    VD_W_STOREP(1)
-    __syncthreads();
+    constexpr bool kTwoBar = V & 1, kOpaque = V & 2, kInterleave = V & 4;
+    constexpr int kPG = (V & 8) ? 4 : 2;  // positions per MFMA group
+    if (kTwoBar) {
+        // before phase ch: V(ch), U(ch), patch(ch + 1) staged; phase ch: MFMA(ch),
+        // transform patch(ch + 1), barrier, store U / patch of chunk ch + 2, barrier
+        VD_W_LOADP(0)
+        VD_W_LOADU(0)
+        VD_W_STOREP(0)
+        VD_W_STOREU(0)
+        __syncthreads();
+        VD_W_XFORM(0)
+        VD_W_LOADP(nch > 1 ? 1 : 0)
+        VD_W_LOADU(nch > 1 ? 1 : 0)
+        VD_W_STOREP(1)
+        VD_W_STOREU(1)
+        __syncthreads();
+    } else {
+        VD_W_LOADP(0)
+        VD_W_LOADU(0)
+        VD_W_STOREP(0)
+        VD_W_STOREU(0)
+        __syncthreads();
+        VD_W_XFORM(0)
+        VD_W_LOADP(nch > 1 ? 1 : 0)
+        VD_W_STOREP(1)
+        __syncthreads();
+    }
     for (int ch = 0; ch < nch; ++ch) {
         const int s = ch & 1;
         const int c1 = ch + 1 < nch ? ch + 1 : nch - 1, c2 = ch + 2 < nch ? ch + 2 : nch - 1;
-        VD_W_LOADU(c1)
+        if (kTwoBar) {
+            VD_W_LOADU(c2)
+        } else {
+            VD_W_LOADU(c1)
+        }
         VD_W_LOADP(c2)
         const float *st = lds + s * kStageF;
-        // four positions at a time: 8 independent accumulators between the two
-        // k-steps of one (the 16x16x4 f32 MFMA's dependent latency is 40 cycles)
+        // with kOpaque, an opaque position stride: hipcc would otherwise pair the
+        // fragment reads of two positions into ds_read2st64_b64, whose 16-lane /
+        // 32-bank groups are 2-way conflicted on this layout (ds_read_b64 is not)
+        int vps = kTiles * kKC, ups = kCo * kKC;
+        if (kOpaque) asm volatile("" : "+v"(vps), "+v"(ups));
+        // kPG positions at a time: 2 kPG independent MFMAs between the two k-steps
+        // of one accumulator (dependent latency 40 cycles)
 #pragma unroll
-        for (int p0 = 0; p0 < 16; p0 += 4) {
-            f2v b[4], a[4][2];
+        for (int p0 = 0; p0 < 16; p0 += kPG) {
+            f2v b[kPG], a[kPG][2];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                b[i] = *reinterpret_cast<const f2v *>(st + (p0 + i) * kTiles * kKC + vfo);
-                a[i][0] = *reinterpret_cast<const f2v *>(st + (p0 + i) * kCo * kKC + ufo[0]);
-                a[i][1] = *reinterpret_cast<const f2v *>(st + (p0 + i) * kCo * kKC + ufo[1]);
+            for (int i = 0; i < kPG; ++i) {
+                const int vo = (p0 + i) * vps + vfo, uo = (p0 + i) * ups;  // 32-bit LDS offsets
+                b[i] = *reinterpret_cast<const f2v *>(st + vo);
+                a[i][0] = *reinterpret_cast<const f2v *>(st + uo + ufo[0]);
+                a[i][1] = *reinterpret_cast<const f2v *>(st + uo + ufo[1]);
             }
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < kPG; ++i)
 #pragma unroll
                 for (int tc = 0; tc < 2; ++tc)
                     acc[p0 + i][tc] = __builtin_amdgcn_mfma_f32_16x16x4f32(
                         a[i][tc].x, b[i].x, acc[p0 + i][tc], 0, 0, 0);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < kPG; ++i)
 #pragma unroll
                 for (int tc = 0; tc < 2; ++tc)
                     acc[p0 + i][tc] = __builtin_amdgcn_mfma_f32_16x16x4f32(
                         a[i][tc].y, b[i].y, acc[p0 + i][tc], 0, 0, 0);
         }
         VD_W_XFORM(s ^ 1)  // patch(ch + 1) -> V(ch + 1)
-        VD_W_STOREU(s ^ 1)  // U(ch + 1)
-        VD_W_STOREP(s)      // patch(ch + 2)
+        if (kTwoBar) {
+            __syncthreads();    // stage s fully read; V(ch + 1) written
+            VD_W_STOREU(s)      // U(ch + 2)
+            VD_W_STOREP(s)      // patch(ch + 2)
+        } else {
+            VD_W_STOREU(s ^ 1)  // U(ch + 1)
+            VD_W_STOREP(s)      // patch(ch + 2)
+        }
+        if (kInterleave) {
+            // transform / staging instructions into the issue shadows of the
+            // MFMAs (32 cycles each on the SIMD) instead of after them
+#pragma unroll
+            for (int k = 0; k < 40; ++k) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 LDS read
+                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // 1 VALU
+                __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // 1 LDS write
+            }
+        }
         __syncthreads();
     }
 #undef VD_W_LOADP
@@ -328,6 +382,30 @@ int launch_conv3x3_wino_weight(const float *w, int Cout, int C, float *U, hipStr
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
+typedef void (*wino_kern_t)(const float *, int, int, int, int, const float *, int,
+                            const float *, float *, int, int);
+
+template <int V>
+wino_kern_t pick_v(bool relu, bool sq) {
+    return sq ? (relu ? conv3x3_wino_kernel<true, 8, V> : conv3x3_wino_kernel<false, 8, V>)
+              : (relu ? conv3x3_wino_kernel<true, 16, V> : conv3x3_wino_kernel<false, 16, V>);
+}
+
+wino_kern_t pick_kernel(bool relu, bool sq, int v) {
+    switch (v) {
+        case 0: return pick_v<0>(relu, sq);   // one barrier, read2 pairs, 2-pos groups
+        case 1: return pick_v<1>(relu, sq);   // two barriers
+        case 6: return pick_v<6>(relu, sq);   // one barrier, plain b64 reads, interleave
+        case 8: return pick_v<8>(relu, sq);   // one barrier, 4-pos groups
+        case 9: return pick_v<9>(relu, sq);   // two barriers, 4-pos groups (round-3 first form)
+        case 11: return pick_v<11>(relu, sq); // two barriers, plain b64, 4-pos groups
+        case 13: return pick_v<13>(relu, sq); // two barriers, interleave, 4-pos groups
+        default: return nullptr;
+    }
+}
+
+constexpr int kDefaultVariant = 0;
+
 int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float *U, int Cout,
                         const float *bias, int relu, float *Y, hipStream_t s) {
     if ((int64_t)N * H * W == 0) return VD_OK;
@@ -340,8 +418,13 @@ int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float 
     const int64_t nsp = (int64_t)N * tby * tbx;
     const int64_t blocks = (nsp + 7) / 8 * 8 * (Cout / kCo);
     if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
-    auto kern = sq ? (relu ? conv3x3_wino_kernel<true, 8> : conv3x3_wino_kernel<false, 8>)
-                   : (relu ? conv3x3_wino_kernel<true, 16> : conv3x3_wino_kernel<false, 16>);
+    // schedule variant (see the kernel): default 0 = one barrier per chunk, read2
+    // fragment pairs, two positions per MFMA group -- best or tied-best on all four
+    // benched shapes in one-process A/B (tools/probe_wino_variants.py)
+    const char *ev = getenv("VOSDET_WINO_VARIANT");
+    const int v = ev ? atoi(ev) : kDefaultVariant;
+    auto kern = pick_kernel(relu != 0, sq, v);
+    if (!kern) return VD_ERR_ARG;
     if (!allow_lds_wino(reinterpret_cast<const void *>(kern))) return VD_ERR_LAUNCH;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kThreads), kLdsBytes, s, X, N, H, W, C,
                        U, Cout, bias, Y, tby, tbx);

@@ -23,10 +23,22 @@
 // For those shapes the search also times the hand-written MFMA kernel
 // (gemm1x1.hip) and keeps it when it is faster; VOSDET_GEMM_MFMA=1 forces it
 // (where supported), =0 excludes it.
+//
+// Pinned choices (the timed search may pick different kernels --
+// different summation orders -- in different processes): VOSDET_GEMM_PLANS
+// names a text file of "M N K relu has_res choice" lines (choice = "own" or
+// "blas <i>", i = the index in hipBLASLt's heuristic list for the shape, stable
+// for one library build and GPU).  A listed shape uses its choice without a
+// search, so every process that reads the same file -- the GPU tests and the
+// bench, every rank of a multi-GPU run -- computes the same numbers.  With
+// VOSDET_GEMM_PLANS_RECORD=1 the result of each new search is appended to it.
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
 
 #include <stdlib.h>
+
+#include <stdio.h>
+#include <string.h>
 
 #include <map>
 #include <mutex>
@@ -53,7 +65,45 @@ struct Plan {
 
 std::mutex g_mu;
 hipblasLtHandle_t g_handle = nullptr;
-std::map<std::tuple<int, int, int, int, int>, Plan> g_plans;  // (M, N, K, relu, has_res)
+typedef std::tuple<int, int, int, int, int> Key;  // (M, N, K, relu, has_res)
+std::map<Key, Plan> g_plans;
+std::map<Key, int> g_pinned;  // -1: the MFMA kernel, i >= 0: heuristic candidate i
+bool g_pins_loaded = false;
+
+void load_pins() {  // once, under g_mu
+    if (g_pins_loaded) return;
+    g_pins_loaded = true;
+    const char *path = getenv("VOSDET_GEMM_PLANS");
+    if (!path || !path[0]) return;
+    FILE *f = fopen(path, "r");
+    if (!f) return;
+    char line[256];
+    while (fgets(line, sizeof line, f)) {
+        int M, N, K, relu, res, idx = 0;
+        char what[16];
+        const int n = sscanf(line, "%d %d %d %d %d %15s %d", &M, &N, &K, &relu, &res, what, &idx);
+        if (n >= 6 && strcmp(what, "own") == 0)
+            g_pinned[Key(M, N, K, relu, res)] = -1;
+        else if (n == 7 && strcmp(what, "blas") == 0 && idx >= 0)
+            g_pinned[Key(M, N, K, relu, res)] = idx;
+    }
+    fclose(f);
+}
+
+void record_pin(const Key &k, int choice) {
+    const char *rec = getenv("VOSDET_GEMM_PLANS_RECORD");
+    const char *path = getenv("VOSDET_GEMM_PLANS");
+    if (!rec || rec[0] != '1' || !path || !path[0]) return;
+    FILE *f = fopen(path, "a");
+    if (!f) return;
+    if (choice < 0)
+        fprintf(f, "%d %d %d %d %d own\n", std::get<0>(k), std::get<1>(k), std::get<2>(k),
+                std::get<3>(k), std::get<4>(k));
+    else
+        fprintf(f, "%d %d %d %d %d blas %d\n", std::get<0>(k), std::get<1>(k), std::get<2>(k),
+                std::get<3>(k), std::get<4>(k), choice);
+    fclose(f);
+}
 
 constexpr size_t kMaxWs = 64ull << 20;
 
@@ -63,6 +113,7 @@ hipblasLtHandle_t handle() {
 }
 
 Plan *plan_for(int M, int N, int K, int relu, int has_res) {
+    load_pins();
     auto key = std::make_tuple(M, N, K, relu, has_res);
     auto it = g_plans.find(key);
     if (it != g_plans.end()) return it->second.ok ? &it->second : nullptr;
@@ -97,6 +148,17 @@ Plan *plan_for(int M, int N, int K, int relu, int has_res) {
     p.algo = p.cand[0].algo;
     p.ws = p.cand[0].workspaceSize;
     p.ok = true;
+    auto pin = g_pinned.find(key);
+    if (pin != g_pinned.end()) {  // a pinned choice: no timing search
+        if (pin->second < 0 && gemm1x1_mfma_supported(K, N)) {
+            p.own = true;
+            p.searched = true;
+        } else if (pin->second >= 0 && pin->second < n) {
+            p.algo = p.cand[pin->second].algo;
+            p.ws = p.cand[pin->second].workspaceSize;
+            p.searched = true;
+        }
+    }
     return &p;
 }
 
@@ -166,6 +228,7 @@ void search(Plan &p, int M, int N, int K, int relu, const float *A, const float 
         p.algo = p.cand[best_i].algo;
         p.ws = p.cand[best_i].workspaceSize;
     }
+    record_pin(Key(M, N, K, relu, R ? 1 : 0), p.own ? -1 : (best_i >= 0 ? best_i : 0));
 }
 
 }  // namespace
