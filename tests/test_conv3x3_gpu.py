@@ -67,7 +67,7 @@ def test_conv3x3_mid_tiles_vs_torch(monkeypatch, N, C, H, W, Cout):
 def test_conv3x3_wino_vs_torch(N, C, H, W, Cout, relu):
     """Winograd F(2x2,3x3) MFMA kernel (csrc/conv3x3_wino.hip) vs a plain torch
     fp32 conv2d(pad 1) + bias (+ ReLU): odd sizes (partial tiles and tile
-    blocks), a 1x1 image, Cin 8..256, Cout 64..256."""
+    blocks; both block shapes), a 1x1 image, Cin 8..256, Cout 64..256."""
     from vosdetectron_amd import ops
     g = torch.Generator(device="cpu").manual_seed(7 * N + C + H + W + Cout)
     x = torch.randn(N, C, H, W, generator=g).cuda().contiguous(memory_format=torch.channels_last)
