@@ -140,9 +140,10 @@ int vd_conv3x3_bias_act(const float *X, int N, int H, int W, int C, const float 
 
 /* The same convolution by Winograd F(2x2, 3x3) on the MFMA pipes (2.25x fewer
  * multiplies; the transforms add, subtract and halve): U from
- * vd_conv3x3_wino_weight (16 x Cout x Cin fp32, once per model) replaces W2.
- * Requires Cin % 8 == 0 and Cout % 64 == 0 (VD_ERR_SHAPE otherwise).  Results
- * agree with the direct form within fp32 rounding (not bit for bit). */
+ * vd_conv3x3_wino_weight (16 x Cout x Cin fp32 in an opaque chunk-blocked order,
+ * once per model) replaces W2.  Both require Cin % 8 == 0 and Cout % 64 == 0
+ * (VD_ERR_SHAPE otherwise).  Results agree with the direct form within fp32
+ * rounding (not bit for bit). */
 int vd_conv3x3_wino_weight(const float *w, int Cout, int Cin, float *U, void *stream);
 int vd_conv3x3_wino_bias_act(const float *X, int N, int H, int W, int C, const float *U,
                              int Cout, const float *bias, int relu, float *Y, void *stream);

@@ -120,12 +120,11 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     const int tg = wave & 1, cg = wave >> 1;  // wave: tiles 16 tg .. + 15, 32-channel group
     const uint32_t sbase = (uint32_t)(uintptr_t)sm;
 
-    // U DMA: blocks b = wave + 4 i (i < 8) of 64 slots, slot s = 64 b + lane =
-    // 2 (pos * 64 + co) + half: co fixed per lane, pos = pos0 + 2 i
-    const int urow0 = 32 * wave + (lane >> 1);
-    const int uco = urow0 & 63, upos0 = urow0 >> 6;
-    const float *usrc = U + ((int64_t)(upos0 * Cout + n0 + uco) * C + 4 * (lane & 1));
-    const int64_t ustep = (int64_t)2 * Cout * C;
+    // U DMA: U is stored chunk-blocked, [Cout / 64][C / 8][16][64][8], so a
+    // chunk's slice is one contiguous 32 KiB run copied verbatim (whole cache
+    // lines per wave instruction); blocks b = wave + 4 i (i < 8) of 64 slots
+    const int nch = C / kKC;
+    const float *usrc = U + (int64_t)cb * nch * (16 * kCo * kKC) + wave * 256 + lane * 4;
     // patch DMA: blocks b = wave + 4 i (i < 2); slots outside the patch or the
     // image copy zeros
     const float *psrc[2];
@@ -146,9 +145,9 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
 #define VD_W2_DMA(CH, ST)                                                                    \
     {                                                                                        \
         const uint32_t d_ = sbase + (uint32_t)(ST) * k2StageB + (uint32_t)wave * 1024u;      \
-        const float *u_ = usrc + (int64_t)(CH) * kKC;                                        \
+        const float *u_ = usrc + (int64_t)(CH) * (16 * kCo * kKC);                           \
         _Pragma("unroll") for (int i = 0; i < 8; ++i)                                        \
-            wino_dma_1k(u_ + i * ustep, d_ + (uint32_t)i * 4096u);                           \
+            wino_dma_1k(u_ + i * 1024, d_ + (uint32_t)i * 4096u);                            \
         _Pragma("unroll") for (int i = 0; i < 2; ++i)                                        \
             wino_dma_1k(pok[i] ? psrc[i] + (CH) * kKC : zero,                                \
                         d_ + (uint32_t)(k2USlots * 16) + (uint32_t)i * 4096u);               \
@@ -175,7 +174,6 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
 #pragma unroll
         for (int t2 = 0; t2 < 2; ++t2) acc[p][t2] = f4v{0.f, 0.f, 0.f, 0.f};
 
-    const int nch = C / kKC;
     VD_W2_DMA(0, 0)
     wino_wait_barrier();
     for (int ch = 0; ch < nch; ++ch) {
@@ -273,15 +271,18 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     }
 }
 
-// U[pos][co][ci'] = (G g G^T)[pos / 4][pos % 4] of the PyTorch weight
-// w[co][ci][3][3]; G = [1 0 0; .5 .5 .5; .5 -.5 .5; 0 0 1]; float64, rounded once;
-// ci' = ci with its 8-byte unit within the 8-channel block swizzled by sw_unit.
+// U = G g G^T of the PyTorch weight w[co][ci][3][3], G = [1 0 0; .5 .5 .5;
+// .5 -.5 .5; 0 0 1], float64, rounded once; stored chunk-blocked as
+// [co / 64][ci / 8][pos][co % 64][ci'] with ci' = ci % 8 with its 8-byte unit
+// swizzled by sw_unit(co).
 __global__ void wino_weight_kernel(const float *__restrict__ w, int Cout, int C,
                                    float *__restrict__ U) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)Cout * C) return;
     const int co = (int)(i / C), ci = (int)(i - (int64_t)(i / C) * C);
-    const int cs = (ci & ~7) | ((((ci >> 1) & 3) ^ sw_unit(co)) << 1) | (ci & 1);
+    const int cs = ((((ci >> 1) & 3) ^ sw_unit(co)) << 1) | (ci & 1);
+    float *dst = U + ((int64_t)(co / kCo) * (C / kKC) + ci / kKC) * (16 * kCo * kKC) +
+                 (co % kCo) * kKC + cs;
     const float *g = w + i * 9;
     double t[4][3];  // G g
     for (int c = 0; c < 3; ++c) {
@@ -295,7 +296,7 @@ __global__ void wino_weight_kernel(const float *__restrict__ w, int Cout, int C,
         const double u[4] = {t[a][0], 0.5 * (t[a][0] + t[a][1] + t[a][2]),
                              0.5 * (t[a][0] - t[a][1] + t[a][2]), t[a][2]};
         for (int b = 0; b < 4; ++b)
-            U[((int64_t)(4 * a + b) * Cout + co) * C + cs] = (float)u[b];
+            dst[(4 * a + b) * kCo * kKC] = (float)u[b];
     }
 }
 
@@ -308,6 +309,7 @@ bool conv3x3_wino_supported(int C, int Cout) {
 int launch_conv3x3_wino_weight(const float *w, int Cout, int C, float *U, hipStream_t s) {
     const int64_t n = (int64_t)Cout * C;
     if (n == 0) return VD_OK;
+    if (!conv3x3_wino_supported(C, Cout)) return VD_ERR_SHAPE;
     hipLaunchKernelGGL(wino_weight_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w,
                        Cout, C, U);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;

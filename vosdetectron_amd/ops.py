@@ -510,14 +510,18 @@ def conv3x3_bias_act(x: torch.Tensor, w2: torch.Tensor, bias: Optional[torch.Ten
     return out
 
 
-def conv3x3_wino_weight(w: torch.Tensor) -> torch.Tensor:
+def conv3x3_wino_weight(w: torch.Tensor) -> Optional[torch.Tensor]:
     """PyTorch conv weight [Cout][Cin][3][3] -> the Winograd F(2x2,3x3) operand
-    U = G g G^T as [16][Cout][Cin] (vd_conv3x3_wino_weight; once per model)."""
+    U = G g G^T, chunk-blocked as [Cout/64][Cin/8][16][64][8] (channel pairs
+    swizzled within a row; vd_conv3x3_wino_weight; once per model).  None for
+    a shape the kernel does not serve (Cout % 64, Cin % 8)."""
     w_ = _need(w, "w")
     if w_.dim() != 4 or tuple(w_.shape[2:]) != (3, 3):
         raise ValueError("conv3x3_wino_weight: weight %s" % (tuple(w_.shape),))
     Cout, C = w_.shape[:2]
-    u = torch.empty((16, Cout, C), dtype=torch.float32, device=w_.device)
+    if Cout % 64 or C % 8 or Cout == 0 or C == 0:
+        return None
+    u = torch.empty((Cout // 64, C // 8, 16, 64, 8), dtype=torch.float32, device=w_.device)
     check(lib().vd_conv3x3_wino_weight(w_.data_ptr(), Cout, C, u.data_ptr(), _stream()),
           "vd_conv3x3_wino_weight")
     return u
@@ -531,11 +535,13 @@ def conv3x3_wino_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch
     if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 4 \
             or not x.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("x must be a channels_last fp32 device tensor")
+    if u is None:
+        return None
     u_ = _need(u, "u")
     N, C, H, W = x.shape
-    Cout = u_.shape[1]
-    if u_.dim() != 3 or u_.shape[0] != 16 or u_.shape[2] != C:
-        raise ValueError("u must be [16][Cout][%d], got %s" % (C, tuple(u_.shape)))
+    if u_.dim() != 5 or tuple(u_.shape[1:]) != (C // 8, 16, 64, 8) or C % 8:
+        raise ValueError("u must be [Cout/64][%d][16][64][8], got %s" % (C // 8, tuple(u_.shape)))
+    Cout = u_.shape[0] * 64
     b_ = _need(bias, "bias") if bias is not None else None
     if out is None:
         out = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device,
