@@ -259,9 +259,38 @@ def frame_flops(sd, cfg):
     fuses or lays out the contractions.  Returns (flops, detections)."""
     from torch.utils.flop_counter import FlopCounterMode
     ref, fr, _ = ref_cpu_pipeline(sd, 0, cfg)
-    with FlopCounterMode(display=False) as fc:
+    with FlopCounterMode(display=False) as fc, _WinoFlops() as wf:
         res = ref(fr[0])
-    return int(fc.get_total_flops()), int(len(res[1]))
+    return int(fc.get_total_flops()), int(len(res[1])), wf.flops
+
+
+class _WinoFlops(torch.overrides.TorchFunctionMode):
+    """Direct-form FLOPs of the frame's 3x3 convolutions the engine runs as
+    Winograd F(2x2,3x3) (modeling._conv3x3_mfma: stride 1, pad 1, Cout % 64,
+    Cin % 8, >= 2^16 output pixels over the 16-frame batch): their MFMA work is
+    1/2.25 of the direct form's."""
+
+    def __init__(self, frames=16):
+        super().__init__()
+        self.flops, self.frames = 0, frames
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        out = func(*args, **kwargs)
+        if func in (torch.nn.functional.conv2d, torch.conv2d):
+            x, w = args[0], args[1]
+            rest = list(args[3:]) + [None] * 4
+            stride = kwargs.get("stride", rest[0] if rest[0] is not None else 1)
+            padding = kwargs.get("padding", rest[1] if rest[1] is not None else 0)
+            groups = kwargs.get("groups", rest[3] if rest[3] is not None else 1)
+            st = tuple(stride) if isinstance(stride, (tuple, list)) else (stride, stride)
+            pd = tuple(padding) if isinstance(padding, (tuple, list)) else (padding, padding)
+            Cout, Cin = w.shape[0], w.shape[1]
+            npx = out.shape[0] * out.shape[2] * out.shape[3]
+            if (tuple(w.shape[2:]) == (3, 3) and st == (1, 1) and pd == (1, 1) and groups == 1
+                    and Cout % 64 == 0 and Cin % 8 == 0 and npx * self.frames >= 1 << 16):
+                self.flops += 2 * npx * Cout * Cin * 9
+        return out
 
 
 def measure_hbm_copy(dev, nbytes=2 << 30, iters=20):
@@ -289,13 +318,19 @@ def measure_hbm_copy(dev, nbytes=2 << 30, iters=20):
 MFMA_FP32_PEAK_TFS = 157.3  # MI355X dense fp32 matrix peak
 
 
-def step_roofline(flops_frame, dets_cpu, frames, ms_per_step, engine_launch, frame_hw, blob_hw):
+def step_roofline(flops_frame, dets_cpu, frames, ms_per_step, engine_launch, frame_hw, blob_hw,
+                  wino_flops_frame=0):
     """the FPS as a fraction of the roofline = sum of per-stage
     bound times / measured step time.  MFMA-bound stages: the frame's algorithmic
     FLOPs at the fp32 matrix peak; HBM-bound stages: the box RoIAlign's algorithmic
     bytes (the engine's own launch) and frame prep (u8 read + fp32 blob write) at
-    8 TB/s; latency-bound stages (proposals, NMS) carry no bound."""
+    8 TB/s; latency-bound stages (proposals, NMS) carry no bound.  'frac' prices
+    every convolution in its direct form (so Winograd can take it past 1);
+    'frac_executed' prices the Winograd convolutions at the 1/2.25 of that their
+    MFMAs execute -- the bound the engine's own algorithm choice can reach."""
     mfma_ms = flops_frame * frames / (MFMA_FP32_PEAK_TFS * 1e12) * 1e3
+    exec_flops = flops_frame - wino_flops_frame * (1 - 1 / 2.25)
+    exec_ms = exec_flops * frames / (MFMA_FP32_PEAK_TFS * 1e12) * 1e3
     h, w = frame_hw
     blob_bytes = frames * (h * w * 3 + 3 * 4 * blob_hw[0] * blob_hw[1])
     ra_bytes = engine_launch["algorithmic_bytes_per_launch"] if engine_launch else 0
@@ -303,6 +338,10 @@ def step_roofline(flops_frame, dets_cpu, frames, ms_per_step, engine_launch, fra
     bound = mfma_ms + hbm_ms
     return {"bound_ms_per_step": round(bound, 3), "mfma_bound_ms": round(mfma_ms, 3),
             "hbm_bound_ms": round(hbm_ms, 3), "frac": round(bound / ms_per_step, 4),
+            "executed": {"gflop_per_frame": round(exec_flops / 1e9, 2),
+                         "winograd_direct_gflop_per_frame": round(wino_flops_frame / 1e9, 2),
+                         "mfma_bound_ms": round(exec_ms, 3),
+                         "frac": round((exec_ms + hbm_ms) / ms_per_step, 4)},
             "gflop_per_frame": round(flops_frame / 1e9, 2), "dets_in_counted_frame": dets_cpu,
             "mfma_util_step": round(mfma_ms / ms_per_step, 4),
             "peaks": {"fp32_matrix_TFs": MFMA_FP32_PEAK_TFS, "hbm_GBs": HBM_PEAK_GBS},
@@ -720,12 +759,13 @@ def main():
         extra["hbm_copy"] = measure_hbm_copy(dev)
         nthr = torch.get_num_threads()
         torch.set_num_threads(cpu_share()[0])
-        flops, dets_cpu = frame_flops(sd, cfg)
+        flops, dets_cpu, wino_flops = frame_flops(sd, cfg)
         torch.set_num_threads(nthr)
         extra["step_roofline"] = step_roofline(
             flops, dets_cpu, F, dt / args.steps * 1e3, roof.get("engine_launch") if roof else None,
             (fh, fw),
-            (getattr(pipe, "Hp", fh), getattr(pipe, "Wp", fw)))
+            (getattr(pipe, "Hp", fh), getattr(pipe, "Wp", fw)),
+            wino_flops if getattr(pipe, "ASYNC", False) and not vos else 0)
     cpu = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:
         cpu = cpu_baseline(args.config, sd, args.cpu_frames, cfg=cfg)

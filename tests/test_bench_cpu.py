@@ -19,6 +19,27 @@ def test_step_roofline_sums_stage_bounds():
     assert abs(r["hbm_bound_ms"] - round(hbm_ms, 3)) < 1e-6
     assert abs(r["frac"] - round((mfma_ms + hbm_ms) / 72.0, 4)) < 1e-9
     assert r["frac"] < 1.0
+    # executed work: the Winograd convolutions' share at 1/2.25 of its direct FLOPs
+    r2 = bench.step_roofline(528e9, 100, 16, 72.0, {"algorithmic_bytes_per_launch": 2.0e9},
+                             (800, 1333), (800, 1344), wino_flops_frame=300e9)
+    ex = (528e9 - 300e9 * (1 - 1 / 2.25)) * 16 / 157.3e12 * 1e3
+    assert abs(r2["executed"]["mfma_bound_ms"] - round(ex, 3)) < 1e-6
+    assert r2["executed"]["frac"] < r2["frac"]
+
+
+def test_winograd_flop_classifier():
+    """bench._WinoFlops counts exactly the 3x3 / stride-1 / pad-1 convolutions
+    with Cout % 64 == 0, Cin % 8 == 0 and >= 2^16 batch output pixels."""
+    import torch
+    import torch.nn.functional as F
+    x = torch.randn(1, 8, 64, 64)
+    with bench._WinoFlops(frames=16) as wf:
+        F.conv2d(x, torch.randn(64, 8, 3, 3), None, 1, 1)        # counted: 16*4096 px
+        F.conv2d(x, torch.randn(64, 8, 3, 3), None, 2, 1)        # stride 2
+        F.conv2d(x, torch.randn(32, 8, 3, 3), None, 1, 1)        # Cout 32
+        F.conv2d(x, torch.randn(64, 8, 1, 1))                    # 1x1
+        F.conv2d(x[:, :, :8, :8], torch.randn(64, 8, 3, 3), padding=1)  # 16*64 px
+    assert wf.flops == 2 * 4096 * 64 * 8 * 9
 
 
 def test_roi_align_algorithmic_bytes_counts_union_once():
