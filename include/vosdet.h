@@ -85,6 +85,23 @@ int vd_roi_align_fpn_forward(const VdFeatLevel *levels, int num_levels, int B, i
                              int aligned_width, int sampling_ratio, int output_layout,
                              float *output, void *stream);
 
+/* Tile-binned, LDS-staged multi-level RoIAlign: the same operation as
+ * vd_roi_align_fpn_forward(layout = output_layout = VD_LAYOUT_NHWC,
+ * aligned_height = aligned_width = aligned_size) -- the per-level loop + cat +
+ * unshuffle of roi_feature_transform (lib/modeling/model_builder.py:252-303)
+ * over the Caffe2 RoIAlign of lib/modeling/roi_xfrom/roi_align/src/
+ * roi_align_kernel.cu:65-121 -- computed in the reference's per-sample
+ * arithmetic (bit-identical to it).  Serves sampling_ratio 2, C % 32 == 0,
+ * B <= 64, aligned_size <= 64; returns VD_ERR_SHAPE otherwise (callers then use
+ * vd_roi_align_fpn_forward).  workspace: >= vd_roi_align_fpn_tiled_workspace_size()
+ * bytes of device memory, stream-ordered (no host sync, graph-capturable). */
+size_t vd_roi_align_fpn_tiled_workspace_size(const VdFeatLevel *levels, int num_levels, int B,
+                                             int C, int num_rois, int aligned_size);
+int vd_roi_align_fpn_tiled_forward(const VdFeatLevel *levels, int num_levels, int B, int C,
+                                   const float *rois, const int32_t *roi_level, int num_rois,
+                                   int aligned_size, int sampling_ratio, float *output,
+                                   void *workspace, size_t workspace_bytes, void *stream);
+
 /* jwyang RoIAlign (legacy, lib/model/roi_align).  Replaces
  * roi_align_forward_cuda(int aligned_height, int aligned_width, float
  * spatial_scale, THCudaTensor *features, THCudaTensor *rois, THCudaTensor

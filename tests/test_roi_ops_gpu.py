@@ -277,3 +277,84 @@ def test_roi_align_lds_bit_exact(P):
     feats = [p[0:1].permute(0, 3, 1, 2).cpu().numpy() for p in pyr]
     oref = orc.roi_feature_transform(feats[::-1], d, "rois", P, scales[::-1], 2)
     assert np.array_equal(ref[sel].transpose(0, 3, 1, 2), oref)
+
+
+@pytest.mark.parametrize("P", [7, 14])
+def test_roi_align_tiled_bit_exact(P):
+    """The tile-binned LDS-staged kernel (variant 30, roi_align_tile.hip) computes
+    every output with the reference's per-sample arithmetic: bit-identical to the
+    reference-order row kernel (variant 3) and to the oracle's per-level loop, on
+    3 frames of the 800x1333 pyramid incl. RoIs off the map (zero bins), degenerate,
+    at the border, wider than a tile window (direct bins), a dense pile of RoIs on
+    one tile (chunked items) and out-of-range level / batch indices (zeros)."""
+    import os
+    from vosdetectron_amd import ops
+    from bench import fpn_levels_np, synthetic_rois
+    C, F = 256, 3
+    g = torch.Generator(device=DEV).manual_seed(13)
+    sizes = [(200, 336), (100, 168), (50, 84), (25, 42)]
+    pyr = [torch.randn((F, h, w, C), generator=g, device=DEV) for h, w in sizes]
+    rois = np.concatenate([synthetic_rois(f + 9, 400, batch_idx=f) for f in range(F)])
+    rois[:8, 1:5] = [[-30, -20, 40, 30], [1300, 780, 1400, 900], [0, 0, 0.5, 0.5],
+                     [1320, 790, 1332.9, 799.9], [0, 400, 1332, 420],  # 167 px wide at P3
+                     [-200, 100, 1500, 140], [0, 0, 1332, 799],  # whole frame at P5: direct
+                     [600, -50, 620, 1000]]
+    rng = np.random.default_rng(5)
+    xy = rng.uniform(500, 560, (60, 2))  # 60 small boxes on one P2 tile: > 128 bins
+    rois[8:68, 1:5] = np.hstack([xy, xy + rng.uniform(4, 30, (60, 2))])
+    lv = fpn_levels_np(rois) - 2
+    lv[68], lv[69] = 7, -1  # malformed level indices pool to zero
+    rois[70, 0] = 5  # batch index past the pyramid
+    rt, lt = torch.from_numpy(rois).to(DEV), torch.from_numpy(lv).to(DEV)
+    scales = [1. / 4, 1. / 8, 1. / 16, 1. / 32]
+
+    def run(variant, **kw):
+        os.environ["VOSDET_ROIALIGN_VARIANT"] = variant
+        try:
+            return ops.roi_align_fpn(pyr, scales, rt, lt, P, 2, out_layout="nhwc",
+                                     **kw).cpu().numpy()
+        finally:
+            del os.environ["VOSDET_ROIALIGN_VARIANT"]
+    ref = run("3")
+    assert not ref[68:71].any()
+    got = run("30")
+    assert np.array_equal(got, ref)
+    os.environ["VOSDET_RA_CHUNK"] = "16"  # every tile split into many items
+    try:
+        assert np.array_equal(run("30"), ref)
+    finally:
+        del os.environ["VOSDET_RA_CHUNK"]
+    sel = (rois[:, 0] == 0) & (np.arange(len(rois)) < 68)
+    d = orc.distribute(rois[sel].copy())
+    feats = [p[0:1].permute(0, 3, 1, 2).cpu().numpy() for p in pyr]
+    oref = orc.roi_feature_transform(feats[::-1], d, "rois", P, scales[::-1], 2)
+    assert np.array_equal(got[sel].transpose(0, 3, 1, 2), oref)
+
+
+def test_roi_align_tiled_shapes():
+    """Variant 30 on other shapes: C = 64 / 96 (fewer slices), one level, B = 1,
+    a single RoI, and a shape it does not serve (C % 32 != 0 -> the register-gather
+    kernel), all against the reference-order kernel."""
+    import os
+    from vosdetectron_amd import ops
+    rng = np.random.default_rng(21)
+    for C, sizes, n in ((64, [(50, 84), (25, 42)], 90), (96, [(37, 61)], 1),
+                        (256, [(13, 21)], 40), (40, [(25, 42), (13, 21)], 30)):
+        L = len(sizes)
+        feats = _pyramid(rng, 1, C, sizes)
+        nhwc = [torch.from_numpy(x).to(DEV).permute(0, 2, 3, 1).contiguous() for x in feats]
+        scales = [1. / 2 ** (k + 2) for k in range(L)]
+        rois = make_rois(rng, n, 336, 200, batch=1)
+        lv = (orc.map_rois_to_fpn_levels(rois[:, 1:5], 2, 1 + L).astype(np.int32) - 2)
+        args = (nhwc, scales, torch.from_numpy(rois).to(DEV), torch.from_numpy(lv).to(DEV), 7, 2)
+        outs = {}
+        for v in ("3", "30"):
+            os.environ["VOSDET_ROIALIGN_VARIANT"] = v
+            try:
+                outs[v] = ops.roi_align_fpn(*args, out_layout="nhwc").cpu().numpy()
+            finally:
+                del os.environ["VOSDET_ROIALIGN_VARIANT"]
+        if C % 32 == 0:
+            assert np.array_equal(outs["30"], outs["3"]), C
+        else:
+            np.testing.assert_allclose(outs["30"], outs["3"], rtol=1e-4, atol=1e-4)

@@ -47,6 +47,10 @@ SIGNATURES = {
     "vd_roi_align_backward": (_I, [_I, _I, _F, _I, _P, _I, _I, _I, _I, _P, _I, _I, _P, _P]),
     "vd_roi_align_fpn_forward": (_I, [ctypes.POINTER(VdFeatLevel), _I, _I, _I, _I, _P, _P, _P,
                                       _I, _I, _I, _I, _I, _P, _P]),
+    "vd_roi_align_fpn_tiled_workspace_size": (_S, [ctypes.POINTER(VdFeatLevel), _I, _I, _I, _I,
+                                                   _I]),
+    "vd_roi_align_fpn_tiled_forward": (_I, [ctypes.POINTER(VdFeatLevel), _I, _I, _I, _P, _P, _I,
+                                            _I, _I, _P, _P, _S, _P]),
     "vd_gemm_workspace_size": (_S, []),
     "vd_gemm_bias_act": (_I, [_P, _I, _I, _P, _I, _P, _P, _I, _P, _P, _S, _P]),
     "vd_gemm_dual_bias_act": (_I, [_P, _I, _P, _I, _I, _P, _I, _P, _I, _P, _P]),

@@ -90,6 +90,30 @@ int vd_roi_align_fpn_forward(const VdFeatLevel *levels, int num_levels, int B, i
                                      fa.scale[0], sampling_ratio, output, VD_STREAM(stream));
 }
 
+size_t vd_roi_align_fpn_tiled_workspace_size(const VdFeatLevel *levels, int num_levels, int B,
+                                             int C, int num_rois, int aligned_size) {
+    FpnLevels fa;
+    if (aligned_size < 1 || fpn_levels(levels, num_levels, B, C, num_rois, fa) != VD_OK) return 0;
+    return roi_align_tiled_workspace_bytes(fa, num_rois, aligned_size, C);
+}
+
+int vd_roi_align_fpn_tiled_forward(const VdFeatLevel *levels, int num_levels, int B, int C,
+                                   const float *rois, const int32_t *roi_level, int num_rois,
+                                   int aligned_size, int sampling_ratio, float *output,
+                                   void *workspace, size_t workspace_bytes, void *stream) {
+    if (num_rois == 0) return VD_OK;
+    if (!rois || !output || aligned_size < 1) return VD_ERR_ARG;
+    if (num_levels > 1 && !roi_level) return VD_ERR_ARG;
+    FpnLevels fa;
+    const int st = fpn_levels(levels, num_levels, B, C, num_rois, fa);
+    if (st != VD_OK) return st;
+    if (B > 64 || !roi_align_tiled_supported(fa, C, aligned_size, sampling_ratio))
+        return VD_ERR_SHAPE;
+    return launch_roi_align_fpn_tiled(fa, C, rois, roi_level, num_rois, aligned_size,
+                                      sampling_ratio, output, workspace, workspace_bytes,
+                                      VD_STREAM(stream));
+}
+
 size_t vd_gemm_workspace_size(void) { return gemm_epi_workspace_bytes(); }
 
 int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,

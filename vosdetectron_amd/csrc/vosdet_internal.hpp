@@ -31,6 +31,12 @@ int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, con
 int launch_roi_align_fpn_lds(const FpnLevels &fa, int C, const float *rois, const int *lvl,
                              const int *order, int R, int P, int sr, float *out, hipStream_t s);
 
+bool roi_align_tiled_supported(const FpnLevels &fa, int C, int P, int sr);
+size_t roi_align_tiled_workspace_bytes(const FpnLevels &fa, int R, int P, int C);
+int launch_roi_align_fpn_tiled(const FpnLevels &fa, int C, const float *rois, const int *lvl,
+                               int R, int P, int sr, float *out, void *ws, size_t ws_bytes,
+                               hipStream_t s);
+
 size_t gemm_epi_workspace_bytes();
 int launch_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,
                          const float *R, int relu, float *D, void *ws, size_t ws_bytes,

@@ -170,6 +170,20 @@ def roi_align_fpn(levels: Sequence[torch.Tensor], spatial_scales: Sequence[float
         raise ValueError("roi_order must have R = %d entries" % R)
     lv = _need(roi_level, "roi_level", torch.int32) if roi_level is not None else None
     od = _need(roi_order, "roi_order", torch.int32) if roi_order is not None else None
+    if nhwc and onhwc and int(sampling_ratio) == 2 and roi_align_variant() == "30" \
+            and (len(levels) == 1 or lv is not None):
+        # tile-binned LDS-staged kernel (csrc/roi_align_tile.hip): bit-identical to the
+        # reference's per-sample arithmetic; roi_order does not apply (tiles set the order)
+        L = len(levels)
+        nws = lib().vd_roi_align_fpn_tiled_workspace_size(descs, L, B, C, R, resolution)
+        if nws:
+            ws = torch.empty((nws,), dtype=torch.uint8, device=r.device)
+            st = lib().vd_roi_align_fpn_tiled_forward(
+                descs, L, B, C, r.data_ptr(), lv.data_ptr() if lv is not None else None, R,
+                resolution, 2, out.data_ptr(), ws.data_ptr(), nws, _stream())
+            if st != _lib.VD_ERR_SHAPE:
+                check(st, "vd_roi_align_fpn_tiled_forward")
+                return out
     check(lib().vd_roi_align_fpn_forward(
         descs, len(levels), B, C, _lib.VD_LAYOUT_NHWC if nhwc else _lib.VD_LAYOUT_NCHW,
         r.data_ptr(), lv.data_ptr() if lv is not None else None,
@@ -180,6 +194,15 @@ def roi_align_fpn(levels: Sequence[torch.Tensor], spatial_scales: Sequence[float
 
 
 _ORDER_CACHE = {}
+
+# FPN RoIAlign kernel for NHWC in/out (VOSDET_ROIALIGN_VARIANT overrides):
+# "30" tile-binned LDS-staged (roi_align_tile.hip), "10" register-gather separable
+# (roi_align.hip), "20" per-RoI LDS windows (roi_align_lds.hip), "3" reference-order rows.
+ROI_ALIGN_DEFAULT_VARIANT = "10"
+
+
+def roi_align_variant() -> str:
+    return os.environ.get("VOSDET_ROIALIGN_VARIANT", ROI_ALIGN_DEFAULT_VARIANT)
 
 
 def _spread16(v: torch.Tensor) -> torch.Tensor:
