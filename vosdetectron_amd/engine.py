@@ -313,11 +313,13 @@ class VOSPipeline(FramePipeline):
         return self.model.temporal_fusion(feats, self._flow)
 
     @torch.no_grad()
-    def run(self, frames: torch.Tensor, flow: torch.Tensor = None, keep_intermediates=False):
+    def run(self, frames: torch.Tensor, flow: torch.Tensor = None, keep_intermediates=False,
+            sync: bool = True):
         """frames: F x H x W x 3 u8 (frame t of each sequence); flow: optional
-        F x 2 x Hp x Wp optical flow at blob resolution (flo_to_blob, data_flow)."""
+        F x 2 x Hp x Wp optical flow at blob resolution (flo_to_blob, data_flow);
+        sync as FramePipeline.run (False: complete() reads the counts later)."""
         self._flow = flow
         try:
-            return super().run(frames, keep_intermediates)
+            return super().run(frames, keep_intermediates, sync=sync)
         finally:
             self._flow = None

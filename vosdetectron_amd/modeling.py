@@ -61,6 +61,15 @@ def _conv_epi(conv: nn.Conv2d, x, relu=True, res=None, res_bias=None, up=False):
 
 _CONV3X3_MIN_PIXELS = 1 << 18  # below this CK's kernels fill the chip better
 _WINO_MIN_PIXELS = 1 << 16
+# Winograd workgroups cover 8 x 16 output pixels of one image (maps <= 16 wide) or
+# 4 x 32: on the C4 head's 7 x 7 RoI maps only 49 / 128 of a block is real work,
+# which loses to the implicit GEMM (pixels packed across images): 69 -> 60 frames/s
+_WINO_MIN_BLOCK_USE = 0.6
+
+
+def _wino_block_use(H: int, W: int) -> float:
+    br, bc = (8, 16) if W <= 16 else (4, 32)
+    return H * W / float(-(-H // br) * br * -(-W // bc) * bc)
 
 
 def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False):
@@ -80,7 +89,8 @@ def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False):
     w = conv.weight
     key = (w.data_ptr(), w._version)
     b = conv.bias.detach() if (bias and conv.bias is not None) else None
-    if os.environ.get("VOSDET_CONV3X3_ALGO", CONV3X3_ALGO) == "wino" and npx >= _WINO_MIN_PIXELS:
+    if (os.environ.get("VOSDET_CONV3X3_ALGO", CONV3X3_ALGO) == "wino" and npx >= _WINO_MIN_PIXELS
+            and _wino_block_use(x.shape[2], x.shape[3]) >= _WINO_MIN_BLOCK_USE):
         if getattr(conv, "_vd_u_key", None) != key:
             conv._vd_u = ops.conv3x3_wino_weight(w.detach())
             conv._vd_u_key = key
