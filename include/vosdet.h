@@ -165,6 +165,14 @@ int vd_conv3x3_wino_weight(const float *w, int Cout, int Cin, float *U, void *st
 int vd_conv3x3_wino_bias_act(const float *X, int N, int H, int W, int C, const float *U,
                              int Cout, const float *bias, int relu, float *Y, void *stream);
 
+/* The same convolution by Winograd F(4x4, 3x3) (4x fewer multiplies than the
+ * direct form; transforms with factors up to 8, ~4x F(2x2, 3x3)'s rounding error,
+ * ~4e-6 of max|y| at 256 channels): U from vd_conv3x3_wino4_weight (36 x Cout x
+ * Cin fp32, opaque chunk-blocked order).  Cin % 4 == 0, Cout % 32 == 0. */
+int vd_conv3x3_wino4_weight(const float *w, int Cout, int Cin, float *U, void *stream);
+int vd_conv3x3_wino4_bias_act(const float *X, int N, int H, int W, int C, const float *U,
+                              int Cout, const float *bias, int relu, float *Y, void *stream);
+
 /* Two 1x1 convolutions of two channels_last inputs summed, with the epilogue:
  * D[M][N] = act(A1[M][K1] . W[:, :K1]^T + A2[M][K2] . W[:, K1:]^T + bias[N]),
  * W = [W1 | W2] as N x (K1 + K2) row-major.  With A1 = the bottleneck's conv2

@@ -82,3 +82,30 @@ def test_conv3x3_wino_vs_torch(N, C, H, W, Cout, relu):
         assert got.is_contiguous(memory_format=torch.channels_last)
         err = float((got - ref).abs().max())
         assert err <= 2e-5 * max(1., float(ref.abs().max())), err
+
+
+@pytest.mark.parametrize("N,C,H,W,Cout", [(2, 64, 9, 13, 128), (1, 256, 14, 14, 256),
+                                          (3, 128, 1, 1, 32), (1, 256, 25, 42, 256),
+                                          (5, 256, 7, 7, 64), (2, 64, 30, 41, 64),
+                                          (1, 4, 5, 3, 32), (1, 256, 17, 70, 192),
+                                          (2, 512, 33, 65, 96), (1, 12, 50, 84, 64)])
+@pytest.mark.parametrize("relu", [False, True])
+def test_conv3x3_wino4_vs_torch(N, C, H, W, Cout, relu):
+    """Winograd F(4x4,3x3) MFMA kernel (csrc/conv3x3_wino4.hip) vs a plain torch
+    fp32 conv2d(pad 1) + bias (+ ReLU): partial tiles and 16 x 32 blocks on every
+    edge, a 1x1 image, Cin 4..512, Cout 32..256.  Tolerance as the other conv
+    kernels (2e-5 of max|y|); F(4x4,3x3) rounds ~4x coarser than F(2x2,3x3)."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(11 * N + C + H + W + Cout)
+    x = torch.randn(N, C, H, W, generator=g).cuda().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** .5).cuda()
+    b = torch.randn(Cout, generator=g).cuda()
+    for bias in (b, None):
+        ref = F.conv2d(x, w, bias, padding=1)
+        if relu:
+            ref = F.relu(ref)
+        got = ops.conv3x3_wino4_bias_act(x, ops.conv3x3_wino4_weight(w), bias, relu=relu)
+        torch.cuda.synchronize()
+        assert got.is_contiguous(memory_format=torch.channels_last)
+        err = float((got - ref).abs().max())
+        assert err <= 2e-5 * max(1., float(ref.abs().max())), err
