@@ -62,13 +62,20 @@ def _worker(rank, world, port, outq):
         stale_raises = False
     except RuntimeError:
         stale_raises = True
-    # more masks than mask rows raises (never truncates)
-    try:
-        g.gather_async(torch.from_numpy(dets), torch.from_numpy(cls), torch.from_numpy(counts),
-                       torch.zeros((49, 28, 28)))
-        overflow_raises = False
-    except RuntimeError:
-        overflow_raises = True
+    # more masks than the packet's mask rows: nothing is truncated -- finish()
+    # ships the rows past mask_rows in a second gather, on every rank alike
+    small = ResultGatherer(3, 16, 28, world, "cpu", mask_rows=20)
+    fin = small.gather_async(torch.from_numpy(dets), torch.from_numpy(cls),
+                             torch.from_numpy(counts), torch.from_numpy(masks)).finish()
+    over_frames = [frame_masks(fin, 3, i).numpy().copy() for i in range(world * 3)]
+    overflow_raises = all(np.array_equal(a, b) for a, b in zip(over_frames, per_frame)) \
+        and "masks_extra" in fin
+    # only rank 1 overflows (29 and 32 rows vs 30): rank 0 sends zero padding
+    one = ResultGatherer(3, 16, 28, world, "cpu", mask_rows=30)
+    fin1 = one.gather_async(torch.from_numpy(dets), torch.from_numpy(cls),
+                            torch.from_numpy(counts), torch.from_numpy(masks)).finish()
+    overflow_raises &= fin1["masks_extra"].shape[1] == 2 and all(
+        np.array_equal(frame_masks(fin1, 3, i).numpy(), per_frame[i]) for i in range(world * 3))
     if rank == 0:
         got = {k: v.numpy().copy() for k, v in out.items()}
         got["per_frame"] = per_frame
@@ -130,3 +137,24 @@ def test_bench_launch_world2_dry_run():
                          "--dry-run"], capture_output=True, text=True, timeout=120, env=env2,
                         cwd=root)
     assert p2.returncode != 0 and "formed a world of 1" in p2.stderr
+
+
+def test_gather_overflow_single_process():
+    """Without a process group the gatherer's send slot is the result; rows past
+    mask_rows come back through finish() (no collective), and frame_masks raises
+    when a caller skips finish()."""
+    from vosdetectron_amd.runner import ResultGatherer, frame_masks
+    dets, cls, counts, masks = _rank_outputs(1)  # counts [5, 16, 11]
+    g = ResultGatherer(3, 16, 28, 1, "cpu", mask_rows=10)
+    t = [torch.from_numpy(a) for a in (dets, cls, counts, masks)]
+    v = g.gather_async(*t).wait(clone=True)
+    with pytest.raises(RuntimeError):
+        frame_masks(v, 3, 1)
+    fin = g.gather_async(*t).finish()
+    o = 0
+    for f in range(3):
+        assert np.array_equal(frame_masks(fin, 3, f).numpy(), masks[o:o + counts[f]])
+        o += counts[f]
+    # the engine path: the packet had only mask_rows rows, complete() added the rest
+    fin2 = g.gather_async(t[0], t[1], t[2], t[3][:10]).finish(masks_full=t[3])
+    assert torch.equal(fin2["masks_extra"][0], t[3][10:])

@@ -38,8 +38,9 @@ class PendingGather:
     earlier `wait()` are NOT guarded -- they alias the buffer and show the
     later step's rows once it is reused."""
 
-    def __init__(self, work, gatherer, rbuf, slot, gen):
+    def __init__(self, work, gatherer, rbuf, slot, gen, over=None):
         self.work, self.g, self.rbuf, self.slot, self.gen = work, gatherer, rbuf, slot, gen
+        self.over = over  # this rank's mask rows past mask_rows (not in the packet)
 
     def wait(self, views: bool = True, clone: bool = False) -> Dict[str, torch.Tensor]:
         """Orders the caller's stream after the collective; returns the gathered
@@ -54,6 +55,46 @@ class PendingGather:
                                "gather_async; wait(clone=True) keeps a private copy" % self.slot)
         v = self.g._views(self.rbuf)
         return {k: t.clone() for k, t in v.items()} if clone else v
+
+    def finish(self, masks_full: Optional[torch.Tensor] = None, clone: bool = False
+               ) -> Dict[str, torch.Tensor]:
+        """wait() plus the mask rows past the packet's mask_rows, on every rank.
+        Collective: call it on all ranks for the same step.  After the packet
+        lands every rank reads the gathered counts (one small D2H) and so takes
+        the same decision: when some rank has M > mask_rows (detections tied at
+        DETECTIONS_PER_IM, or the engine's complete() adding rows after the packet
+        was sent), ONE more all_gather ships each rank's extra rows, zero-padded to
+        the largest overflow, as views["masks_extra"] [W, max_overflow, R, R];
+        frame_masks reads them.  masks_full: this rank's complete M-row masks
+        (after FramePipeline.complete); default: the rows gather_async could not
+        pack."""
+        v = self.wait(clone=clone)
+        g = self.g
+        if not g.with_masks:
+            return v
+        W = v["counts"].shape[0] // g.F
+        M = v["counts"].view(W, g.F).to(torch.int64).sum(1).cpu().tolist()
+        over = [max(0, m - g.mask_rows) for m in M]
+        mo = max(over, default=0)
+        if mo == 0:
+            return v
+        rank = dist.get_rank() if g.collective else 0
+        mine = masks_full[g.mask_rows:M[rank]] if masks_full is not None else self.over
+        if over[rank] and (mine is None or mine.shape[0] != over[rank]):
+            raise RuntimeError("rank %d has %d mask rows past the packet, %s given"
+                               % (rank, over[rank], None if mine is None else mine.shape[0]))
+        dev = g.send[0].device
+        send = torch.zeros((mo, g.R, g.R), dtype=torch.float32, device=dev)
+        if over[rank]:
+            send[:over[rank]].copy_(mine.reshape(-1, g.R, g.R))
+        if g.collective:
+            recv = torch.empty((W, mo, g.R, g.R), dtype=torch.float32, device=dev)
+            dist.all_gather_into_tensor(recv.view(-1), send.view(-1))
+        else:
+            recv = send.view(1, mo, g.R, g.R)
+        v = dict(v)
+        v["masks_extra"] = recv
+        return v
 
 
 class ResultGatherer:
@@ -74,7 +115,9 @@ class ResultGatherer:
     With F = 16 that is 5.0 MB per rank per step (vs 12.8 MB for masks padded to
     the engine's det_cap of 256 rows per frame), still exact fp32 -- the
     reference's segm_results resizes the probabilities before thresholding, so a
-    pre-binarised mask would change its output.
+    pre-binarised mask would change its output.  Rows past mask_rows are not
+    dropped: PendingGather.finish() ships them in a second all_gather, only on
+    steps where some rank has them.
 
     Two buffer slots alternate, so `gather_async` of step t can run on RCCL's
     stream while step t+1 computes; the caller keeps at most one gather in
@@ -110,13 +153,9 @@ class ResultGatherer:
         buf[self.o_cls:self.o_cnt].view(torch.int32).copy_(classes.reshape(-1))
         buf[self.o_cnt:self.o_msk].view(torch.int32).copy_(counts.reshape(-1))
         if self.with_masks:
-            M = masks.shape[0]
-            if M > self.mask_rows:
-                raise RuntimeError("%d masks in one step exceed the gather's %d mask rows "
-                                   "(build ResultGatherer with a larger mask_rows)"
-                                   % (M, self.mask_rows))
+            M = min(masks.shape[0], self.mask_rows)  # the rest: PendingGather.finish
             if M:
-                buf[self.o_msk:self.o_msk + M * self.R * self.R].copy_(masks.reshape(-1))
+                buf[self.o_msk:self.o_msk + M * self.R * self.R].copy_(masks[:M].reshape(-1))
 
     def _views(self, rb):
         W, F, D, R = rb.shape[0], self.F, self.D, self.R
@@ -147,10 +186,12 @@ class ResultGatherer:
         self.slot ^= 1
         self.gen[s] += 1
         self._pack(self.send[s], dets, classes, counts, masks)
+        over = masks[self.mask_rows:] if self.with_masks and masks.shape[0] > self.mask_rows \
+            else None
         if not self.collective:
-            return PendingGather(None, self, self.send[s].view(1, -1), s, self.gen[s])
+            return PendingGather(None, self, self.send[s].view(1, -1), s, self.gen[s], over)
         work = dist.all_gather_into_tensor(self.recv[s].view(-1), self.send[s], async_op=True)
-        return PendingGather(work, self, self.recv[s], s, self.gen[s])
+        return PendingGather(work, self, self.recv[s], s, self.gen[s], over)
 
     def gather(self, dets, classes, counts, masks, counts_host=None) -> Dict[str, torch.Tensor]:
         return self.gather_async(dets, classes, counts, masks).wait()
@@ -158,16 +199,21 @@ class ResultGatherer:
 
 def frame_masks(views: Dict[str, torch.Tensor], frames_per_rank: int, frame: int
                 ) -> torch.Tensor:
-    """The gathered masks of global frame index `frame` (rank-major order).
-    Raises if the frame's rows lie past the gathered mask rows (a step with more
-    detections than the engine's padded mask batch, FramePipeline.complete)."""
+    """The gathered masks of global frame index `frame` (rank-major order); rows
+    past the packet's mask rows come from views["masks_extra"]
+    (PendingGather.finish), and raise if the views lack them."""
     r, f = divmod(frame, frames_per_rank)
     o = int(views["mask_offsets"][r, f])
     k = int(views["counts"][frame])
-    if o + k > views["masks"].shape[1]:
-        raise RuntimeError("frame %d's masks (rows %d..%d) exceed the %d gathered mask rows"
-                           % (frame, o, o + k, views["masks"].shape[1]))
-    return views["masks"][r, o:o + k]
+    cap = views["masks"].shape[1]
+    if o + k <= cap:
+        return views["masks"][r, o:o + k]
+    extra = views.get("masks_extra")
+    if extra is None or o + k - cap > extra.shape[1]:
+        raise RuntimeError("frame %d's masks (rows %d..%d) exceed the %d gathered mask rows "
+                           "(PendingGather.finish ships the rest)" % (frame, o, o + k, cap))
+    head = views["masks"][r, o:cap] if o < cap else views["masks"][r, :0]
+    return torch.cat([head, extra[r, max(0, o - cap):o + k - cap]])
 
 
 class FrameUploader:
