@@ -98,7 +98,8 @@ __device__ __forceinline__ void wino_wait_barrier() {
 template <bool RELU, int TC, int PR = 0>
 __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
-    int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx) {
+    int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
+    int cb_per_xcd) {
     using PG = Patch2<TC>;
     __shared__ __attribute__((aligned(16))) float sm[2 * k2StageB / 4];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -107,9 +108,16 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     // the Cout / 64 channel blocks of one spatial block run on one XCD (blocks
     // b, b + 8, ...): its input patches come from one L2
     const int ncb = Cout / kCo;
-    const int r8 = blockIdx.x % (8 * ncb);
-    const int cb = r8 / 8;
-    const int sp = (blockIdx.x / (8 * ncb)) * 8 + (r8 & 7);
+    int cb, sp;
+    if (cb_per_xcd) {  // XCD x computes channel block x % ncb: its L2 holds one U block
+        const int xcd = blockIdx.x & 7;
+        cb = xcd % ncb;
+        sp = (blockIdx.x >> 3) * (8 / ncb) + xcd / ncb;
+    } else {
+        const int r8 = blockIdx.x % (8 * ncb);
+        cb = r8 / 8;
+        sp = (blockIdx.x / (8 * ncb)) * 8 + (r8 & 7);
+    }
     if (sp >= N * tby * tbx) return;
     const int n = sp / (tby * tbx);
     const int rem = sp - n * tby * tbx;
@@ -323,7 +331,11 @@ int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float 
     const int tby = sq ? (H + 7) / 8 : (H + 3) / 4;
     const int tbx = sq ? (W + 15) / 16 : (W + 31) / 32;
     const int64_t nsp = (int64_t)N * tby * tbx;
-    const int64_t blocks = (nsp + 7) / 8 * 8 * (Cout / kCo);
+    const int ncb = Cout / kCo;
+    const char *em = getenv("VOSDET_WINO_MAP");  // 1: channel block per XCD
+    const int cbx = em && atoi(em) == 1 && 8 % ncb == 0;
+    const int64_t blocks = cbx ? (nsp + 8 / ncb - 1) / (8 / ncb) * 8
+                               : (nsp + 7) / 8 * 8 * ncb;
     if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
     auto kern = sq ? (relu ? conv3x3_wino2_kernel<true, 8> : conv3x3_wino2_kernel<false, 8>)
                    : (relu ? conv3x3_wino2_kernel<true, 16> : conv3x3_wino2_kernel<false, 16>);
@@ -340,7 +352,7 @@ int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float 
         default: break;
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(k2Threads), 0, s, X, N, H, W, C, U, Cout,
-                       bias, Y, tby, tbx);
+                       bias, Y, tby, tbx, cbx);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
