@@ -320,6 +320,48 @@ def measure_hbm_copy(dev, nbytes=2 << 30, iters=20):
 MFMA_FP32_PEAK_TFS = 157.3  # MI355X dense fp32 matrix peak
 
 
+def measure_dominant_conv(dev, F, H, W, C=256, iters=None):
+    """The step's dominant kernel by time: the P2 3x3 256 -> 256 convolution (FPN
+    posthoc and RPN conv, Winograd F(2x2,3x3) on the MFMA pipes), timed alone at
+    the benched shape with HIP events on its stream.  Algorithmic FLOPs are the
+    direct convolution's 2*9*C*Cout per output pixel (what the reference computes;
+    Winograd can take the rate past the peak), executed FLOPs the 16 MFMA
+    positions per 2x2 tile actually run (4/9 of them)."""
+    from vosdetectron_amd import ops
+    iters = iters or int(os.environ.get("CONV_ITERS", "10"))
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn((F, C, H, W), generator=g, device=dev).contiguous(
+        memory_format=torch.channels_last)
+    w = torch.randn((C, C, 3, 3), generator=g, device=dev) / (9 * C) ** .5
+    b = torch.randn((C,), generator=g, device=dev)
+    u = ops.conv3x3_wino_weight(w)
+    y = ops.conv3x3_wino_bias_act(x, u, b)
+    if y is None:
+        return None
+    for _ in range(2):
+        ops.conv3x3_wino_bias_act(x, u, b, out=y)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        ops.conv3x3_wino_bias_act(x, u, b, out=y)
+    e1.record(s)
+    e1.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / iters
+    alg = 2.0 * F * H * W * C * C * 9
+    exe = alg * 4 / 9
+    del x, y, u
+    return {"kernel": "vd::conv3x3_wino2_kernel (Winograd F(2x2,3x3), v_mfma_f32_16x16x4_f32)",
+            "bound": "mfma", "shape": [F, C, H, W, C], "avg_launch_us": round(t * 1e6, 1),
+            "unit": "TFLOP/s", "peak": MFMA_FP32_PEAK_TFS,
+            "achieved_algorithmic": round(alg / t / 1e12, 1),
+            "frac_algorithmic": round(alg / t / 1e12 / MFMA_FP32_PEAK_TFS, 4),
+            "achieved_executed": round(exe / t / 1e12, 1),
+            "frac_executed": round(exe / t / 1e12 / MFMA_FP32_PEAK_TFS, 4),
+            "how": "HIP events over %d launches; algorithmic = direct-conv FLOPs, executed = "
+                   "the MFMA work Winograd runs (4/9)" % iters}
+
+
 def step_roofline(flops_frame, dets_cpu, frames, ms_per_step, engine_launch, frame_hw, blob_hw,
                   wino_flops_frame=0):
     """the FPS as a fraction of the roofline = sum of per-stage
@@ -759,6 +801,9 @@ def main():
             roof["engine_launch"] = measure_pipeline_roialign(pipe, any_frames)
     if not args.no_roofline and rank == 0 and world == 1:  # N=1 line only (no ranks waiting)
         extra["hbm_copy"] = measure_hbm_copy(dev)
+        if not vos and cfg.FPN.FPN_ON:
+            extra["dominant_kernel"] = measure_dominant_conv(
+                dev, F, getattr(pipe, "Hp", fh) // 4, getattr(pipe, "Wp", fw) // 4)
         nthr = torch.get_num_threads()
         torch.set_num_threads(cpu_share()[0])
         flops, dets_cpu, wino_flops = frame_flops(sd, cfg)
