@@ -56,3 +56,16 @@ def test_roi_align_algorithmic_bytes_counts_union_once():
 def test_cpu_share_is_positive():
     n, caps = bench.cpu_share()
     assert n >= 1 and "affinity" in caps
+
+
+def test_winograd_block_occupancy_gate():
+    """modeling._conv3x3_mfma sends a 3x3 conv to Winograd only where its pixel
+    blocks (8 x 16 for maps <= 16 wide, else 4 x 32) are >= 60 % real work: the C4
+    head's 7 x 7 RoI maps (38 %) stay on the implicit GEMM, the mask head's 14 x 14
+    maps (77 %) and the FPN levels go to Winograd."""
+    from vosdetectron_amd.modeling import _WINO_MIN_BLOCK_USE, _wino_block_use
+    assert _wino_block_use(7, 7) < _WINO_MIN_BLOCK_USE
+    for hw in [(14, 14), (200, 336), (100, 168), (50, 84), (120, 214), (60, 107)]:
+        assert _wino_block_use(*hw) >= _WINO_MIN_BLOCK_USE, hw
+    assert abs(_wino_block_use(14, 14) - 196 / 256) < 1e-12
+    assert _wino_block_use(8, 32) == 1.0
