@@ -332,8 +332,12 @@ int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float 
     const int tbx = sq ? (W + 15) / 16 : (W + 31) / 32;
     const int64_t nsp = (int64_t)N * tby * tbx;
     const int ncb = Cout / kCo;
-    const char *em = getenv("VOSDET_WINO_MAP");  // 1: channel block per XCD
-    const int cbx = em && atoi(em) == 1 && 8 % ncb == 0;
+    // XCD x computes channel block x % ncb (its L2 keeps one U block instead of
+    // all of them): bit-identical, P3 1.66 -> 1.51 ms, P2 / mask head 1-3 %
+    // (profiles/r03/wino_map_probe.json); VOSDET_WINO_MAP=0 restores the
+    // channel-blocks-of-a-spatial-block-on-one-XCD order
+    const char *em = getenv("VOSDET_WINO_MAP");
+    const int cbx = (!em || atoi(em) != 0) && 8 % ncb == 0;
     const int64_t blocks = cbx ? (nsp + 8 / ncb - 1) / (8 / ncb) * 8
                                : (nsp + 7) / 8 * 8 * ncb;
     if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
