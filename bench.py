@@ -852,7 +852,7 @@ def main():
             line["stages_ms"] = stages
         line.update(extra)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if world > 1 or args.rccl_gather:
         dist.destroy_process_group()
     return 0
 
