@@ -6,7 +6,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/${TAG:-r03e}; mkdir -p $O
-export MIOPEN_USER_DB_PATH=/tmp/vd_miopen_db; mkdir -p $MIOPEN_USER_DB_PATH
+# MIOpen reads the in-tree find-db (vosdetectron_amd/miopen_db, set by the package)
 for part in ${PART:-roof}; do
 case $part in
 roof)
