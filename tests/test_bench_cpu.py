@@ -69,3 +69,5 @@ def test_winograd_block_occupancy_gate():
         assert _wino_block_use(*hw) >= _WINO_MIN_BLOCK_USE, hw
     assert abs(_wino_block_use(14, 14) - 196 / 256) < 1e-12
     assert _wino_block_use(8, 32) == 1.0
+    # res5 / P5 25 x 42 maps: the 8 x 16 blocks (68 %) beat 4 x 32 (59 %)
+    assert abs(_wino_block_use(25, 42) - 25 * 42 / (32 * 48)) < 1e-12

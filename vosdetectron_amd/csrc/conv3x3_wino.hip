@@ -327,7 +327,13 @@ int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float 
                         const float *bias, int relu, float *Y, hipStream_t s) {
     if ((int64_t)N * H * W == 0) return VD_OK;
     if (!conv3x3_wino_supported(C, Cout)) return VD_ERR_SHAPE;
-    const bool sq = W <= 16;  // 8 x 16-pixel blocks, else 4 x 32
+    // block shape: 8 x 16 or 4 x 32 output pixels, whichever wastes less of the map
+    // (measured, profiles/r03/wino_small_probe.json: 8 x 16 wins on res5 / P5
+    // 25 x 42 maps and at P3, 4 x 32 at P4); VOSDET_WINO_SQ=1/0 forces one
+    const double use_sq = (double)H * W / ((double)((H + 7) / 8 * 8) * ((W + 15) / 16 * 16));
+    const double use_wide = (double)H * W / ((double)((H + 3) / 4 * 4) * ((W + 31) / 32 * 32));
+    const char *esq = getenv("VOSDET_WINO_SQ");
+    const bool sq = esq ? atoi(esq) == 1 : use_sq > use_wide;
     const int tby = sq ? (H + 7) / 8 : (H + 3) / 4;
     const int tbx = sq ? (W + 15) / 16 : (W + 31) / 32;
     const int64_t nsp = (int64_t)N * tby * tbx;

@@ -60,16 +60,18 @@ def _conv_epi(conv: nn.Conv2d, x, relu=True, res=None, res_bias=None, up=False):
 
 
 _CONV3X3_MIN_PIXELS = 1 << 18  # below this CK's kernels fill the chip better
-_WINO_MIN_PIXELS = 1 << 16
-# Winograd workgroups cover 8 x 16 output pixels of one image (maps <= 16 wide) or
-# 4 x 32: on the C4 head's 7 x 7 RoI maps only 49 / 128 of a block is real work,
-# which loses to the implicit GEMM (pixels packed across images): 69 -> 60 frames/s
+_WINO_MIN_PIXELS = 1 << 12  # res5 / P5 / P6 of a 16-frame batch included (beats MIOpen / CK)
+# Winograd workgroups cover 8 x 16 or 4 x 32 output pixels of one image (the kernel
+# takes the shape that wastes less): on the C4 head's 7 x 7 RoI maps only 49 / 128 of
+# a block is real work, which loses to the implicit GEMM (pixels packed across
+# images): 69 -> 60 frames/s
 _WINO_MIN_BLOCK_USE = 0.6
 
 
 def _wino_block_use(H: int, W: int) -> float:
-    br, bc = (8, 16) if W <= 16 else (4, 32)
-    return H * W / float(-(-H // br) * br * -(-W // bc) * bc)
+    """Fraction of the Winograd kernel's pixel blocks that is real output, for the
+    block shape it picks (csrc/conv3x3_wino.hip, launch_conv3x3_wino)."""
+    return max(H * W / float(-(-H // br) * br * -(-W // bc) * bc) for br, bc in ((8, 16), (4, 32)))
 
 
 def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False):
@@ -77,9 +79,8 @@ def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False):
     hand-written MFMA kernels with the bias (+ ReLU) epilogue, or None where
     they do not apply (other geometry, VOSDET_CONV3X3_MFMA=0).  Algorithm
     (VOSDET_CONV3X3_ALGO): 'wino' -- Winograd F(2x2,3x3), csrc/conv3x3_wino.hip,
-    from 2^16 output pixels -- else / below that the implicit GEMM
-    (csrc/conv3x3.hip) from 2^18 pixels (P4-P6 of a 16-frame batch stay on
-    MIOpen / CK).  The transformed weights are cached on the module."""
+    from 2^12 output pixels where its blocks are >= 60 % real output -- else the
+    implicit GEMM (csrc/conv3x3.hip) from 2^18 pixels, else MIOpen / CK.  The transformed weights are cached on the module."""
     if (os.environ.get("VOSDET_CONV3X3_MFMA", "1") == "0" or not x.is_cuda
             or conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1)
             or conv.dilation != (1, 1) or conv.groups != 1 or x.dtype != torch.float32
