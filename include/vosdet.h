@@ -165,6 +165,14 @@ int vd_conv3x3_wino_weight(const float *w, int Cout, int Cin, float *U, void *st
 int vd_conv3x3_wino_bias_act(const float *X, int N, int H, int W, int C, const float *U,
                              int Cout, const float *bias, int relu, float *Y, void *stream);
 
+/* The Winograd convolution of R images of seg_h x W pixels stored back to back
+ * (R x seg_h x W x C, i.e. one H = R * seg_h image), each padded by its own zeros:
+ * the mask head's RoI maps run as one mosaic, so the 8 x 16-pixel blocks are not
+ * split at every 14-row map.  seg_h even, H % seg_h == 0; bit-identical to
+ * vd_conv3x3_wino_bias_act on the R images. */
+int vd_conv3x3_wino_seg_bias_act(const float *X, int H, int W, int C, const float *U, int Cout,
+                                 const float *bias, int relu, int seg_h, float *Y, void *stream);
+
 /* The same convolution by Winograd F(4x4, 3x3) (4x fewer multiplies than the
  * direct form; transforms with factors up to 8, ~4x F(2x2, 3x3)'s rounding error,
  * ~4e-6 of max|y| at 256 channels): U from vd_conv3x3_wino4_weight (36 x Cout x

@@ -109,3 +109,26 @@ def test_conv3x3_wino4_vs_torch(N, C, H, W, Cout, relu):
         assert got.is_contiguous(memory_format=torch.channels_last)
         err = float((got - ref).abs().max())
         assert err <= 2e-5 * max(1., float(ref.abs().max())), err
+
+
+@pytest.mark.parametrize("N,C,H,W,Cout", [(37, 256, 14, 14, 256), (5, 64, 6, 20, 128),
+                                          (3, 8, 2, 9, 64), (9, 128, 14, 14, 64)])
+@pytest.mark.parametrize("relu", [False, True])
+def test_conv3x3_wino_mosaic_bit_exact(N, C, H, W, Cout, relu):
+    """The N maps as one (N * H)-row mosaic with per-map zero padding
+    (vd_conv3x3_wino_seg_bias_act, the mask head's route) give bit for bit the
+    per-map Winograd result, and stay within the conv tolerance of torch fp32."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(13 * N + C + H + W + Cout)
+    x = torch.randn(N, C, H, W, generator=g).cuda().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** .5).cuda()
+    b = torch.randn(Cout, generator=g).cuda()
+    u = ops.conv3x3_wino_weight(w)
+    per = ops.conv3x3_wino_bias_act(x, u, b, relu=relu)
+    mos = ops.conv3x3_wino_bias_act(x, u, b, relu=relu, mosaic=True)
+    torch.cuda.synchronize()
+    assert torch.equal(per, mos)
+    ref = F.conv2d(x, w, b, padding=1)
+    if relu:
+        ref = F.relu(ref)
+    assert float((mos - ref).abs().max()) <= 2e-5 * max(1., float(ref.abs().max()))

@@ -99,7 +99,7 @@ template <bool RELU, int TC, int PR = 0>
 __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
-    int cb_per_xcd) {
+    int cb_per_xcd, int seg_h) {
     using PG = Patch2<TC>;
     __shared__ __attribute__((aligned(16))) float sm[2 * k2StageB / 4];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -163,6 +163,13 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     // transform reads: lane (j, q) -> tile 16 tg + j, channels 2q, 2q + 1 (half
     // q >> 1, dwords 2 (q & 1) ..): byte offsets within a stage
     const int vt = tg * 16 + j, tr = vt / TC, tc = vt % TC;
+    // segmented rows (seg_h > 0: the image is a vertical mosaic of seg_h-row
+    // images, e.g. [R][14][14][C] as [1][14 R][14][C]): the patch row above / below
+    // a tile at a segment edge belongs to the neighbouring image and reads as the
+    // zero padding of its own (seg_h even: a 2x2 tile never straddles an edge)
+    const int toy = oy0 + 2 * tr;  // the tile's first output row
+    const bool zero_top = seg_h > 0 && toy % seg_h == 0;
+    const bool zero_bot = seg_h > 0 && (toy + 2) % seg_h == 0;
     int roff[4], coff[4];
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -197,6 +204,11 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
             for (int c = 0; c < 4; ++c)
                 d[a][c] = (PR & 2) ? f2v{(float)roff[a], (float)coff[c]}
                                    : *reinterpret_cast<const f2v *>(stb + roff[a] + coff[c]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (zero_top) d[0][c] = f2v{0.f, 0.f};
+            if (zero_bot) d[3][c] = f2v{0.f, 0.f};
+        }
         f2v b[16];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -324,9 +336,10 @@ int launch_conv3x3_wino_weight(const float *w, int Cout, int C, float *U, hipStr
 }
 
 int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float *U, int Cout,
-                        const float *bias, int relu, float *Y, hipStream_t s) {
+                        const float *bias, int relu, float *Y, hipStream_t s, int seg_h) {
     if ((int64_t)N * H * W == 0) return VD_OK;
     if (!conv3x3_wino_supported(C, Cout)) return VD_ERR_SHAPE;
+    if (seg_h < 0 || (seg_h > 0 && (seg_h % 2 || H % seg_h))) return VD_ERR_SHAPE;
     // block shape: 8 x 16 or 4 x 32 output pixels, whichever wastes less of the map
     // (measured, profiles/r03/wino_small_probe.json: 8 x 16 wins on res5 / P5
     // 25 x 42 maps and at P3, 4 x 32 at P4); VOSDET_WINO_SQ=1/0 forces one
@@ -362,7 +375,7 @@ int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float 
         default: break;
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(k2Threads), 0, s, X, N, H, W, C, U, Cout,
-                       bias, Y, tby, tbx, cbx);
+                       bias, Y, tby, tbx, cbx, seg_h);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 

@@ -596,10 +596,14 @@ def conv3x3_wino4_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torc
 
 
 def conv3x3_wino_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch.Tensor],
-                          relu: bool = False, out: Optional[torch.Tensor] = None):
+                          relu: bool = False, out: Optional[torch.Tensor] = None,
+                          mosaic: bool = False):
     """act(conv3x3(x, pad 1) + bias) on a channels_last fp32 tensor by Winograd
     F(2x2,3x3) on the MFMA pipes (vd_conv3x3_wino_bias_act); u from
-    conv3x3_wino_weight.  Returns None for a shape the kernel does not serve."""
+    conv3x3_wino_weight.  mosaic=True runs the N images as one N*H-row image with
+    per-image zero padding (vd_conv3x3_wino_seg_bias_act; H even): bit-identical,
+    fewer idle block rows on small maps.  Returns None for a shape the kernel
+    does not serve."""
     if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 4 \
             or not x.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("x must be a channels_last fp32 device tensor")
@@ -614,9 +618,14 @@ def conv3x3_wino_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch
     if out is None:
         out = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device,
                           memory_format=torch.channels_last)
-    st = lib().vd_conv3x3_wino_bias_act(x.data_ptr(), N, H, W, C, u_.data_ptr(), Cout,
-                                        b_.data_ptr() if b_ is not None else None, int(relu),
-                                        out.data_ptr(), _stream())
+    if mosaic and N > 0:
+        st = lib().vd_conv3x3_wino_seg_bias_act(x.data_ptr(), N * H, W, C, u_.data_ptr(), Cout,
+                                                b_.data_ptr() if b_ is not None else None,
+                                                int(relu), H, out.data_ptr(), _stream())
+    else:
+        st = lib().vd_conv3x3_wino_bias_act(x.data_ptr(), N, H, W, C, u_.data_ptr(), Cout,
+                                            b_.data_ptr() if b_ is not None else None,
+                                            int(relu), out.data_ptr(), _stream())
     if st == VD_ERR_SHAPE:
         return None
     check(st, "vd_conv3x3_wino_bias_act")
