@@ -93,12 +93,13 @@ def main():
     ops.conv3x3_bias_act = timed("conv3x3_mfma", cl, ck)
     wl = ops.conv3x3_wino_bias_act
 
-    def wk(y, x, u, bias, relu=False, out=None):
+    def wk(y, x, u, bias, relu=False, out=None, mosaic=False):
         if y is None:
             return 0.0, "conv3x3_wino (fell back)"
         N, C, H, W = x.shape
-        return 2.0 * N * H * W * y.shape[1] * C * 9, "conv3x3_wino x%s Cout%d%s" % (
-            list(x.shape), y.shape[1], " +bias" if bias is not None else "")
+        return 2.0 * N * H * W * y.shape[1] * C * 9, "conv3x3_wino x%s Cout%d%s%s" % (
+            list(x.shape), y.shape[1], " +bias" if bias is not None else "",
+            " mosaic" if mosaic else "")
     ops.conv3x3_wino_bias_act = timed("conv3x3_wino", wl, wk)
     dl = ops.gemm_dual_bias_act
 
