@@ -104,7 +104,8 @@ ROIALIGN_KERNEL = {"3": "vd::roi_align_fpn_nhwc_kernel<7,2,2> (reference order)"
 # rocprofv3 --pmc passes of this exact launch (tools/prof_roialign.sh, separate
 # passes per counter group; FETCH_SIZE doubled per the MI355X guide): L2<->fabric
 # bytes per launch, committed under profiles/ and reported as "traffic".
-ROIALIGN_PMC = {"8": "separable_v8_xcd.json", "10": "separable_buf_v10_xcd.json"}
+ROIALIGN_PMC = {"8": "r02_roialign_pmc/separable_v8_xcd.json",
+                "10": "r03/roialign_pmc/separable_buf_v10_xcd.json"}
 
 
 def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=None,
@@ -148,7 +149,7 @@ def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=Non
     t = e0.elapsed_time(e1) / 1e3 / iters
     achieved = nbytes / t / 1e9
     traffic, tsrc = None, None
-    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r02_roialign_pmc",
+    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                        ROIALIGN_PMC.get(variant, "-"))
     if use_order and out_layout == "nhwc" and (frames, R, C, P, sr) == (8, 1000, 256, 7, 2) \
             and os.path.exists(pmc):
