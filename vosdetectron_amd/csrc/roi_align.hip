@@ -369,10 +369,17 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_sep_kernel(
 // same occupancy and the union of their footprints stays closer to the 4 MiB
 // L2 (tools/research/ra_l2_sim.py); each run re-reads at most one boundary
 // column of its neighbour.
-template <int SR, bool NT>
+//
+// SIMPLE: the default launch (C <= 256, segs = parts = 1) -- wave w computes
+// output row w with no runtime divisions ahead of its first tap load.
+template <int SR, bool NT, bool SIMPLE>
 __global__ __launch_bounds__(1024) void roi_align_fpn_nhwc_sep_buf_kernel(
     FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
     const int *__restrict__ roi_order, int P, int segs, int parts, float *__restrict__ out) {
+    if (SIMPLE) {
+        segs = 1;
+        parts = 1;
+    }
     // parts > 1: a RoI's units are spread over `parts` consecutive workgroups of
     // the same XCD (block b runs on XCD b % 8): b -> schedule position p.
     const int b = blockIdx.x;
@@ -384,7 +391,7 @@ __global__ __launch_bounds__(1024) void roi_align_fpn_nhwc_sep_buf_kernel(
     int li = roi_level ? roi_level[r] : 0;
     li = __builtin_amdgcn_readfirstlane(li);
     const RoiGeom g = roi_geom(fa, C, rois + (int64_t)r * 5, li, P, P, SR);
-    const int chunks = (C + 255) / 256;
+    const int chunks = SIMPLE ? 1 : (C + 255) / 256;
     const int lane = lane_id();
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float *>(g.feat), (short)0, g.H * g.W * C * 4, 0x00020000);
@@ -392,10 +399,10 @@ __global__ __launch_bounds__(1024) void roi_align_fpn_nhwc_sep_buf_kernel(
     const int units = P * chunks * segs, per = (units + parts - 1) / parts;
     const int u1 = min(units, (part + 1) * per);
     for (int u = part * per + wave_id(); u < u1; u += num_waves()) {
-        const int ph = u / (chunks * segs);
-        const int rem = u - ph * chunks * segs;
-        const int ck = rem / segs;
-        const int sg = rem - ck * segs;
+        const int ph = SIMPLE ? u : u / (chunks * segs);
+        const int rem = SIMPLE ? 0 : u - ph * chunks * segs;
+        const int ck = SIMPLE ? 0 : rem / segs;
+        const int sg = SIMPLE ? 0 : rem - ck * segs;
         const int c0 = ck * 256 + lane * 4;
         const bool active = c0 < C;
         const int voff = (active ? c0 : 0) * 4;
@@ -415,7 +422,8 @@ __global__ __launch_bounds__(1024) void roi_align_fpn_nhwc_sep_buf_kernel(
                         float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, rowoff[k] + xo, 0));
             return combine_column<SR>(taps, c);
         };
-        sep_row_sweep<SR>(g, sg * P / segs, (sg + 1) * P / segs, column, [&](int pw, float4 acc) {
+        const int pw0 = SIMPLE ? 0 : sg * P / segs, pw1 = SIMPLE ? P : (sg + 1) * P / segs;
+        sep_row_sweep<SR>(g, pw0, pw1, column, [&](int pw, float4 acc) {
             if (active) store_bin<NT>(orow + (int64_t)pw * C, acc);
         });
     }
@@ -612,8 +620,12 @@ static int launch_sep_buf(const FpnLevels &fa, int C, const float *rois, const i
     if (waves > 16) waves = 16;
     if (segs == 1 && parts == 1 && waves > 8) waves = 8;
     const int nblk = parts == 1 ? R : (R + 7) / 8 * 8 * parts;
-    hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_buf_kernel<2, true>), dim3(nblk), dim3(64 * waves),
-                       0, s, fa, C, rois, lvl, order, P, segs, parts, out);
+    if (segs == 1 && parts == 1 && C <= 256 && getenv("VOSDET_RA_GENERAL") == nullptr)
+        hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_buf_kernel<2, true, true>), dim3(nblk),
+                           dim3(64 * waves), 0, s, fa, C, rois, lvl, order, P, 1, 1, out);
+    else
+        hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_buf_kernel<2, true, false>), dim3(nblk),
+                           dim3(64 * waves), 0, s, fa, C, rois, lvl, order, P, segs, parts, out);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
