@@ -42,22 +42,13 @@ namespace {
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef float f2v __attribute__((ext_vector_type(2)));
 
-constexpr int kCo = 64;  // output channels per U storage block
+constexpr int kCo = 64;  // output channels per workgroup
 constexpr int kKC = 8;   // input channels per chunk
+constexpr int k2Tiles = 32;
 constexpr int k2Threads = 256;
-
-// Workgroup shape: TILES = 32 tiles x 64 output channels (waves: 2 tile groups x 2
-// channel groups) or 64 tiles x 32 channels (4 tile groups).  Both compute 2048
-// (tile, channel) outputs per chunk; the 64 x 32 form stages half the U bytes (16
-// vs 32 KiB per chunk; the patch grows 8 -> 13-14 KiB) and transforms each tile's
-// patch once instead of twice -- the LDS-DMA fill, not the MFMA pipe, is what the
-// 32 x 64 form waits on at P2 (profiles/r03/wino_sol_probe.json).
-template <int TILES>
-struct WShape {
-    static constexpr int kCoW = TILES == 64 ? 32 : 64;  // output channels per workgroup
-    static constexpr int kUSlots = 16 * kCoW * 2;       // 16-B slots: U slice [pos][co][8]
-    static constexpr int kUDma = kUSlots / 256;         // 1 KiB U DMAs per wave per chunk
-};
+constexpr int k2USlots = 16 * kCo * 2;                // 16-B slots: U slice [pos][co][8]
+constexpr int k2PSlots = 512;                         // patch slots (480 used)
+constexpr int k2StageB = (k2USlots + k2PSlots) * 16;  // 40,960 B; two stages = 80 KiB
 
 __device__ float4 g_wino_zero;  // the source of out-of-image patch taps
 
@@ -68,14 +59,11 @@ __device__ float4 g_wino_zero;  // the source of out-of-image patch taps
 // distinct 8-byte bank pairs -- unswizzled they are 4-way conflicted
 __device__ __forceinline__ int sw_unit(int co) { return (co >> 2) & 3; }
 
-template <int TC, int TILES>
+template <int TC>
 struct Patch2 {  // patch [row][half][column] in 16-B slots
-    static constexpr int kTR = TILES / TC, kPR = 2 * kTR + 2, kPC = 2 * TC + 2;
+    static constexpr int kTR = k2Tiles / TC, kPR = 2 * kTR + 2, kPC = 2 * TC + 2;
     static constexpr int kHP = TC == 16 ? 37 : 20, kRP = TC == 16 ? 80 : 48;
-    // patch slots rounded up to whole 64-slot DMA blocks: 512 (32 tiles), 832 / 896
-    static constexpr int kPSlots = (kPR * kRP + 63) / 64 * 64, kPBlocks = kPSlots / 64;
-    static constexpr int kPDma = (kPBlocks + 3) / 4;  // patch DMAs per wave per chunk
-    static constexpr int kStageB = (WShape<TILES>::kUSlots + kPSlots) * 16;  // 40,960 B (32)
+    static_assert(kPR * kRP <= k2PSlots, "patch fits its LDS region");
     static_assert(kRP % 16 == 0, "row pitch: whole bank sweeps");
     // (p >> 4): columns 16 apart land 17 slots apart, so the 16 tiles of one
     // fragment read (pixel columns 2j + c) fall in distinct 16-B bank groups (one
@@ -107,21 +95,19 @@ __device__ __forceinline__ void wino_wait_barrier() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <bool RELU, int TC, int PR = 0, int TILES = 32>
+template <bool RELU, int TC, int PR = 0>
 __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
     int cb_per_xcd, int seg_h) {
-    using PG = Patch2<TC, TILES>;
-    using WS = WShape<TILES>;
-    constexpr int kCoW = WS::kCoW, k2StageB = PG::kStageB, k2USlots = WS::kUSlots;
+    using PG = Patch2<TC>;
     __shared__ __attribute__((aligned(16))) float sm[2 * k2StageB / 4];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int j = lane & 15, q = lane >> 4;
     // the Cout / 64 channel blocks of one spatial block run on one XCD (blocks
     // b, b + 8, ...): its input patches come from one L2
-    const int ncb = Cout / kCoW;
+    const int ncb = Cout / kCo;
     int cb, sp;
     if (cb_per_xcd) {  // XCD x computes channel block x % ncb: its L2 holds one U block
         const int xcd = blockIdx.x & 7;
@@ -138,28 +124,21 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     const int tyb = rem / tbx, txb = rem - (rem / tbx) * tbx;
     const int oy0 = 2 * PG::kTR * tyb, ox0 = 2 * TC * txb;
     const int iy0 = oy0 - 1, ix0 = ox0 - 1;
-    const int n0 = cb * kCoW;
-    // wave: tiles 16 tg .. + 15, 32-channel group cg
-    const int tg = TILES == 64 ? wave : (wave & 1), cg = TILES == 64 ? 0 : (wave >> 1);
+    const int n0 = cb * kCo;
+    const int tg = wave & 1, cg = wave >> 1;  // wave: tiles 16 tg .. + 15, 32-channel group
     const uint32_t sbase = (uint32_t)(uintptr_t)sm;
 
     // U DMA: U is stored chunk-blocked, [Cout / 64][C / 8][16][64][8], so a
     // chunk's slice is one contiguous 32 KiB run copied verbatim (whole cache
-    // lines per wave instruction); blocks b = wave + 4 i (i < 8) of 64 slots.
-    // TILES = 64: the workgroup's 32 channels are half of each position's 2 KiB
-    // row block, one contiguous 1 KiB run per position p = wave + 4 i (i < 4)
+    // lines per wave instruction); blocks b = wave + 4 i (i < 8) of 64 slots
     const int nch = C / kKC;
-    const float *usrc =
-        TILES == 64 ? U + (int64_t)(n0 / kCo) * nch * (16 * kCo * kKC) + wave * 512 +
-                          (n0 % kCo) * kKC + lane * 4
-                    : U + (int64_t)cb * nch * (16 * kCo * kKC) + wave * 256 + lane * 4;
-    constexpr int kUStep = TILES == 64 ? 2048 : 1024;  // floats between a wave's U DMAs
-    // patch DMA: blocks b = wave + 4 i (b < kPBlocks); slots outside the patch or
-    // the image copy zeros
-    const float *psrc[PG::kPDma];
-    bool pok[PG::kPDma];
+    const float *usrc = U + (int64_t)cb * nch * (16 * kCo * kKC) + wave * 256 + lane * 4;
+    // patch DMA: blocks b = wave + 4 i (i < 2); slots outside the patch or the
+    // image copy zeros
+    const float *psrc[2];
+    bool pok[2];
 #pragma unroll
-    for (int i = 0; i < PG::kPDma; ++i) {
+    for (int i = 0; i < 2; ++i) {
         const int s = 64 * (wave + 4 * i) + lane;
         const int r = s / PG::kRP, t = s - (s / PG::kRP) * PG::kRP;
         const int h = t >= PG::kHP;
@@ -175,12 +154,11 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     {                                                                                        \
         const uint32_t d_ = sbase + (uint32_t)(ST) * k2StageB + (uint32_t)wave * 1024u;      \
         const float *u_ = usrc + (int64_t)(CH) * (16 * kCo * kKC);                           \
-        _Pragma("unroll") for (int i = 0; i < WS::kUDma; ++i)                                \
-            wino_dma_1k(u_ + i * kUStep, d_ + (uint32_t)i * 4096u);                          \
-        _Pragma("unroll") for (int i = 0; i < PG::kPDma; ++i)                                \
-            if (wave + 4 * i < PG::kPBlocks)                                                 \
-                wino_dma_1k(pok[i] ? psrc[i] + (CH) * kKC : zero,                            \
-                            d_ + (uint32_t)(k2USlots * 16) + (uint32_t)i * 4096u);           \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i)                                        \
+            wino_dma_1k(u_ + i * 1024, d_ + (uint32_t)i * 4096u);                            \
+        _Pragma("unroll") for (int i = 0; i < 2; ++i)                                        \
+            wino_dma_1k(pok[i] ? psrc[i] + (CH) * kKC : zero,                                \
+                        d_ + (uint32_t)(k2USlots * 16) + (uint32_t)i * 4096u);               \
     }
     // transform reads: lane (j, q) -> tile 16 tg + j, channels 2q, 2q + 1 (half
     // q >> 1, dwords 2 (q & 1) ..): byte offsets within a stage
@@ -257,7 +235,7 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
 #pragma unroll
                 for (int t2 = 0; t2 < 2; ++t2)
                     af[i][t2] = (PR & 8) ? b[p0 + i + t2]
-                                         : *reinterpret_cast<const f2v *>(st + (p0 + i) * kCoW * kKC + ufo[t2]);
+                                         : *reinterpret_cast<const f2v *>(st + (p0 + i) * kCo * kKC + ufo[t2]);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -344,10 +322,6 @@ __global__ void wino_weight_kernel(const float *__restrict__ w, int Cout, int C,
 
 }  // namespace
 
-// the 64-tile form runs when its block shape covers at least this fraction of the
-// 32-tile form's useful pixels
-constexpr double kT64MinUse = 0.98;
-
 bool conv3x3_wino_supported(int C, int Cout) {
     return C % kKC == 0 && C >= kKC && Cout % kCo == 0 && Cout >= kCo;
 }
@@ -366,25 +340,17 @@ int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float 
     if ((int64_t)N * H * W == 0) return VD_OK;
     if (!conv3x3_wino_supported(C, Cout)) return VD_ERR_SHAPE;
     if (seg_h < 0 || (seg_h > 0 && (seg_h % 2 || H % seg_h))) return VD_ERR_SHAPE;
-    // block shape: 32 tiles x 64 channels as 8 x 16 or 4 x 32 output pixels, or 64
-    // tiles x 32 channels as 16 x 16 or 8 x 32, whichever wastes less of the map
+    // block shape: 8 x 16 or 4 x 32 output pixels, whichever wastes less of the map
     // (measured, profiles/r03/wino_small_probe.json: 8 x 16 wins on res5 / P5
-    // 25 x 42 maps and at P3, 4 x 32 at P4); VOSDET_WINO_SQ=1/0 forces the square /
-    // wide shape, VOSDET_WINO_T64=1/0 the 64- / 32-tile form
-    auto use = [&](int bh, int bw) {
-        return (double)H * W / ((double)((H + bh - 1) / bh * bh) * ((W + bw - 1) / bw * bw));
-    };
+    // 25 x 42 maps and at P3, 4 x 32 at P4); VOSDET_WINO_SQ=1/0 forces one
+    const double use_sq = (double)H * W / ((double)((H + 7) / 8 * 8) * ((W + 15) / 16 * 16));
+    const double use_wide = (double)H * W / ((double)((H + 3) / 4 * 4) * ((W + 31) / 32 * 32));
     const char *esq = getenv("VOSDET_WINO_SQ");
-    const bool sq32 = esq ? atoi(esq) == 1 : use(8, 16) > use(4, 32);
-    const bool sq64 = esq ? atoi(esq) == 1 : use(16, 16) > use(8, 32);
-    const double u32 = sq32 ? use(8, 16) : use(4, 32), u64 = sq64 ? use(16, 16) : use(8, 32);
-    const char *e64 = getenv("VOSDET_WINO_T64");
-    const bool t64 = e64 ? atoi(e64) == 1 : u64 >= kT64MinUse * u32;
-    const bool sq = t64 ? sq64 : sq32;
-    const int bh = t64 ? (sq ? 16 : 8) : (sq ? 8 : 4), bw = sq ? 16 : 32;
-    const int tby = (H + bh - 1) / bh, tbx = (W + bw - 1) / bw;
+    const bool sq = esq ? atoi(esq) == 1 : use_sq > use_wide;
+    const int tby = sq ? (H + 7) / 8 : (H + 3) / 4;
+    const int tbx = sq ? (W + 15) / 16 : (W + 31) / 32;
     const int64_t nsp = (int64_t)N * tby * tbx;
-    const int ncb = Cout / (t64 ? 32 : kCo);
+    const int ncb = Cout / kCo;
     // XCD x computes channel block x % ncb (its L2 keeps one U block instead of
     // all of them): bit-identical, P3 1.66 -> 1.51 ms, P2 / mask head 1-3 %
     // (profiles/r03/wino_map_probe.json); VOSDET_WINO_MAP=0 restores the
@@ -394,17 +360,12 @@ int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float 
     const int64_t blocks = cbx ? (nsp + 8 / ncb - 1) / (8 / ncb) * 8
                                : (nsp + 7) / 8 * 8 * ncb;
     if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
-    auto kern = t64 ? (sq ? (relu ? conv3x3_wino2_kernel<true, 8, 0, 64>
-                                  : conv3x3_wino2_kernel<false, 8, 0, 64>)
-                          : (relu ? conv3x3_wino2_kernel<true, 16, 0, 64>
-                                  : conv3x3_wino2_kernel<false, 16, 0, 64>))
-                    : (sq ? (relu ? conv3x3_wino2_kernel<true, 8> : conv3x3_wino2_kernel<false, 8>)
-                          : (relu ? conv3x3_wino2_kernel<true, 16>
-                                  : conv3x3_wino2_kernel<false, 16>));
+    auto kern = sq ? (relu ? conv3x3_wino2_kernel<true, 8> : conv3x3_wino2_kernel<false, 8>)
+                   : (relu ? conv3x3_wino2_kernel<true, 16> : conv3x3_wino2_kernel<false, 16>);
     // speed-of-light probes (wrong results): 1 no DMA, 2 no patch reads, 4 no
     // barrier, 8 no U reads
     const char *pe = getenv("VOSDET_WINO_PROBE");
-    switch (pe && !sq && !relu && !t64 ? atoi(pe) : 0) {
+    switch (pe && !sq && !relu ? atoi(pe) : 0) {
         case 1: kern = conv3x3_wino2_kernel<false, 16, 1>; break;
         case 2: kern = conv3x3_wino2_kernel<false, 16, 2>; break;
         case 4: kern = conv3x3_wino2_kernel<false, 16, 4>; break;
