@@ -173,6 +173,15 @@ int vd_conv3x3_wino_bias_act(const float *X, int N, int H, int W, int C, const f
 int vd_conv3x3_wino_seg_bias_act(const float *X, int H, int W, int C, const float *U, int Cout,
                                  const float *bias, int relu, int seg_h, float *Y, void *stream);
 
+/* The Winograd convolution of R maps of H x W pixels (R x H x W x C, each padded by
+ * its own zeros) run as one 2-D mosaic: g maps side by side per mosaic row, g the
+ * least count with g * W a multiple of 16, so neither the 8-row nor the 16-column
+ * side of a pixel block is split at a map edge (the mask head's 14 x 14 RoI maps:
+ * 8 per row, 112 columns).  H and W even; output in the input's R x H x W layout;
+ * bit-identical to vd_conv3x3_wino_bias_act on the R maps. */
+int vd_conv3x3_wino_mosaic_bias_act(const float *X, int R, int H, int W, int C, const float *U,
+                                    int Cout, const float *bias, int relu, float *Y, void *stream);
+
 /* The same convolution by Winograd F(4x4, 3x3) (4x fewer multiplies than the
  * direct form; transforms with factors up to 8, ~4x F(2x2, 3x3)'s rounding error,
  * ~4e-6 of max|y| at 256 channels): U from vd_conv3x3_wino4_weight (36 x Cout x

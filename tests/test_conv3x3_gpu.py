@@ -112,12 +112,18 @@ def test_conv3x3_wino4_vs_torch(N, C, H, W, Cout, relu):
 
 
 @pytest.mark.parametrize("N,C,H,W,Cout", [(37, 256, 14, 14, 256), (5, 64, 6, 20, 128),
-                                          (3, 8, 2, 9, 64), (9, 128, 14, 14, 64)])
+                                          (3, 8, 2, 9, 64), (9, 128, 14, 14, 64),
+                                          (1, 64, 14, 14, 64), (100, 256, 14, 14, 256),
+                                          (16, 64, 4, 6, 64), (7, 64, 8, 24, 64)])
 @pytest.mark.parametrize("relu", [False, True])
-def test_conv3x3_wino_mosaic_bit_exact(N, C, H, W, Cout, relu):
-    """The N maps as one (N * H)-row mosaic with per-map zero padding
-    (vd_conv3x3_wino_seg_bias_act, the mask head's route) give bit for bit the
-    per-map Winograd result, and stay within the conv tolerance of torch fp32."""
+@pytest.mark.parametrize("mode", [True, "2d"])
+def test_conv3x3_wino_mosaic_bit_exact(N, C, H, W, Cout, relu, mode):
+    """The N maps as one mosaic with per-map zero padding give bit for bit the
+    per-map Winograd result, and stay within the conv tolerance of torch fp32:
+    mode True stacks them in one (N * H)-row column (vd_conv3x3_wino_seg_bias_act),
+    "2d" also packs 16 / gcd(W, 16) maps side by side per mosaic row
+    (vd_conv3x3_wino_mosaic_bias_act, the mask head's route; a partly filled last
+    row when N is not a multiple of it; W odd is refused)."""
     from vosdetectron_amd import ops
     g = torch.Generator(device="cpu").manual_seed(13 * N + C + H + W + Cout)
     x = torch.randn(N, C, H, W, generator=g).cuda().contiguous(memory_format=torch.channels_last)
@@ -125,8 +131,12 @@ def test_conv3x3_wino_mosaic_bit_exact(N, C, H, W, Cout, relu):
     b = torch.randn(Cout, generator=g).cuda()
     u = ops.conv3x3_wino_weight(w)
     per = ops.conv3x3_wino_bias_act(x, u, b, relu=relu)
-    mos = ops.conv3x3_wino_bias_act(x, u, b, relu=relu, mosaic=True)
+    mos = ops.conv3x3_wino_bias_act(x, u, b, relu=relu, mosaic=mode)
     torch.cuda.synchronize()
+    if mode == "2d" and W % 2:
+        assert mos is None
+        return
+    assert mos.is_contiguous(memory_format=torch.channels_last)
     assert torch.equal(per, mos)
     ref = F.conv2d(x, w, b, padding=1)
     if relu:

@@ -149,6 +149,11 @@ int vd_conv3x3_wino_seg_bias_act(const float *X, int H, int W, int C, const floa
     return launch_conv3x3_wino(X, 1, H, W, C, U, Cout, bias, relu, Y, VD_STREAM(stream), seg_h);
 }
 
+int vd_conv3x3_wino_mosaic_bias_act(const float *X, int R, int H, int W, int C, const float *U,
+                                    int Cout, const float *bias, int relu, float *Y, void *stream) {
+    return launch_conv3x3_wino_mosaic(X, R, H, W, C, U, Cout, bias, relu, Y, VD_STREAM(stream));
+}
+
 int vd_conv3x3_wino4_weight(const float *w, int Cout, int Cin, float *U, void *stream) {
     if (Cout < 1 || Cin < 1 || !w || !U) return VD_ERR_ARG;
     return launch_conv3x3_wino4_weight(w, Cout, Cin, U, VD_STREAM(stream));

@@ -99,7 +99,7 @@ template <bool RELU, int TC, int PR = 0>
 __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
-    int cb_per_xcd, int seg_h) {
+    int cb_per_xcd, int seg_h, int seg_w, int gx, int nmaps) {
     using PG = Patch2<TC>;
     __shared__ __attribute__((aligned(16))) float sm[2 * k2StageB / 4];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -145,9 +145,16 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
         const int u = t - h * PG::kHP - ((r >> 1) & 1);
         const int p = u < 16 ? u : (u < 33 ? u - 1 : u - 2);
         const int y = iy0 + r, x = ix0 + p;
-        pok[i] = r < PG::kPR && u >= 0 && p < PG::kPC && PG::slot(r, h, p) == s &&
-                 (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-        psrc[i] = pok[i] ? X + (((int64_t)n * H + y) * W + x) * C + 4 * h : X;
+        bool ok = r < PG::kPR && u >= 0 && p < PG::kPC && PG::slot(r, h, p) == s &&
+                  (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+        int64_t pix = ((int64_t)n * H + y) * W + x;
+        if (seg_w > 0 && ok) {  // 2-D mosaic pixel (y, x) -> map, row, column in X
+            const int m = (y / seg_h) * gx + x / seg_w;
+            ok = m < nmaps;
+            pix = ((int64_t)m * seg_h + y % seg_h) * seg_w + x % seg_w;
+        }
+        pok[i] = ok;
+        psrc[i] = ok ? X + pix * C + 4 * h : X;
     }
     const float *zero = reinterpret_cast<const float *>(&g_wino_zero);
 #define VD_W2_DMA(CH, ST)                                                                    \
@@ -170,6 +177,11 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     const int toy = oy0 + 2 * tr;  // the tile's first output row
     const bool zero_top = seg_h > 0 && toy % seg_h == 0;
     const bool zero_bot = seg_h > 0 && (toy + 2) % seg_h == 0;
+    // 2-D mosaic (seg_w > 0: gx maps side by side per mosaic row): the same for the
+    // patch columns left / right of a tile at a map's side (seg_w even)
+    const int tox = ox0 + 2 * tc;
+    const bool zero_left = seg_w > 0 && tox % seg_w == 0;
+    const bool zero_right = seg_w > 0 && (tox + 2) % seg_w == 0;
     int roff[4], coff[4];
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -208,6 +220,8 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
         for (int c = 0; c < 4; ++c) {
             if (zero_top) d[0][c] = f2v{0.f, 0.f};
             if (zero_bot) d[3][c] = f2v{0.f, 0.f};
+            if (zero_left) d[c][0] = f2v{0.f, 0.f};
+            if (zero_right) d[c][3] = f2v{0.f, 0.f};
         }
         f2v b[16];
 #pragma unroll
@@ -278,6 +292,12 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
         for (int k = 0; k < 4; ++k) {
             const int y = oy + (k >> 1), x = ox + (k & 1);
             if (y >= H || x >= W) continue;
+            int64_t pix = (int64_t)(n * H + y) * W + x;
+            if (seg_w > 0) {
+                const int m = (y / seg_h) * gx + x / seg_w;
+                if (m >= nmaps) continue;
+                pix = ((int64_t)m * seg_h + y % seg_h) * seg_w + x % seg_w;
+            }
             float4 v = make_float4(o[k][0] + bv.x, o[k][1] + bv.y, o[k][2] + bv.z,
                                    o[k][3] + bv.w);
             if (RELU) {
@@ -286,7 +306,7 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
                 v.z = fmaxf(v.z, 0.f);
                 v.w = fmaxf(v.w, 0.f);
             }
-            *reinterpret_cast<float4 *>(Y + ((int64_t)(n * H + y) * W + x) * Cout + co) = v;
+            *reinterpret_cast<float4 *>(Y + pix * Cout + co) = v;
         }
     }
 }
@@ -335,11 +355,11 @@ int launch_conv3x3_wino_weight(const float *w, int Cout, int C, float *U, hipStr
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
-int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float *U, int Cout,
-                        const float *bias, int relu, float *Y, hipStream_t s, int seg_h) {
-    if ((int64_t)N * H * W == 0) return VD_OK;
-    if (!conv3x3_wino_supported(C, Cout)) return VD_ERR_SHAPE;
-    if (seg_h < 0 || (seg_h > 0 && (seg_h % 2 || H % seg_h))) return VD_ERR_SHAPE;
+namespace {
+
+int launch_wino(const float *X, int N, int H, int W, int C, const float *U, int Cout,
+                const float *bias, int relu, float *Y, hipStream_t s, int seg_h, int seg_w, int gx,
+                int nmaps) {
     // block shape: 8 x 16 or 4 x 32 output pixels, whichever wastes less of the map
     // (measured, profiles/r03/wino_small_probe.json: 8 x 16 wins on res5 / P5
     // 25 x 42 maps and at P3, 4 x 32 at P4); VOSDET_WINO_SQ=1/0 forces one
@@ -375,8 +395,35 @@ int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float 
         default: break;
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(k2Threads), 0, s, X, N, H, W, C, U, Cout,
-                       bias, Y, tby, tbx, cbx, seg_h);
+                       bias, Y, tby, tbx, cbx, seg_h, seg_w, gx, nmaps);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+}  // namespace
+
+int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float *U, int Cout,
+                        const float *bias, int relu, float *Y, hipStream_t s, int seg_h) {
+    if ((int64_t)N * H * W == 0) return VD_OK;
+    if (!conv3x3_wino_supported(C, Cout)) return VD_ERR_SHAPE;
+    if (seg_h < 0 || (seg_h > 0 && (seg_h % 2 || H % seg_h))) return VD_ERR_SHAPE;
+    return launch_wino(X, N, H, W, C, U, Cout, bias, relu, Y, s, seg_h, 0, 0, 0);
+}
+
+// R maps of H x W pixels ([R][H][W][C]) as one 2-D mosaic: gx maps side by side per
+// mosaic row, gx the least count that makes the mosaic width a multiple of 16 (the
+// 8 x 16-pixel block: 14 x 14 maps -> gx = 8, 112 columns, no idle block columns);
+// the last mosaic row may be partly empty (its pixels read 0 and are not stored)
+int launch_conv3x3_wino_mosaic(const float *X, int R, int H, int W, int C, const float *U,
+                               int Cout, const float *bias, int relu, float *Y, hipStream_t s) {
+    if ((int64_t)R * H * W == 0) return VD_OK;
+    if (!conv3x3_wino_supported(C, Cout)) return VD_ERR_SHAPE;
+    if (R < 0 || H < 0 || W < 0 || H % 2 || W % 2) return VD_ERR_SHAPE;
+    int g = 16;
+    for (int w = W; w % 2 == 0 && g > 1; w /= 2) g /= 2;  // 16 / gcd(W, 16)
+    if (g > R) g = R;
+    const int64_t Hm = (int64_t)(R + g - 1) / g * H, Wm = (int64_t)g * W;
+    if (Hm > 0x3fffffff || Wm > 0x3fffffff) return VD_ERR_SHAPE;
+    return launch_wino(X, 1, (int)Hm, (int)Wm, C, U, Cout, bias, relu, Y, s, H, W, g, R);
 }
 
 }  // namespace vd

@@ -53,6 +53,8 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
 int launch_conv3x3_wino_weight(const float *w, int Cout, int C, float *U, hipStream_t s);
 int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float *U, int Cout,
                         const float *bias, int relu, float *Y, hipStream_t s, int seg_h = 0);
+int launch_conv3x3_wino_mosaic(const float *X, int R, int H, int W, int C, const float *U,
+                               int Cout, const float *bias, int relu, float *Y, hipStream_t s);
 bool gemm1x1_dual_supported(int K1, int K2, int N);
 int launch_gemm1x1_dual(const float *A1, int K1, const float *A2, int K2, int M, const float *W,
                         int N, const float *bias, int relu, float *D, hipStream_t s);

@@ -18,6 +18,7 @@ preceding conv (``fold_affine``), the RPN's cls/bbox 1x1 convs are fused into on
 """
 from __future__ import annotations
 
+import math
 import os
 from collections import OrderedDict
 
@@ -74,6 +75,16 @@ def _wino_block_use(H: int, W: int) -> float:
     return max(H * W / float(-(-H // br) * br * -(-W // bc) * bc) for br, bc in ((8, 16), (4, 32)))
 
 
+def _mosaic_dims(N: int, H: int, W: int, mos):
+    """(rows, columns) of the image the Winograd kernel sees: one map, the maps
+    stacked (mosaic rows), or g = 16 / gcd(W, 16) maps side by side per mosaic row
+    (launch_conv3x3_wino_mosaic)."""
+    if mos == "2d":
+        g = min(16 // math.gcd(W, 16), N)
+        return -(-N // g) * H, g * W
+    return (N * H, W) if mos else (H, W)
+
+
 def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=False):
     """conv (3x3, stride 1, pad 1) of a channels_last fp32 tensor on the
     hand-written MFMA kernels with the bias (+ ReLU) epilogue, or None where
@@ -82,8 +93,11 @@ def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=False):
     from 2^12 output pixels where its blocks are >= 60 % real output -- else the
     implicit GEMM (csrc/conv3x3.hip) from 2^18 pixels, else MIOpen / CK.
     mosaic=True (the mask head's N x 14 x 14 RoI maps): Winograd runs the batch as
-    one (N * H)-row image with per-map zero padding -- 87.5 % instead of 77 % of its
-    8 x 16-pixel blocks is real output, bit-identical results.  The transformed weights are cached on the module."""
+    one 2-D mosaic of maps with per-map zero padding, 8 maps of 14 x 14 side by side
+    per 112-column mosaic row -- every 8 x 16-pixel block is real output (77 % one
+    map per block, 87.5 % with the maps stacked in one column,
+    VOSDET_WINO_MOSAIC=1), bit-identical results.  The transformed weights are
+    cached on the module."""
     if (os.environ.get("VOSDET_CONV3X3_MFMA", "1") == "0" or not x.is_cuda
             or conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1)
             or conv.dilation != (1, 1) or conv.groups != 1 or x.dtype != torch.float32
@@ -93,9 +107,11 @@ def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=False):
     w = conv.weight
     key = (w.data_ptr(), w._version)
     b = conv.bias.detach() if (bias and conv.bias is not None) else None
-    mos = mosaic and x.shape[0] > 1 and x.shape[2] % 2 == 0 \
-        and os.environ.get("VOSDET_WINO_MOSAIC", "1") != "0"
-    use = _wino_block_use(x.shape[0] * x.shape[2] if mos else x.shape[2], x.shape[3])
+    mos_env = os.environ.get("VOSDET_WINO_MOSAIC", "2")
+    mos = mosaic and x.shape[0] > 1 and x.shape[2] % 2 == 0 and mos_env != "0"
+    if mos and mos_env == "2" and x.shape[3] % 2 == 0:
+        mos = "2d"
+    use = _wino_block_use(*_mosaic_dims(x.shape[0], x.shape[2], x.shape[3], mos))
     if (os.environ.get("VOSDET_CONV3X3_ALGO", CONV3X3_ALGO) == "wino" and npx >= _WINO_MIN_PIXELS
             and use >= _WINO_MIN_BLOCK_USE):
         if getattr(conv, "_vd_u_key", None) != key:

@@ -602,8 +602,9 @@ def conv3x3_wino_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch
     F(2x2,3x3) on the MFMA pipes (vd_conv3x3_wino_bias_act); u from
     conv3x3_wino_weight.  mosaic=True runs the N images as one N*H-row image with
     per-image zero padding (vd_conv3x3_wino_seg_bias_act; H even): bit-identical,
-    fewer idle block rows on small maps.  Returns None for a shape the kernel
-    does not serve."""
+    fewer idle block rows on small maps.  mosaic="2d" also packs maps side by side
+    (vd_conv3x3_wino_mosaic_bias_act; H, W even): no idle block columns either.
+    Returns None for a shape the kernel does not serve."""
     if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 4 \
             or not x.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("x must be a channels_last fp32 device tensor")
@@ -618,7 +619,11 @@ def conv3x3_wino_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch
     if out is None:
         out = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device,
                           memory_format=torch.channels_last)
-    if mosaic and N > 0:
+    if mosaic == "2d" and N > 0:
+        st = lib().vd_conv3x3_wino_mosaic_bias_act(x.data_ptr(), N, H, W, C, u_.data_ptr(), Cout,
+                                                   b_.data_ptr() if b_ is not None else None,
+                                                   int(relu), out.data_ptr(), _stream())
+    elif mosaic and N > 0:
         st = lib().vd_conv3x3_wino_seg_bias_act(x.data_ptr(), N * H, W, C, u_.data_ptr(), Cout,
                                                 b_.data_ptr() if b_ is not None else None,
                                                 int(relu), H, out.data_ptr(), _stream())
