@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Mask-head Winograd conv (1600 RoI maps of 14 x 14, 256 -> 256, bias + ReLU):
-per-map launch vs the row mosaic (maps stacked, VOSDET_WINO_MOSAIC=1) vs the 2-D
-mosaic (8 maps per 112-column row, the default); HIP-event ms per call, alternating."""
+"""Winograd layouts of a batch of maps on the step's shapes: per-map launch (False)
+vs the row mosaic (maps stacked, True) vs the 2-D mosaic ("2d": 16 / gcd(W, 16) maps
+per row) -- HIP-event ms per call, alternating, and which one modeling._pick_mosaic
+routes.  Mask head: 1600 RoI maps of 14 x 14; P3 / P4: the 16-frame batch."""
 import json
 import os
 import sys
@@ -10,18 +11,14 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from vosdetectron_amd import ops  # noqa: E402
+from vosdetectron_amd.modeling import _pick_mosaic  # noqa: E402
 
-N, C, H, W = int(os.environ.get("MAPS", "1600")), 256, 14, 14
-g = torch.Generator(device="cuda").manual_seed(0)
-x = torch.randn(N, C, H, W, device="cuda", generator=g).contiguous(memory_format=torch.channels_last)
-w = torch.randn(C, C, 3, 3, device="cuda", generator=g) / (9 * C) ** .5
-b = torch.randn(C, device="cuda", generator=g)
-u = ops.conv3x3_wino_weight(w)
-out = torch.empty_like(x)
+SHAPES = [(1600, 256, 256, 14, 14, True), (16, 256, 256, 100, 168, False),
+          (16, 256, 256, 100, 168, True), (16, 128, 128, 100, 168, True),
+          (16, 256, 256, 50, 84, True), (16, 256, 256, 50, 84, False)]
 
 
-def timed(mode, iters=20):
-    f = lambda: ops.conv3x3_wino_bias_act(x, u, b, relu=True, out=out, mosaic=mode)  # noqa: E731
+def timed(f, iters=20):
     for _ in range(3):
         f()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -33,8 +30,23 @@ def timed(mode, iters=20):
     return e0.elapsed_time(e1) / iters
 
 
-res = {"maps": N, "per_map": [], "rows": [], "2d": []}
-for _ in range(3):
-    for k, m in (("per_map", False), ("rows", True), ("2d", "2d")):
-        res[k].append(round(timed(m), 4))
-print(json.dumps(res), flush=True)
+for N, C, Co, H, W, relu in SHAPES:
+    g = torch.Generator(device="cuda").manual_seed(0)
+    x = torch.randn(N, C, H, W, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    w = torch.randn(Co, C, 3, 3, device="cuda", generator=g) / (9 * C) ** .5
+    b = torch.randn(Co, device="cuda", generator=g)
+    u = ops.conv3x3_wino_weight(w)
+    out = torch.empty((N, Co, H, W), device="cuda").contiguous(memory_format=torch.channels_last)
+    res = {"shape": [N, C, Co, H, W], "relu": relu, "routed": str(_pick_mosaic(N, H, W)[0]),
+           "per_map": [], "rows": [], "2d": []}
+    ref = ops.conv3x3_wino_bias_act(x, u, b, relu=relu).clone()
+    for _ in range(3):
+        for k, m in (("per_map", False), ("rows", True), ("2d", "2d")):
+            res[k].append(round(timed(lambda: ops.conv3x3_wino_bias_act(
+                x, u, b, relu=relu, out=out, mosaic=m)), 4))
+            res.setdefault("bit_identical_" + k, True)
+            res["bit_identical_" + k] &= bool(torch.equal(out, ref))
+    print(json.dumps(res), flush=True)
+    del x, out, ref
+    torch.cuda.empty_cache()

@@ -85,19 +85,35 @@ def _mosaic_dims(N: int, H: int, W: int, mos):
     return (N * H, W) if mos else (H, W)
 
 
-def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=False):
+def _pick_mosaic(N: int, H: int, W: int, allow=True):
+    """The Winograd layout of a batch with the most real output per pixel block:
+    one launch over the N images as they are (False), stacked in one column (True),
+    or tiled 2-D ("2d"); ties keep the simpler layout.  VOSDET_WINO_MOSAIC: 0 off,
+    1 rows at most, 2 (default) any."""
+    env = os.environ.get("VOSDET_WINO_MOSAIC", "2")
+    best = (False, _wino_block_use(H, W))
+    if not allow or env == "0" or N < 2 or H % 2:
+        return best
+    cands = [True] + (["2d"] if env == "2" and W % 2 == 0 else [])
+    for m in cands:
+        u = _wino_block_use(*_mosaic_dims(N, H, W, m))
+        if u > best[1] + 1e-9:
+            best = (m, u)
+    return best
+
+
+def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=True):
     """conv (3x3, stride 1, pad 1) of a channels_last fp32 tensor on the
     hand-written MFMA kernels with the bias (+ ReLU) epilogue, or None where
     they do not apply (other geometry, VOSDET_CONV3X3_MFMA=0).  Algorithm
     (VOSDET_CONV3X3_ALGO): 'wino' -- Winograd F(2x2,3x3), csrc/conv3x3_wino.hip,
     from 2^12 output pixels where its blocks are >= 60 % real output -- else the
     implicit GEMM (csrc/conv3x3.hip) from 2^18 pixels, else MIOpen / CK.
-    mosaic=True (the mask head's N x 14 x 14 RoI maps): Winograd runs the batch as
-    one 2-D mosaic of maps with per-map zero padding, 8 maps of 14 x 14 side by side
-    per 112-column mosaic row -- every 8 x 16-pixel block is real output (77 % one
-    map per block, 87.5 % with the maps stacked in one column,
-    VOSDET_WINO_MOSAIC=1), bit-identical results.  The transformed weights are
-    cached on the module."""
+    mosaic=True lets Winograd run the batch as a mosaic of maps with per-map zero
+    padding (_pick_mosaic): the mask head's 14 x 14 RoI maps 8 side by side per
+    112-column row -- every 8 x 16-pixel block real output (77 % one map per block,
+    87.5 % stacked in one column) -- and the 16-frame P3 / P4 maps 2 / 4 per row;
+    bit-identical results.  The transformed weights are cached on the module."""
     if (os.environ.get("VOSDET_CONV3X3_MFMA", "1") == "0" or not x.is_cuda
             or conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1)
             or conv.dilation != (1, 1) or conv.groups != 1 or x.dtype != torch.float32
@@ -107,11 +123,7 @@ def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=False):
     w = conv.weight
     key = (w.data_ptr(), w._version)
     b = conv.bias.detach() if (bias and conv.bias is not None) else None
-    mos_env = os.environ.get("VOSDET_WINO_MOSAIC", "2")
-    mos = mosaic and x.shape[0] > 1 and x.shape[2] % 2 == 0 and mos_env != "0"
-    if mos and mos_env == "2" and x.shape[3] % 2 == 0:
-        mos = "2d"
-    use = _wino_block_use(*_mosaic_dims(x.shape[0], x.shape[2], x.shape[3], mos))
+    mos, use = _pick_mosaic(x.shape[0], x.shape[2], x.shape[3], mosaic)
     if (os.environ.get("VOSDET_CONV3X3_ALGO", CONV3X3_ALGO) == "wino" and npx >= _WINO_MIN_PIXELS
             and use >= _WINO_MIN_BLOCK_USE):
         if getattr(conv, "_vd_u_key", None) != key:
