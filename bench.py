@@ -95,7 +95,7 @@ def xcd_order(rois, lvls, n_xcd=8):
 
 ROIALIGN_KERNEL = {"3": "vd::roi_align_fpn_nhwc_kernel<7,2,2> (reference order)",
                    "8": "vd::roi_align_fpn_nhwc_sep_kernel<2,true> (separable, nt stores)",
-                   "10": "vd::roi_align_fpn_nhwc_sep_buf_kernel<2,true> (separable, buffer loads, "
+                   "10": "vd::roi_align_fpn_nhwc_sep_buf_kernel<2,true,true> (separable, buffer loads, "
                          "nt stores)",
                    "30": "vd::ratile::tile_kernel (tile-binned, LDS-DMA windows, reference "
                          "arithmetic) + bin_count / tile_scan / bin_scatter / direct"}
