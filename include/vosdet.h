@@ -177,8 +177,9 @@ int vd_conv3x3_wino_seg_bias_act(const float *X, int H, int W, int C, const floa
  * its own zeros) run as one 2-D mosaic: g maps side by side per mosaic row, g the
  * least count with g * W a multiple of 16, so neither the 8-row nor the 16-column
  * side of a pixel block is split at a map edge (the mask head's 14 x 14 RoI maps:
- * 8 per row, 112 columns).  H and W even; output in the input's R x H x W layout;
- * bit-identical to vd_conv3x3_wino_bias_act on the R maps. */
+ * 8 per row, 112 columns).  An odd H or W gets one phantom row / column per map
+ * (reads 0, never stored).  Output in the input's R x H x W layout; bit-identical to
+ * vd_conv3x3_wino_bias_act on the R maps. */
 int vd_conv3x3_wino_mosaic_bias_act(const float *X, int R, int H, int W, int C, const float *U,
                                     int Cout, const float *bias, int relu, float *Y, void *stream);
 

@@ -71,3 +71,34 @@ def test_winograd_block_occupancy_gate():
     assert _wino_block_use(8, 32) == 1.0
     # res5 / P5 25 x 42 maps: the 8 x 16 blocks (68 %) beat 4 x 32 (59 %)
     assert abs(_wino_block_use(25, 42) - 25 * 42 / (32 * 48)) < 1e-12
+
+
+def test_winograd_mosaic_choice():
+    """modeling._pick_mosaic: a batch runs per image when its blocks are already
+    full (P2 200 x 336), else as the 2-D mosaic, whose use counts the phantom
+    row / column of an odd side as waste: C4's 7 x 7 RoI maps 49 / 64 (over the
+    0.6 gate), res5 25 x 42 maps 16 * 1050 / (52 * 352), the mask head's 14 x 14
+    maps and the P3 / P4 batches 100 %; one map never mosaics; VOSDET_WINO_MOSAIC=1
+    allows the one-column form only (even H), 0 none."""
+    import os
+    from vosdetectron_amd.modeling import _WINO_MIN_BLOCK_USE, _pick_mosaic
+    assert _pick_mosaic(16, 200, 336) == (False, 1.0)
+    m, u = _pick_mosaic(8000, 7, 7)
+    assert m == "2d" and abs(u - 49 / 64) < 1e-12 and u >= _WINO_MIN_BLOCK_USE
+    m, u = _pick_mosaic(16, 25, 42)
+    assert m == "2d" and abs(u - 16 * 25 * 42 / (52 * 352)) < 1e-12  # 4 x 32 blocks
+    for shape in [(1600, 14, 14), (16, 100, 168), (16, 50, 84)]:
+        assert _pick_mosaic(*shape) == ("2d", 1.0), shape
+    assert _pick_mosaic(1, 7, 7)[0] is False
+    old = os.environ.get("VOSDET_WINO_MOSAIC")
+    try:
+        os.environ["VOSDET_WINO_MOSAIC"] = "1"
+        assert _pick_mosaic(1600, 14, 14)[0] is True
+        assert _pick_mosaic(8000, 7, 7)[0] is False
+        os.environ["VOSDET_WINO_MOSAIC"] = "0"
+        assert _pick_mosaic(1600, 14, 14)[0] is False
+    finally:
+        if old is None:
+            os.environ.pop("VOSDET_WINO_MOSAIC", None)
+        else:
+            os.environ["VOSDET_WINO_MOSAIC"] = old

@@ -114,7 +114,9 @@ def test_conv3x3_wino4_vs_torch(N, C, H, W, Cout, relu):
 @pytest.mark.parametrize("N,C,H,W,Cout", [(37, 256, 14, 14, 256), (5, 64, 6, 20, 128),
                                           (3, 8, 2, 9, 64), (9, 128, 14, 14, 64),
                                           (1, 64, 14, 14, 64), (100, 256, 14, 14, 256),
-                                          (16, 64, 4, 6, 64), (7, 64, 8, 24, 64)])
+                                          (16, 64, 4, 6, 64), (7, 64, 8, 24, 64),
+                                          (16, 64, 25, 42, 64), (5, 64, 13, 21, 128),
+                                          (9, 64, 7, 7, 64)])
 @pytest.mark.parametrize("relu", [False, True])
 @pytest.mark.parametrize("mode", [True, "2d"])
 def test_conv3x3_wino_mosaic_bit_exact(N, C, H, W, Cout, relu, mode):
@@ -122,8 +124,9 @@ def test_conv3x3_wino_mosaic_bit_exact(N, C, H, W, Cout, relu, mode):
     per-map Winograd result, and stay within the conv tolerance of torch fp32:
     mode True stacks them in one (N * H)-row column (vd_conv3x3_wino_seg_bias_act),
     "2d" also packs 16 / gcd(W, 16) maps side by side per mosaic row
-    (vd_conv3x3_wino_mosaic_bias_act, the mask head's route; a partly filled last
-    row when N is not a multiple of it; W odd is refused)."""
+    (vd_conv3x3_wino_mosaic_bias_act; a partly filled last row when N is not a
+    multiple of it; odd sides padded by a phantom row / column per map).  The row
+    mosaic refuses an odd H."""
     from vosdetectron_amd import ops
     g = torch.Generator(device="cpu").manual_seed(13 * N + C + H + W + Cout)
     x = torch.randn(N, C, H, W, generator=g).cuda().contiguous(memory_format=torch.channels_last)
@@ -133,7 +136,7 @@ def test_conv3x3_wino_mosaic_bit_exact(N, C, H, W, Cout, relu, mode):
     per = ops.conv3x3_wino_bias_act(x, u, b, relu=relu)
     mos = ops.conv3x3_wino_bias_act(x, u, b, relu=relu, mosaic=mode)
     torch.cuda.synchronize()
-    if mode == "2d" and W % 2:
+    if mode is True and H % 2:
         assert mos is None
         return
     assert mos.is_contiguous(memory_format=torch.channels_last)

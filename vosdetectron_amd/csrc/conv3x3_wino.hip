@@ -99,7 +99,7 @@ template <bool RELU, int TC, int PR = 0>
 __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
-    int cb_per_xcd, int seg_h, int seg_w, int gx, int nmaps) {
+    int cb_per_xcd, int seg_h, int seg_w, int gx, int nmaps, int map_h, int map_w) {
     using PG = Patch2<TC>;
     __shared__ __attribute__((aligned(16))) float sm[2 * k2StageB / 4];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -149,9 +149,9 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
                   (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
         int64_t pix = ((int64_t)n * H + y) * W + x;
         if (seg_w > 0 && ok) {  // 2-D mosaic pixel (y, x) -> map, row, column in X
-            const int m = (y / seg_h) * gx + x / seg_w;
-            ok = m < nmaps;
-            pix = ((int64_t)m * seg_h + y % seg_h) * seg_w + x % seg_w;
+            const int m = (y / seg_h) * gx + x / seg_w, my = y % seg_h, mx = x % seg_w;
+            ok = m < nmaps && my < map_h && mx < map_w;  // a map's phantom row / column: 0
+            pix = ((int64_t)m * map_h + my) * map_w + mx;
         }
         pok[i] = ok;
         psrc[i] = ok ? X + pix * C + 4 * h : X;
@@ -294,9 +294,9 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
             if (y >= H || x >= W) continue;
             int64_t pix = (int64_t)(n * H + y) * W + x;
             if (seg_w > 0) {
-                const int m = (y / seg_h) * gx + x / seg_w;
-                if (m >= nmaps) continue;
-                pix = ((int64_t)m * seg_h + y % seg_h) * seg_w + x % seg_w;
+                const int m = (y / seg_h) * gx + x / seg_w, my = y % seg_h, mx = x % seg_w;
+                if (m >= nmaps || my >= map_h || mx >= map_w) continue;
+                pix = ((int64_t)m * map_h + my) * map_w + mx;
             }
             float4 v = make_float4(o[k][0] + bv.x, o[k][1] + bv.y, o[k][2] + bv.z,
                                    o[k][3] + bv.w);
@@ -359,7 +359,7 @@ namespace {
 
 int launch_wino(const float *X, int N, int H, int W, int C, const float *U, int Cout,
                 const float *bias, int relu, float *Y, hipStream_t s, int seg_h, int seg_w, int gx,
-                int nmaps) {
+                int nmaps, int map_h, int map_w) {
     // block shape: 8 x 16 or 4 x 32 output pixels, whichever wastes less of the map
     // (measured, profiles/r03/wino_small_probe.json: 8 x 16 wins on res5 / P5
     // 25 x 42 maps and at P3, 4 x 32 at P4); VOSDET_WINO_SQ=1/0 forces one
@@ -395,7 +395,7 @@ int launch_wino(const float *X, int N, int H, int W, int C, const float *U, int 
         default: break;
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(k2Threads), 0, s, X, N, H, W, C, U, Cout,
-                       bias, Y, tby, tbx, cbx, seg_h, seg_w, gx, nmaps);
+                       bias, Y, tby, tbx, cbx, seg_h, seg_w, gx, nmaps, map_h, map_w);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
@@ -406,24 +406,27 @@ int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float 
     if ((int64_t)N * H * W == 0) return VD_OK;
     if (!conv3x3_wino_supported(C, Cout)) return VD_ERR_SHAPE;
     if (seg_h < 0 || (seg_h > 0 && (seg_h % 2 || H % seg_h))) return VD_ERR_SHAPE;
-    return launch_wino(X, N, H, W, C, U, Cout, bias, relu, Y, s, seg_h, 0, 0, 0);
+    return launch_wino(X, N, H, W, C, U, Cout, bias, relu, Y, s, seg_h, 0, 0, 0, 0, 0);
 }
 
-// R maps of H x W pixels ([R][H][W][C]) as one 2-D mosaic: gx maps side by side per
+// R maps of H x W pixels ([R][H][W][C]) as one 2-D mosaic: each map on an even
+// pitch (an odd side gets one phantom row / column that reads 0 and is not stored,
+// which is what the map's own zero padding gives that tile), gx maps side by side per
 // mosaic row, gx the least count that makes the mosaic width a multiple of 16 (the
 // 8 x 16-pixel block: 14 x 14 maps -> gx = 8, 112 columns, no idle block columns);
 // the last mosaic row may be partly empty (its pixels read 0 and are not stored)
 int launch_conv3x3_wino_mosaic(const float *X, int R, int H, int W, int C, const float *U,
                                int Cout, const float *bias, int relu, float *Y, hipStream_t s) {
+    if (R < 0 || H < 0 || W < 0) return VD_ERR_SHAPE;
     if ((int64_t)R * H * W == 0) return VD_OK;
     if (!conv3x3_wino_supported(C, Cout)) return VD_ERR_SHAPE;
-    if (R < 0 || H < 0 || W < 0 || H % 2 || W % 2) return VD_ERR_SHAPE;
+    const int ph = H + (H & 1), pw = W + (W & 1);
     int g = 16;
-    for (int w = W; w % 2 == 0 && g > 1; w /= 2) g /= 2;  // 16 / gcd(W, 16)
+    for (int w = pw; w % 2 == 0 && g > 1; w /= 2) g /= 2;  // 16 / gcd(pw, 16)
     if (g > R) g = R;
-    const int64_t Hm = (int64_t)(R + g - 1) / g * H, Wm = (int64_t)g * W;
+    const int64_t Hm = (int64_t)(R + g - 1) / g * ph, Wm = (int64_t)g * pw;
     if (Hm > 0x3fffffff || Wm > 0x3fffffff) return VD_ERR_SHAPE;
-    return launch_wino(X, 1, (int)Hm, (int)Wm, C, U, Cout, bias, relu, Y, s, H, W, g, R);
+    return launch_wino(X, 1, (int)Hm, (int)Wm, C, U, Cout, bias, relu, Y, s, ph, pw, g, R, H, W);
 }
 
 }  // namespace vd

@@ -62,26 +62,33 @@ def _conv_epi(conv: nn.Conv2d, x, relu=True, res=None, res_bias=None, up=False):
 
 _CONV3X3_MIN_PIXELS = 1 << 18  # below this CK's kernels fill the chip better
 _WINO_MIN_PIXELS = 1 << 12  # res5 / P5 / P6 of a 16-frame batch included (beats MIOpen / CK)
-# Winograd workgroups cover 8 x 16 or 4 x 32 output pixels of one image (the kernel
-# takes the shape that wastes less): on the C4 head's 7 x 7 RoI maps only 49 / 128 of
-# a block is real work, which loses to the implicit GEMM (pixels packed across
-# images): 69 -> 60 frames/s
+# Winograd workgroups cover 8 x 16 or 4 x 32 output pixels (the kernel takes the
+# shape that wastes less): the C4 head's 7 x 7 RoI maps one per block are 49 / 128
+# real work, which lost to the implicit GEMM (69 -> 60 frames/s); as a 2-D mosaic of
+# 8 x 8-pitch maps they are 77 % real and beat it, 9.99 vs 13.24 ms per 8000-map conv
+# (profiles/r03/wino_mosaic2d/odd_shapes_probe.json)
 _WINO_MIN_BLOCK_USE = 0.6
 
 
+def _wino_block_area(H: int, W: int) -> int:
+    """Pixels of the Winograd pixel blocks covering an H x W image, for the block
+    shape the kernel picks (csrc/conv3x3_wino.hip, launch_conv3x3_wino)."""
+    return min(-(-H // br) * br * -(-W // bc) * bc for br, bc in ((8, 16), (4, 32)))
+
+
 def _wino_block_use(H: int, W: int) -> float:
-    """Fraction of the Winograd kernel's pixel blocks that is real output, for the
-    block shape it picks (csrc/conv3x3_wino.hip, launch_conv3x3_wino)."""
-    return max(H * W / float(-(-H // br) * br * -(-W // bc) * bc) for br, bc in ((8, 16), (4, 32)))
+    """Fraction of the Winograd kernel's pixel blocks that is real output."""
+    return H * W / float(_wino_block_area(H, W))
 
 
 def _mosaic_dims(N: int, H: int, W: int, mos):
     """(rows, columns) of the image the Winograd kernel sees: one map, the maps
-    stacked (mosaic rows), or g = 16 / gcd(W, 16) maps side by side per mosaic row
-    (launch_conv3x3_wino_mosaic)."""
+    stacked (mosaic rows), or g = 16 / gcd(W', 16) maps of H' x W' side by side per
+    mosaic row, H' / W' = H / W rounded up to even (launch_conv3x3_wino_mosaic)."""
     if mos == "2d":
-        g = min(16 // math.gcd(W, 16), N)
-        return -(-N // g) * H, g * W
+        ph, pw = H + H % 2, W + W % 2
+        g = min(16 // math.gcd(pw, 16), N)
+        return -(-N // g) * ph, g * pw
     return (N * H, W) if mos else (H, W)
 
 
@@ -92,11 +99,11 @@ def _pick_mosaic(N: int, H: int, W: int, allow=True):
     1 rows at most, 2 (default) any."""
     env = os.environ.get("VOSDET_WINO_MOSAIC", "2")
     best = (False, _wino_block_use(H, W))
-    if not allow or env == "0" or N < 2 or H % 2:
+    if not allow or env == "0" or N < 2:
         return best
-    cands = [True] + (["2d"] if env == "2" and W % 2 == 0 else [])
-    for m in cands:
-        u = _wino_block_use(*_mosaic_dims(N, H, W, m))
+    cands = ([True] if H % 2 == 0 else []) + (["2d"] if env == "2" else [])
+    for m in cands:  # real pixels over block pixels (phantom rows / columns are waste)
+        u = N * H * W / float(_wino_block_area(*_mosaic_dims(N, H, W, m)))
         if u > best[1] + 1e-9:
             best = (m, u)
     return best

@@ -603,7 +603,8 @@ def conv3x3_wino_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch
     conv3x3_wino_weight.  mosaic=True runs the N images as one N*H-row image with
     per-image zero padding (vd_conv3x3_wino_seg_bias_act; H even): bit-identical,
     fewer idle block rows on small maps.  mosaic="2d" also packs maps side by side
-    (vd_conv3x3_wino_mosaic_bias_act; H, W even): no idle block columns either.
+    (vd_conv3x3_wino_mosaic_bias_act; an odd side padded by a phantom row / column
+    per map): no idle block columns either.
     Returns None for a shape the kernel does not serve."""
     if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 4 \
             or not x.is_contiguous(memory_format=torch.channels_last):
