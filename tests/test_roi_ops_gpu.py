@@ -229,6 +229,18 @@ def test_roi_align_fpn_schedules_and_edges(P):
         finally:
             del os.environ["VOSDET_ROIALIGN_VARIANT"]
         assert np.array_equal(got, ref), variant
+    # the product kernel's general form (runtime row segments / workgroup parts, the
+    # C > 256 path) vs its specialised default launch: bit-identical
+    for env in ({"VOSDET_RA_GENERAL": "1"}, {"VOSDET_RA_SEGS": "2"},
+                {"VOSDET_RA_SEGS": "4", "VOSDET_RA_PARTS": "2"}):
+        os.environ.update(env)
+        try:
+            got = ops.roi_align_fpn(pyr, scales, rt, lt, P, 2, roi_order=ops.xcd_roi_order(rt, lt),
+                                    out_layout="nhwc").cpu().numpy()
+        finally:
+            for k in env:
+                del os.environ[k]
+        assert np.array_equal(got, ref), env
     sel = rois[:, 0] == 0
     r1 = rois[sel].copy()
     d = orc.distribute(r1)
