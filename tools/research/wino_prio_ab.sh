@@ -1,3 +1,5 @@
+# NOTE: the VOSDET_WINO_PROBE=32 (s_setprio) kernel variant this compares was reverted
+# after the measurement (profiles/r03/wino_prio/README.md); kept as the record.
 # Same-box A/B: Winograd with s_setprio around the MFMA block (VOSDET_WINO_PROBE=32)
 # vs as shipped -- per-shape probe and the default bench.
 set -o pipefail
