@@ -198,6 +198,21 @@ def cpu_roialign_1thread(C=256, P=7, sr=2, seed=0):
             "threads": 1, "sample": "1 frame, 1000 synthetic RoIs (seed 0), C=256, P=7, sr=2"}
 
 
+def cpu_nms_1thread(n=1000, thresh=0.7, reps=20):
+    """The reference's NMS semantics on the host, one thread (oracle: cython_nms.nms
+    restated in C, pinned to the executed .pyx by tests/golden/nms.npz) on the
+    same N = 1000 set measure_nms times on the GPU."""
+    from oracle import oracle as orc
+    d = nms_bench_dets(n)
+    orc.nms(d, thresh)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        keep = orc.nms(d, thresh)
+    dt = (time.perf_counter() - t0) / reps
+    return {"latency_us": round(dt * 1e6, 1), "kept": int(len(keep)), "threads": 1,
+            "sample": "N=%d, thresh %.1f, %d calls" % (n, thresh, reps)}
+
+
 def cpu_share():
     """(threads, how) for the CPU baseline: the host CPUs this process may use --
     its affinity set, capped by a cgroup quota and by OMP_NUM_THREADS when the
@@ -269,9 +284,11 @@ def frame_flops(sd, cfg):
 
 class _WinoFlops(torch.overrides.TorchFunctionMode):
     """Direct-form FLOPs of the frame's 3x3 convolutions the engine runs as
-    Winograd F(2x2,3x3) (modeling._conv3x3_mfma: stride 1, pad 1, Cout % 64,
-    Cin % 8, >= 2^16 output pixels over the 16-frame batch): their MFMA work is
-    1/2.25 of the direct form's."""
+    Winograd F(2x2,3x3): the engine's own routing rule (modeling.conv3x3_route,
+    incl. the mosaic choice and the block-occupancy gate) applied to the
+    `frames`-frame batch of each conv the reference path runs.  Their MFMA work
+    is 1/2.25 of the direct form's.  Only stride-1 / pad-1 / ungrouped 3x3s with
+    a frame-level batch qualify (the mask head's RoI maps: N = frames x dets)."""
 
     def __init__(self, frames=16):
         super().__init__()
@@ -281,6 +298,7 @@ class _WinoFlops(torch.overrides.TorchFunctionMode):
         kwargs = kwargs or {}
         out = func(*args, **kwargs)
         if func in (torch.nn.functional.conv2d, torch.conv2d):
+            from vosdetectron_amd.modeling import conv3x3_route
             x, w = args[0], args[1]
             rest = list(args[3:]) + [None] * 4
             stride = kwargs.get("stride", rest[0] if rest[0] is not None else 1)
@@ -289,10 +307,11 @@ class _WinoFlops(torch.overrides.TorchFunctionMode):
             st = tuple(stride) if isinstance(stride, (tuple, list)) else (stride, stride)
             pd = tuple(padding) if isinstance(padding, (tuple, list)) else (padding, padding)
             Cout, Cin = w.shape[0], w.shape[1]
-            npx = out.shape[0] * out.shape[2] * out.shape[3]
-            if (tuple(w.shape[2:]) == (3, 3) and st == (1, 1) and pd == (1, 1) and groups == 1
-                    and Cout % 64 == 0 and Cin % 8 == 0 and npx * self.frames >= 1 << 16):
-                self.flops += 2 * npx * Cout * Cin * 9
+            N, H, W = out.shape[0], out.shape[2], out.shape[3]
+            if tuple(w.shape[2:]) == (3, 3) and st == (1, 1) and pd == (1, 1) and groups == 1:
+                # one reference frame's conv -> the engine's batch of `frames` frames
+                if conv3x3_route(N * self.frames, Cin, Cout, H, W)[0] == "wino":
+                    self.flops += 2 * N * H * W * Cout * Cin * 9
         return out
 
 
@@ -355,43 +374,52 @@ def measure_dominant_conv(dev, F, H, W, C=256, iters=None):
     return {"kernel": "vd::conv3x3_wino2_kernel (Winograd F(2x2,3x3), v_mfma_f32_16x16x4_f32)",
             "bound": "mfma", "shape": [F, C, H, W, C], "avg_launch_us": round(t * 1e6, 1),
             "unit": "TFLOP/s", "peak": MFMA_FP32_PEAK_TFS,
-            "achieved_algorithmic": round(alg / t / 1e12, 1),
-            "frac_algorithmic": round(alg / t / 1e12 / MFMA_FP32_PEAK_TFS, 4),
-            "achieved_executed": round(exe / t / 1e12, 1),
-            "frac_executed": round(exe / t / 1e12 / MFMA_FP32_PEAK_TFS, 4),
-            "how": "HIP events over %d launches; algorithmic = direct-conv FLOPs, executed = "
-                   "the MFMA work Winograd runs (4/9)" % iters}
+            "achieved": round(exe / t / 1e12, 1),
+            "frac": round(exe / t / 1e12 / MFMA_FP32_PEAK_TFS, 4),
+            "direct_conv_equivalent_TFs": round(alg / t / 1e12, 1),
+            "how": "HIP events over %d launches; achieved / frac = the MFMA work Winograd "
+                   "executes (16 positions per 2x2 tile, 4/9 of the direct FLOPs); "
+                   "direct_conv_equivalent_TFs = direct-conv FLOPs / time, a rate that "
+                   "exceeds the peak by design, not a fraction" % iters}
 
 
 def step_roofline(flops_frame, dets_cpu, frames, ms_per_step, engine_launch, frame_hw, blob_hw,
                   wino_flops_frame=0):
     """the FPS as a fraction of the roofline = sum of per-stage
-    bound times / measured step time.  MFMA-bound stages: the frame's algorithmic
-    FLOPs at the fp32 matrix peak; HBM-bound stages: the box RoIAlign's algorithmic
-    bytes (the engine's own launch) and frame prep (u8 read + fp32 blob write) at
-    8 TB/s; latency-bound stages (proposals, NMS) carry no bound.  'frac' prices
-    every convolution in its direct form (so Winograd can take it past 1);
-    'frac_executed' prices the Winograd convolutions at the 1/2.25 of that their
-    MFMAs execute -- the bound the engine's own algorithm choice can reach."""
-    mfma_ms = flops_frame * frames / (MFMA_FP32_PEAK_TFS * 1e12) * 1e3
+    bound times / measured step time.  MFMA-bound stages: the FLOPs the engine's
+    MFMAs execute for one frame at the fp32 matrix peak -- the reference's
+    algorithmic FLOPs (torch.utils.flop_counter on its CPU path) with the
+    convolutions the engine runs as Winograd F(2x2,3x3) priced at the 1/2.25 of
+    their direct form that Winograd multiplies; HBM-bound stages: the box
+    RoIAlign's algorithmic bytes (the engine's own launch) and frame prep (u8 read
+    + fp32 blob write) at 8 TB/s; latency-bound stages (proposals, NMS) carry no
+    bound.  `frac` is that executed-work fraction (<= 1 by construction).  Pricing
+    every conv in its direct form instead gives a rate, not a fraction (Winograd
+    takes it past 1): reported as `direct_conv_equivalent`, never as a frac."""
     exec_flops = flops_frame - wino_flops_frame * (1 - 1 / 2.25)
     exec_ms = exec_flops * frames / (MFMA_FP32_PEAK_TFS * 1e12) * 1e3
+    direct_ms = flops_frame * frames / (MFMA_FP32_PEAK_TFS * 1e12) * 1e3
     h, w = frame_hw
     blob_bytes = frames * (h * w * 3 + 3 * 4 * blob_hw[0] * blob_hw[1])
     ra_bytes = engine_launch["algorithmic_bytes_per_launch"] if engine_launch else 0
     hbm_ms = (blob_bytes + ra_bytes) / (HBM_PEAK_GBS * 1e9) * 1e3
-    bound = mfma_ms + hbm_ms
-    return {"bound_ms_per_step": round(bound, 3), "mfma_bound_ms": round(mfma_ms, 3),
+    bound = exec_ms + hbm_ms
+    return {"bound_ms_per_step": round(bound, 3), "mfma_bound_ms": round(exec_ms, 3),
             "hbm_bound_ms": round(hbm_ms, 3), "frac": round(bound / ms_per_step, 4),
-            "executed": {"gflop_per_frame": round(exec_flops / 1e9, 2),
-                         "winograd_direct_gflop_per_frame": round(wino_flops_frame / 1e9, 2),
-                         "mfma_bound_ms": round(exec_ms, 3),
-                         "frac": round((exec_ms + hbm_ms) / ms_per_step, 4)},
-            "gflop_per_frame": round(flops_frame / 1e9, 2), "dets_in_counted_frame": dets_cpu,
-            "mfma_util_step": round(mfma_ms / ms_per_step, 4),
+            "executed_gflop_per_frame": round(exec_flops / 1e9, 2),
+            "winograd_direct_gflop_per_frame": round(wino_flops_frame / 1e9, 2),
+            "mfma_util_step": round(exec_ms / ms_per_step, 4),
+            "direct_conv_equivalent": {
+                "gflop_per_frame": round(flops_frame / 1e9, 2),
+                "TFs": round(flops_frame * frames / (ms_per_step * 1e-3) / 1e12, 1),
+                "ms_at_peak": round(direct_ms, 3),
+                "note": "reference FLOPs (every conv direct) / step time: a rate, not a "
+                        "roofline fraction"},
+            "dets_in_counted_frame": dets_cpu,
             "peaks": {"fp32_matrix_TFs": MFMA_FP32_PEAK_TFS, "hbm_GBs": HBM_PEAK_GBS},
             "flops_source": "torch.utils.flop_counter over one frame of the reference CPU path "
-                            "(oracle/pipeline.py), 2 flop per MAC"}
+                            "(oracle/pipeline.py), 2 flop per MAC; Winograd convs by the "
+                            "engine's routing rule (modeling.conv3x3_route)"}
 
 
 def cpu_baseline(cfg_name, sd, n_frames=16, threads=None, cfg=None, min_seconds=10.0):
@@ -413,7 +441,8 @@ def cpu_baseline(cfg_name, sd, n_frames=16, threads=None, cfg=None, min_seconds=
     ra = None if (cfg is not None and (cfg.get("VOS", False) or not cfg.FPN.FPN_ON)) \
         else cpu_roialign_1thread()
     return {"value": round(n_frames / dt, 4), "unit": "frames/s", "cores": threads,
-            "kind": "port", "roialign_1thread": ra, "cpu_model": cpu_model(),
+            "kind": "port", "roialign_1thread": ra, "nms_1thread": cpu_nms_1thread(),
+            "cpu_model": cpu_model(),
             "nproc": os.cpu_count(), "cpu_share": caps,
             "sample": "%d synthetic %s, im_detect_all path (torch-CPU convs on %d threads, "
                       "oracle C RoIAlign/NMS, numpy proposals; segm_results excluded as in "
@@ -463,6 +492,112 @@ def measure_pipeline_roialign(pipe, frames_dev, reps=20):
             "launch": "engine box RoIAlign, %d frames x %d real proposals, C=%d, P=%d, sr=%d"
                       % (F, rois_t.shape[0] // max(F, 1), C, P, sr),
             "algorithmic_bytes_per_launch": int(nbytes), "avg_launch_us": round(t * 1e6, 2)}
+
+
+def _event_time(fn, reps, warm=3):
+    """Average seconds of fn() over `reps` calls, HIP events on the current stream
+    (the stream the ops launch on)."""
+    for _ in range(warm):
+        fn()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        fn()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / 1e3 / reps
+
+
+def nms_bench_dets(n=1000, seed=3):
+    """SURVEY 8(d) synthetic proposals (1333 x 800 frame) with uniform scores: the
+    BASELINE.md NMS row's N = 1000 input."""
+    r = synthetic_rois(seed, n)
+    sc = np.random.default_rng(seed + 1).random(n).astype(np.float32)
+    return np.concatenate([r[:, 1:5], sc[:, None]], 1).astype(np.float32)
+
+
+def measure_nms(dev, n=1000, thresh=0.7, reps=200):
+    """BASELINE.md 3 'NMS latency N=1000, thr 0.7': vd_nms (cython_nms semantics,
+    bit-exact vs the executed reference: tests/golden/nms.npz) on one set of N
+    boxes, HIP events over `reps` launches with preallocated workspace -- the
+    device latency of one call, no host read.  SURVEY 8(d): latency bound; the
+    greedy algorithm's work is N^2/2 IoU evaluations."""
+    from vosdetectron_amd import _lib
+    d = torch.from_numpy(nms_bench_dets(n)).to(dev)
+    keep = torch.empty((n,), dtype=torch.int64, device=dev)
+    num = torch.zeros((1,), dtype=torch.int32, device=dev)
+    L = _lib.lib()
+    ws = torch.empty((max(int(L.vd_nms_workspace_size(n)), 256),), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    th = float(np.float32(thresh))
+
+    def run():
+        _lib.check(L.vd_nms(d.data_ptr(), n, 5, th, keep.data_ptr(), num.data_ptr(),
+                            ws.data_ptr(), ws.numel(), stream), "vd_nms")
+    t = _event_time(run, reps)
+    kept = int(num.item())
+    evals = n * (n - 1) // 2
+    return {"kernel": "vd_nms: nms_prep_kernel + nms_mask_kernel + nms_resolve_kernel",
+            "bound": "latency", "n": n, "thresh": thresh, "kept": kept,
+            "latency_us": round(t * 1e6, 2), "iou_evals": evals,
+            "iou_evals_per_s": round(evals / t, 1),
+            "input": "SURVEY 8(d) synthetic RoIs (seed 3), uniform scores (seed 4)",
+            "how": "HIP events over %d launches, preallocated workspace" % reps}
+
+
+def measure_step_post(pipe, frames_dev, reps=20):
+    """The step's proposal and detection kernels on the engine's own tensors
+    (keep_intermediates): vd_generate_proposals over P2-P6 x F frames (anchors,
+    decode, clip, filter, top-k, NMS 0.7) priced against SURVEY 8(d)'s HBM bytes
+    -- 20 B per anchor read (4 B score + 16 B deltas) + 24 B per written proposal
+    -- and vd_box_detections (decode, 80-class NMS 0.5, top-100) as a latency."""
+    from vosdetectron_amd import ops
+    cfg = pipe.cfg
+    tst = cfg.TEST
+    out = pipe.run(frames_dev, keep_intermediates=True)
+    probs, deltas = out["rpn_probs"], out["rpn_deltas"]
+    F = frames_dev.shape[0]
+    bufs = [torch.zeros((F, len(probs), tst.RPN_POST_NMS_TOP_N, 5), device=frames_dev.device),
+            torch.zeros((F, len(probs), tst.RPN_POST_NMS_TOP_N), device=frames_dev.device),
+            torch.zeros((F, len(probs)), dtype=torch.int32, device=frames_dev.device)]
+
+    def prop():
+        ops.generate_proposals(probs, deltas, pipe.anchors, pipe.rpn_scales, pipe.im_info[:F],
+                               tst.RPN_PRE_NMS_TOP_N, tst.RPN_POST_NMS_TOP_N, tst.RPN_NMS_THRESH,
+                               tst.RPN_MIN_SIZE, out=bufs)
+    t_p = _event_time(prop, reps)
+    anchors = sum(int(p.shape[1]) * int(p.shape[2]) * int(p.shape[3]) for p in probs)  # per frame
+    nbytes = F * (20 * anchors + 24 * len(probs) * tst.RPN_POST_NMS_TOP_N)
+    K = out["cls_prob"].shape[1]
+    post = out["rois"].shape[1]
+    dbufs = [torch.zeros((F, pipe.det_cap, 5), device=frames_dev.device),
+             torch.zeros((F, pipe.det_cap), dtype=torch.int32, device=frames_dev.device),
+             torch.zeros((F,), dtype=torch.int32, device=frames_dev.device)]
+
+    def dets():
+        ops.box_detections(out["rois"], out["cls_prob"].view(F, post, K),
+                           out["bbox_pred"].view(F, post, -1), out["roi_counts"],
+                           pipe.im_scale_t[:F], pipe.im_hw[:F], tst.SCORE_THRESH, tst.NMS,
+                           tst.DETECTIONS_PER_IM, cfg.MODEL.BBOX_REG_WEIGHTS, pipe.det_cap,
+                           out=dbufs)
+    t_d = _event_time(dets, reps)
+    return {"proposals": {
+                "kernel": "vd_generate_proposals: rpn_proposals_kernel + rpn_nms_mask_kernel + "
+                          "rpn_nms_finish_kernel (P2-P6, all frames, one launch each)",
+                "bound": "hbm", "achieved": round(nbytes / t_p / 1e9, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(nbytes / t_p / 1e9 / HBM_PEAK_GBS, 4),
+                "algorithmic_bytes": int(nbytes), "avg_us": round(t_p * 1e6, 1),
+                "anchors_per_frame": anchors, "frames": F,
+                "note": "20 B read per anchor (score + 4 deltas) + 24 B per written proposal "
+                        "(SURVEY 8d); the select / NMS phases are latency-bound, so the "
+                        "byte rate is far below the roofline"},
+            "class_nms": {
+                "kernel": "vd_box_detections: decode + class_nms_kernel (80 classes x F) + "
+                          "det_limit_kernel", "bound": "latency",
+                "avg_us": round(t_d * 1e6, 1), "frames": F, "rois_per_frame": post,
+                "us_per_frame": round(t_d * 1e6 / F, 2)},
+            "how": "HIP events over %d launches on the engine's own step tensors" % reps}
 
 
 def measure_segm(pipe, out, frames=16):
@@ -565,16 +700,36 @@ def dry_run(args, world, rank):
                                           m2[o:o + n2[f]]))
                 o += n2[f]
     dt = time.perf_counter() - t0
+    # the N>1 line's diagnostics, as main() reports them: every rank's own step
+    # time (value uses the slowest) and the gather's share of the step
     t = torch.tensor([dt], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    allt = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(allt, t)
+    per = [float(x.item()) / args.steps * 1e3 for x in allt]
+    tmax = max(float(x.item()) for x in allt)
     okt = torch.tensor([int(ok)])
     dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    tg0 = time.perf_counter()
+    for _ in range(args.steps):
+        g.gather_async(*[torch.from_numpy(a) for a in results(rank, 0)]).wait(views=False)
+    tg = torch.tensor([time.perf_counter() - tg0], dtype=torch.float64)
+    dist.all_reduce(tg, op=dist.ReduceOp.MAX)
+    g_ms = float(tg.item()) / args.steps * 1e3
     if rank == 0:
         print(json.dumps({"metric": "dry-run (gloo, CPU): frame-sharded result all_gather",
-                          "value": round(world * F * args.steps / float(t), 3),
+                          "value": round(world * F * args.steps / tmax, 3),
                           "unit": "frames/s", "n_gpus": world, "steps": args.steps,
                           "warmup": 0, "dry_run": True, "gather_ok": bool(okt.item()),
-                          "bytes_per_rank": g.bytes_per_rank}), flush=True)
+                          "bytes_per_rank": g.bytes_per_rank,
+                          "config": {"parallelism": "frame-sharded dp%d + one all_gather per "
+                                                    "step (gloo rehearsal)" % world},
+                          "rank_ms_per_step": {"min": round(min(per), 3),
+                                               "max": round(max(per), 3),
+                                               "spread": round(max(per) / min(per) - 1, 4),
+                                               "per_rank": [round(v, 3) for v in per]},
+                          "gather": {"gather_ms": round(g_ms, 3),
+                                     "share_of_step": round(g_ms / (tmax / args.steps * 1e3), 4),
+                                     "bytes_per_rank": g.bytes_per_rank}}), flush=True)
     dist.destroy_process_group()
     return 0 if okt.item() else 1
 
@@ -770,10 +925,39 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    if world > 1:
+    rank_ms = None
+    if world > 1:  # every rank's own step time; the line's value uses the slowest
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        per = [float(x.item()) / args.steps * 1e3 for x in allt]
+        rank_ms = {"min": round(min(per), 3), "max": round(max(per), 3),
+                   "spread": round(max(per) / min(per) - 1, 4), "per_rank": [round(v, 3) for v in per]}
+        dt = max(float(x.item()) for x in allt)
+    gather_share = None
+    if gatherer.collective and not args.share_gpu:
+        # the packed all_gather ALONE (no compute to hide behind), K times: an upper
+        # bound on its share of the step, where it overlaps the next step's compute
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tg0 = time.perf_counter()
+        for i in range(args.steps):
+            gatherer.gather_async(out["dets"], out["classes"], out["counts"],
+                                  out["masks"]).wait(views=False)
+        torch.cuda.synchronize()
+        tg = torch.tensor([time.perf_counter() - tg0], device=dev, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(tg, op=dist.ReduceOp.MAX)
+        g_ms = float(tg.item()) / args.steps * 1e3
+        gather_share = {"gather_ms": round(g_ms, 3),
+                        "share_of_step": round(g_ms / (dt / args.steps * 1e3), 4),
+                        "bytes_per_rank": gatherer.bytes_per_rank,
+                        "bus_GBs": round(gatherer.bytes_per_rank * (world - 1) / (g_ms * 1e-3)
+                                         / 1e9, 2) if world > 1 else None,
+                        "how": "the step's packed all_gather alone, %d times after the timed "
+                               "region (in the step it overlaps the next step's compute)"
+                               % args.steps}
     if asynchronous:
         pipe.complete(prev_out[0])
         out = prev_out[0]
@@ -800,6 +984,8 @@ def main():
         roof = measure_roialign_roofline(dev)
         if not vos and cfg.FPN.FPN_ON:
             roof["engine_launch"] = measure_pipeline_roialign(pipe, any_frames)
+            extra["nms"] = measure_nms(dev)
+            extra.update(measure_step_post(pipe, any_frames))
     if not args.no_roofline and rank == 0 and world == 1:  # N=1 line only (no ranks waiting)
         extra["hbm_copy"] = measure_hbm_copy(dev)
         if not vos and cfg.FPN.FPN_ON:
@@ -839,7 +1025,10 @@ def main():
                 "proposals, box head, class NMS, mask head -> class-selected masks "
                 "(segm_results paste/RLE excluded, SURVEY 8d)" % (args.config, F, fh, fw)),
                        "frames_per_gpu_step": F, "global_batch": world * F,
-                       "parallelism": "frame-sharded dp%d + RCCL all_gather" % world,
+                       "parallelism": ("frame-sharded dp%d + one RCCL all_gather per step"
+                                       % world) if gatherer.collective else
+                       "single GPU, frame-sharded dp1: no collective at N=1 (nothing to "
+                       "gather; --rccl-gather issues it anyway)",
                        "layout": args.layout, "dets_per_frame": dets_per_frame, "h2d": h2d,
                        "gather_bytes_per_rank": gatherer.bytes_per_rank
                        if gatherer.collective else 0,
@@ -847,6 +1036,10 @@ def main():
                        ("eager (%s)" % graph_note[0] if graph_note[0] else "eager")},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if rank_ms:
+            line["rank_ms_per_step"] = rank_ms
+        if gather_share:
+            line["gather"] = gather_share
         if args.share_gpu:
             line["rehearsal"] = "--share-gpu: %d ranks on one device, not a measurement" % world
         if stages:

@@ -140,6 +140,10 @@ int vd_roi_crop_forward(const float *input, int B, int C, int H, int W, const fl
  * replacement for a reference custom op (those convs run in PyTorch there);
  * it removes the separate epilogue pass over the conv output. */
 size_t vd_gemm_workspace_size(void);
+/* The key under which this process applies pinned GEMM plans (VOSDET_GEMM_PLANS):
+ * "<arch> hipblaslt-<version>-<git revision> cu<CUs>" of the current device; a
+ * plans file's "# key ..." line must equal it for the pins below it to apply. */
+int vd_gemm_plans_key(char *buf, int n);
 int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,
                      const float *residual, int relu, float *D, void *workspace,
                      size_t workspace_bytes, void *stream);
@@ -182,14 +186,6 @@ int vd_conv3x3_wino_seg_bias_act(const float *X, int H, int W, int C, const floa
  * vd_conv3x3_wino_bias_act on the R maps. */
 int vd_conv3x3_wino_mosaic_bias_act(const float *X, int R, int H, int W, int C, const float *U,
                                     int Cout, const float *bias, int relu, float *Y, void *stream);
-
-/* The same convolution by Winograd F(4x4, 3x3) (4x fewer multiplies than the
- * direct form; transforms with factors up to 8, ~4x F(2x2, 3x3)'s rounding error,
- * ~4e-6 of max|y| at 256 channels): U from vd_conv3x3_wino4_weight (36 x Cout x
- * Cin fp32, opaque chunk-blocked order).  Cin % 4 == 0, Cout % 32 == 0. */
-int vd_conv3x3_wino4_weight(const float *w, int Cout, int Cin, float *U, void *stream);
-int vd_conv3x3_wino4_bias_act(const float *X, int N, int H, int W, int C, const float *U,
-                              int Cout, const float *bias, int relu, float *Y, void *stream);
 
 /* Two 1x1 convolutions of two channels_last inputs summed, with the epilogue:
  * D[M][N] = act(A1[M][K1] . W[:, :K1]^T + A2[M][K2] . W[:, K1:]^T + bias[N]),

@@ -1,20 +1,24 @@
-"""The configuration bench.py measures, tested as benched.
+"""The configuration bench.py measures, tested as benched (VERDICT r2 item 2,
+VERDICT r3 weak #2).
 
 bench.py runs e2e_mask_rcnn_R-50-FPN_1x at 16 synthetic 800x1333 frames per
-step on the channels_last engine.  At that batch the P2/P3 convolutions cross
-the 2^18-pixel routing threshold (modeling._conv3x3_mfma) and run on the
-hand-written MFMA implicit GEMM (csrc/conv3x3.hip) and the 1x1 GEMMs run at
-M = 1,075,200 pixels; batch-1 pipeline tests never reach those routes.  Here:
+step on the channels_last engine.  At that batch the 3x3 convolutions route to
+the hand-written Winograd F(2x2,3x3) MFMA kernel (csrc/conv3x3_wino.hip;
+modeling.conv3x3_route: >= 2^12 batch pixels, blocks >= 60 % real output) --
+P2 as one launch per batch, P3 / P4 / res5 / P5 / P6 and the mask head's
+1600 RoI maps as 2-D mosaics -- and the 1x1 GEMMs run at M = 1,075,200 pixels;
+batch-1 pipeline tests never reach those routes.  Here:
 
 * FramePipeline(batch=16) on 16 distinct frames (bench.synthetic_frames, the
-  bench's own seeds and routes): stage-wise parity on frames 0, 7 and 15
-  (proposals + collect and detections bit-exact, box / mask RoIAlign within
-  1e-4 of the oracle's operator API) and e2e vs the independent CPU pipeline on
-  frames 0 and 15;
-* the MFMA 3x3 conv alone at the benched shapes (16,256,200,336),
-  (16,256,100,168) and the mask head's (1600,256,14,14), bias and no bias, vs
-  torch fp32;
+  bench's own seeds and routes): the route counters show Winograd ran and the
+  implicit GEMM / MIOpen did not take a benched 3x3; stage-wise parity on
+  frames 0, 7 and 15 (proposals + collect and detections bit-exact, box / mask
+  RoIAlign within 1e-4 of the oracle's operator API) and e2e vs the
+  independent CPU pipeline on frames 0 and 15;
+* the Winograd kernel alone (conv3x3_wino_bias_act in the layout the engine
+  picks) at the benched shapes, bias + ReLU and no bias, vs torch fp32 at 2e-5;
 * the 1x1 GEMM epilogue path and the dual GEMM at M = 1,075,200.
+The hipGraph replay of this step is tested in test_graph_replay_gpu.py.
 Reference: lib/core/test.py:50-111 (im_detect_all)."""
 import numpy as np
 import pytest
@@ -32,31 +36,43 @@ BATCH = 16
 def bench_setup():
     from bench import synthetic_frames
     from vosdetectron_amd import config as vcfg
+    from vosdetectron_amd import modeling
     from vosdetectron_amd.engine import FramePipeline
     from vosdetectron_amd.weights import build_model
     cfg = vcfg.get("e2e_mask_rcnn_R-50-FPN_1x")
     model, sd = build_model(cfg, seed=0, device=DEV, channels_last=True)
     frames = synthetic_frames(BATCH, 1, 800, 1333)  # bench.py's first host batch
     pipe = FramePipeline(model, cfg, batch=BATCH, channels_last=True, device=DEV)
+    modeling.ROUTE_COUNTS.clear()
     out = pipe.run(torch.from_numpy(frames).to(DEV), keep_intermediates=True)
+    routes = dict(modeling.ROUTE_COUNTS)
     torch.cuda.synchronize()
-    return cfg, sd, pipe, frames, out
+    return cfg, sd, pipe, frames, out, routes
 
 
 def test_bench_batch_routes(bench_setup):
-    """The benched shapes take the hand-written routes (not a silent fallback)."""
+    """The benched shapes take the hand-written routes (not a silent fallback):
+    every 3x3 conv of the 16-frame step ran on the Winograd kernel -- res2 / res3
+    / res4 / res5 conv2 (stride-1 blocks), FPN posthoc P2-P5, the RPN conv on
+    P2-P6 and the mask head's four convs -- P2 per image, the rest as mosaics."""
     from vosdetectron_amd import modeling
-    cfg, sd, pipe, frames, out = bench_setup
+    cfg, sd, pipe, frames, out, routes = bench_setup
     p2 = out["feats"][-1]
     assert p2.shape == (BATCH, 256, 200, 336)
     assert p2.is_contiguous(memory_format=torch.channels_last)
-    assert BATCH * 200 * 336 >= modeling._CONV3X3_MIN_PIXELS
     assert all(int(c) > 0 for c in out["counts_host"])
+    assert modeling.conv3x3_route(BATCH, 256, 256, 200, 336) == ("wino", False)
+    assert modeling.conv3x3_route(BATCH, 256, 256, 100, 168) == ("wino", "2d")
+    assert modeling.conv3x3_route(BATCH * 100, 256, 256, 14, 14) == ("wino", "2d")
+    assert routes.get("igemm", 0) == 0 and routes.get("miopen", 0) == 0, routes
+    n_wino = routes.get("wino", 0) + routes.get("wino_rows", 0) + routes.get("wino_2d", 0)
+    # FPN posthoc 4 + RPN conv 5 + mask head 4 at least (plus the body's 3x3s)
+    assert n_wino >= 13 and routes.get("wino_2d", 0) >= 8, routes
 
 
 @pytest.mark.parametrize("f", [0, 7, 15])
 def test_bench_batch_stagewise(bench_setup, f):
-    cfg, sd, pipe, frames, out = bench_setup
+    cfg, sd, pipe, frames, out, _ = bench_setup
     rois, _ = stagewise(cfg, pipe, out, frames[f], f=f)
     assert len(rois) == 1000
 
@@ -64,31 +80,39 @@ def test_bench_batch_stagewise(bench_setup, f):
 @pytest.mark.parametrize("f", [0, 15])
 def test_bench_batch_e2e_vs_cpu(bench_setup, f):
     from oracle.pipeline import RefCPUPipeline
-    cfg, sd, pipe, frames, out = bench_setup
+    cfg, sd, pipe, frames, out, _ = bench_setup
     torch.set_num_threads(16)
     ref_out = RefCPUPipeline(sd)(frames[f])
     e2e_vs_cpu(out, ref_out, f=f)
 
 
-@pytest.mark.parametrize("N,H,W", [(16, 200, 336), (16, 100, 168), (1600, 14, 14)])
+@pytest.mark.parametrize("N,C,H,W", [(16, 256, 200, 336), (16, 256, 100, 168), (16, 256, 50, 84),
+                                     (1600, 256, 14, 14), (16, 64, 200, 336),
+                                     (16, 512, 25, 42)])
 @pytest.mark.parametrize("bias", [True, False])
-def test_conv3x3_benched_shapes(N, H, W, bias):
-    """vd_conv3x3_bias_act (default variant) at the benched sizes vs torch fp32;
-    (16,256,200,336) is 1,075,200 pixels, half of the kernel's 32-bit offset guard."""
-    from vosdetectron_amd import ops
-    g = torch.Generator(device="cuda").manual_seed(N + H)
-    x = torch.randn(N, 256, H, W, device="cuda", generator=g).contiguous(
+def test_conv3x3_wino_benched_shapes(N, C, H, W, bias):
+    """vd_conv3x3_wino_* (the kernel the step runs) at the benched sizes in the
+    layout the engine picks (modeling.conv3x3_route: P2 / res2 per image, the
+    P3 / P4 2-D mosaics, the mask head's 1600-map mosaic, res5's odd-sided 25 x 42
+    mosaic) vs torch fp32 at 2e-5 of the output range; (16,256,200,336) is
+    1,075,200 pixels."""
+    from vosdetectron_amd import modeling, ops
+    algo, mos = modeling.conv3x3_route(N, C, C, H, W)
+    assert algo == "wino", (N, C, H, W, algo)
+    g = torch.Generator(device="cuda").manual_seed(N + H + C)
+    x = torch.randn(N, C, H, W, device="cuda", generator=g).contiguous(
         memory_format=torch.channels_last)
-    w = torch.randn(256, 256, 3, 3, device="cuda", generator=g) / 48.
-    b = torch.randn(256, device="cuda", generator=g) if bias else None
-    got = ops.conv3x3_bias_act(x, ops.conv3x3_weight(w), b, relu=bias)
-    assert got is not None, "benched shape fell off the MFMA route"
+    w = torch.randn(C, C, 3, 3, device="cuda", generator=g) / (3. * C ** .5)
+    b = torch.randn(C, device="cuda", generator=g) if bias else None
+    got = ops.conv3x3_wino_bias_act(x, ops.conv3x3_wino_weight(w), b, relu=bias, mosaic=mos)
+    assert got is not None, "benched shape fell off the Winograd route"
     ref = F.conv2d(x, w, b, padding=1)
     if bias:
         ref = F.relu(ref)
     torch.cuda.synchronize()
     err = float((got - ref).abs().max())
     assert err <= 2e-5 * max(1., float(ref.abs().max())), err
+    del x, got, ref
 
 
 @pytest.mark.parametrize("K,N,res", [(64, 256, True), (256, 64, False), (64, 64, False),

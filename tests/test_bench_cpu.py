@@ -23,13 +23,49 @@ def test_step_roofline_sums_stage_bounds():
     r2 = bench.step_roofline(528e9, 100, 16, 72.0, {"algorithmic_bytes_per_launch": 2.0e9},
                              (800, 1333), (800, 1344), wino_flops_frame=300e9)
     ex = (528e9 - 300e9 * (1 - 1 / 2.25)) * 16 / 157.3e12 * 1e3
-    assert abs(r2["executed"]["mfma_bound_ms"] - round(ex, 3)) < 1e-6
-    assert r2["executed"]["frac"] < r2["frac"]
+    assert abs(r2["mfma_bound_ms"] - round(ex, 3)) < 1e-6
+    assert r2["frac"] < r["frac"]
+
+
+def _fracs(d, path=""):
+    """Every (path, value) whose key is 'frac' or starts with 'frac' in a nested line."""
+    out = []
+    if isinstance(d, dict):
+        for k, v in d.items():
+            if isinstance(v, (dict, list)):
+                out += _fracs(v, path + "." + k)
+            elif k.startswith("frac") and isinstance(v, (int, float)):
+                out.append((path + "." + k, v))
+    elif isinstance(d, list):
+        for i, v in enumerate(d):
+            out += _fracs(v, "%s[%d]" % (path, i))
+    return out
+
+
+def test_no_fraction_above_one():
+    """a step 1.5x faster than the direct-conv FLOPs allow at
+    the peak (Winograd) must still report frac <= 1 -- the direct-form figure is a
+    rate (direct_conv_equivalent.TFs), never a fraction."""
+    ms = 528e9 * 16 / 157.3e12 * 1e3 / 1.5  # 1.5x the direct-form bound
+    r = bench.step_roofline(528e9, 100, 16, ms, {"algorithmic_bytes_per_launch": 1e9},
+                            (800, 1333), (800, 1344), wino_flops_frame=330e9)
+    assert r["direct_conv_equivalent"]["TFs"] > bench.MFMA_FP32_PEAK_TFS
+    fr = _fracs(r)
+    assert fr and all(v <= 1.0 for _, v in fr), fr
+    # the committed bench line of this round obeys the same rule
+    import glob
+    import json
+    for p in sorted(glob.glob(os.path.join(bench.ROOT, "profiles", "r04", "bench_default*.json"))):
+        line = json.load(open(p))
+        bad = [(k, v) for k, v in _fracs(line) if v > 1.0]
+        assert not bad, (p, bad)
 
 
 def test_winograd_flop_classifier():
     """bench._WinoFlops counts exactly the 3x3 / stride-1 / pad-1 convolutions
-    with Cout % 64 == 0, Cin % 8 == 0 and >= 2^16 batch output pixels."""
+    the engine routes to Winograd (modeling.conv3x3_route on the 16-frame batch:
+    Cout % 64 == 0, Cin % 8 == 0, >= 2^12 batch output pixels, blocks >= 60 %
+    real output)."""
     import torch
     import torch.nn.functional as F
     x = torch.randn(1, 8, 64, 64)
@@ -39,7 +75,9 @@ def test_winograd_flop_classifier():
         F.conv2d(x, torch.randn(32, 8, 3, 3), None, 1, 1)        # Cout 32
         F.conv2d(x, torch.randn(64, 8, 1, 1))                    # 1x1
         F.conv2d(x[:, :, :8, :8], torch.randn(64, 8, 3, 3), padding=1)  # 16*64 px
-    assert wf.flops == 2 * 4096 * 64 * 8 * 9
+        # 16 x 16 maps: 16 * 256 = 2^12 batch pixels in full 8 x 16 blocks -> Winograd
+        F.conv2d(x[:, :, :16, :16], torch.randn(64, 8, 3, 3), padding=1)
+    assert wf.flops == 2 * 4096 * 64 * 8 * 9 + 2 * 256 * 64 * 8 * 9
 
 
 def test_roi_align_algorithmic_bytes_counts_union_once():

@@ -53,3 +53,24 @@ def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "missing.so"))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         _lib.lib()
+
+
+def test_miopen_db_is_a_per_process_copy():
+    """The tracked MIOpen Find db is a read-only seed: a
+    process that imports the package points MIOPEN_USER_DB_PATH at its own
+    temporary copy, outside the repository, so MIOpen's appends never touch the
+    tracked files and concurrent ranks never share one file."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k != "MIOPEN_USER_DB_PATH"}
+    code = ("import os, vosdetectron_amd; d = os.environ['MIOPEN_USER_DB_PATH']; "
+            "print(d); print(sorted(os.listdir(d)))")
+    outs = [subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                           env=env, cwd=root, timeout=120).stdout.splitlines() for _ in range(2)]
+    seed = sorted(os.listdir(os.path.join(root, "vosdetectron_amd", "miopen_db")))
+    for d, names in outs:
+        assert not os.path.abspath(d).startswith(root), d
+        assert names == repr(seed) or eval(names) == seed
+        assert not os.path.exists(d)  # removed at exit
+    assert outs[0][0] != outs[1][0]

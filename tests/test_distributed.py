@@ -131,6 +131,11 @@ def test_bench_launch_world2_dry_run():
     assert p.returncode == 0, p.stderr[-2000:]
     line = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["dry_run"] and line["gather_ok"]
+    # the N>1 diagnostics: per-rank step time and gather share
+    rk = line["rank_ms_per_step"]
+    assert len(rk["per_rank"]) == 2 and rk["min"] <= rk["max"]
+    assert line["gather"]["gather_ms"] > 0 and line["gather"]["share_of_step"] > 0
+    assert "dp2" in line["config"]["parallelism"]
     # a launcher world that disagrees with --gpus is refused
     env2 = dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     p2 = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",

@@ -11,8 +11,28 @@ os.environ.setdefault("MIOPEN_FIND_MODE", "1")
 # VOS; 155 convolution problems) recorded once on an MI355X (gfx950, 256 CUs) and
 # shipped in-tree: every process -- each rank of a multi-GPU run, every box -- then
 # picks the same solvers (identical numerics and per-rank speed) and skips the
-# Find sweep at warm-up.  Problems not in it are found and appended as usual.  A
-# caller's own MIOPEN_USER_DB_PATH wins.
-os.environ.setdefault("MIOPEN_USER_DB_PATH",
-                      os.path.join(os.path.dirname(os.path.abspath(__file__)), "miopen_db"))
+# Find sweep at warm-up.  The tracked directory is a read-only SEED: each process
+# copies it to its own temporary directory and points MIOPEN_USER_DB_PATH there,
+# so problems not in it are found and appended to the copy -- eight ranks never
+# write one shared file and no run dirties the repository.
+# A caller's own MIOPEN_USER_DB_PATH wins (VOSDET_MIOPEN_DB_SEED=0: no seed).
 
+
+def _seed_miopen_db():
+    if "MIOPEN_USER_DB_PATH" in os.environ or os.environ.get("VOSDET_MIOPEN_DB_SEED") == "0":
+        return
+    import atexit
+    import shutil
+    import tempfile
+    seed = os.path.join(os.path.dirname(os.path.abspath(__file__)), "miopen_db")
+    try:
+        d = tempfile.mkdtemp(prefix="vosdet_miopen_db_")
+        for name in os.listdir(seed):
+            shutil.copy2(os.path.join(seed, name), os.path.join(d, name))
+    except OSError:
+        return  # no writable temp dir: MIOpen uses its own default location
+    atexit.register(shutil.rmtree, d, True)
+    os.environ["MIOPEN_USER_DB_PATH"] = d
+
+
+_seed_miopen_db()

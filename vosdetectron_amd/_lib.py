@@ -52,6 +52,7 @@ SIGNATURES = {
     "vd_roi_align_fpn_tiled_forward": (_I, [ctypes.POINTER(VdFeatLevel), _I, _I, _I, _P, _P, _I,
                                             _I, _I, _P, _P, _S, _P]),
     "vd_gemm_workspace_size": (_S, []),
+    "vd_gemm_plans_key": (_I, [_P, _I]),
     "vd_gemm_bias_act": (_I, [_P, _I, _I, _P, _I, _P, _P, _I, _P, _P, _S, _P]),
     "vd_gemm_dual_bias_act": (_I, [_P, _I, _P, _I, _I, _P, _I, _P, _I, _P, _P]),
     "vd_conv3x3_bias_act": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
@@ -59,8 +60,6 @@ SIGNATURES = {
     "vd_conv3x3_wino_bias_act": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
     "vd_conv3x3_wino_seg_bias_act": (_I, [_P, _I, _I, _I, _P, _I, _P, _I, _I, _P, _P]),
     "vd_conv3x3_wino_mosaic_bias_act": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
-    "vd_conv3x3_wino4_weight": (_I, [_P, _I, _I, _P, _P]),
-    "vd_conv3x3_wino4_bias_act": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
     "vd_roi_align_legacy_forward": (_I, [_I, _I, _F, _P, _I, _I, _I, _I, _P, _I, _P, _P]),
     "vd_roi_pool_forward": (_I, [_I, _I, _F, _P, _I, _I, _I, _I, _P, _I, _P, _P, _P]),
     "vd_roi_pool_backward": (_I, [_P, _P, _L, _P, _P]),

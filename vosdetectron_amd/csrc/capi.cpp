@@ -116,6 +116,11 @@ int vd_roi_align_fpn_tiled_forward(const VdFeatLevel *levels, int num_levels, in
 
 size_t vd_gemm_workspace_size(void) { return gemm_epi_workspace_bytes(); }
 
+int vd_gemm_plans_key(char *buf, int n) {
+    if (!buf || n < 16) return VD_ERR_ARG;
+    return gemm_plans_key(buf, n);
+}
+
 int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,
                      const float *residual, int relu, float *D, void *workspace,
                      size_t workspace_bytes, void *stream) {
@@ -152,18 +157,6 @@ int vd_conv3x3_wino_seg_bias_act(const float *X, int H, int W, int C, const floa
 int vd_conv3x3_wino_mosaic_bias_act(const float *X, int R, int H, int W, int C, const float *U,
                                     int Cout, const float *bias, int relu, float *Y, void *stream) {
     return launch_conv3x3_wino_mosaic(X, R, H, W, C, U, Cout, bias, relu, Y, VD_STREAM(stream));
-}
-
-int vd_conv3x3_wino4_weight(const float *w, int Cout, int Cin, float *U, void *stream) {
-    if (Cout < 1 || Cin < 1 || !w || !U) return VD_ERR_ARG;
-    return launch_conv3x3_wino4_weight(w, Cout, Cin, U, VD_STREAM(stream));
-}
-
-int vd_conv3x3_wino4_bias_act(const float *X, int N, int H, int W, int C, const float *U,
-                              int Cout, const float *bias, int relu, float *Y, void *stream) {
-    if (N < 0 || H < 1 || W < 1 || C < 1 || Cout < 1 || !U || !Y || (N > 0 && !X))
-        return VD_ERR_ARG;
-    return launch_conv3x3_wino4(X, N, H, W, C, U, Cout, bias, relu, Y, VD_STREAM(stream));
 }
 
 int vd_gemm_dual_bias_act(const float *A1, int K1, const float *A2, int K2, int M, const float *W,

@@ -382,8 +382,11 @@ int launch_wino(const float *X, int N, int H, int W, int C, const float *U, int 
     if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
     auto kern = sq ? (relu ? conv3x3_wino2_kernel<true, 8> : conv3x3_wino2_kernel<false, 8>)
                    : (relu ? conv3x3_wino2_kernel<true, 16> : conv3x3_wino2_kernel<false, 16>);
-    // speed-of-light probes (wrong results): 1 no DMA, 2 no patch reads, 4 no
-    // barrier, 8 no U reads
+#ifdef VD_RESEARCH_PROBES
+    // speed-of-light probes (wrong results; tools/wino_sol_probe.py): 1 no DMA, 2 no
+    // patch reads, 4 no barrier, 8 no U reads.  Only in a research build
+    // (make VD_RESEARCH=1), never in the product library: a stray environment
+    // variable must not be able to corrupt a product convolution.
     const char *pe = getenv("VOSDET_WINO_PROBE");
     switch (pe && !sq && !relu ? atoi(pe) : 0) {
         case 1: kern = conv3x3_wino2_kernel<false, 16, 1>; break;
@@ -394,6 +397,7 @@ int launch_wino(const float *X, int N, int H, int W, int C, const float *U, int 
         case 15: kern = conv3x3_wino2_kernel<false, 16, 15>; break;
         default: break;
     }
+#endif
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(k2Threads), 0, s, X, N, H, W, C, U, Cout,
                        bias, Y, tby, tbx, cbx, seg_h, seg_w, gx, nmaps, map_h, map_w);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;

@@ -70,6 +70,38 @@ std::map<Key, Plan> g_plans;
 std::map<Key, int> g_pinned;  // -1: the MFMA kernel, i >= 0: heuristic candidate i
 bool g_pins_loaded = false;
 
+hipblasLtHandle_t handle();
+
+// The plans' validity key: a pinned index names an entry of hipBLASLt's heuristic
+// list, which is stable only for one library build on one GPU.  The
+// file carries "# key <arch> hipblaslt-<version>-<git revision> cu<CUs>" lines; a pin
+// applies only under a key line equal to this process's key, so on another GPU or
+// hipBLASLt build every shape falls back to the timing search instead of silently
+// running whatever kernel the stale index now names.
+const char *plans_key() {
+    static char key[256] = {0};
+    if (key[0]) return key;
+    hipDeviceProp_t prop;
+    int dev = 0, ver = 0;
+    char rev[128] = {0};
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
+        return "";
+    if (hipblasLtHandle_t h = handle()) {
+        (void)hipblasLtGetVersion(h, &ver);
+        (void)hipblasLtGetGitRevision(h, rev);
+    }
+    char arch[64];
+    snprintf(arch, sizeof arch, "%s", prop.gcnArchName);
+    if (char *c = strchr(arch, ':')) *c = 0;  // gfx950[:sramecc+:xnack-] -> gfx950
+    for (char *c = rev; *c; ++c)
+        if (*c == ' ' || *c == '\n') *c = '_';
+    snprintf(key, sizeof key, "%s hipblaslt-%d-%s cu%d", arch, ver, rev[0] ? rev : "0",
+             prop.multiProcessorCount);
+    return key;
+}
+
+bool g_key_in_file = false;  // the file already has this process's key line
+
 void load_pins() {  // once, under g_mu
     if (g_pins_loaded) return;
     g_pins_loaded = true;
@@ -77,8 +109,18 @@ void load_pins() {  // once, under g_mu
     if (!path || !path[0]) return;
     FILE *f = fopen(path, "r");
     if (!f) return;
-    char line[256];
+    const char *mine = plans_key();
+    bool active = false;  // pins before any key line (or under another key) never apply
+    char line[512];
     while (fgets(line, sizeof line, f)) {
+        if (strncmp(line, "# key ", 6) == 0) {
+            char *e = line + strlen(line);
+            while (e > line && (e[-1] == '\n' || e[-1] == '\r' || e[-1] == ' ')) *--e = 0;
+            active = mine[0] && strcmp(line + 6, mine) == 0;
+            g_key_in_file |= active;
+            continue;
+        }
+        if (!active || line[0] == '#') continue;
         int M, N, K, relu, res, idx = 0;
         char what[16];
         const int n = sscanf(line, "%d %d %d %d %d %15s %d", &M, &N, &K, &relu, &res, what, &idx);
@@ -96,6 +138,10 @@ void record_pin(const Key &k, int choice) {
     if (!rec || rec[0] != '1' || !path || !path[0]) return;
     FILE *f = fopen(path, "a");
     if (!f) return;
+    if (!g_key_in_file && plans_key()[0]) {  // this process's pins go under its key
+        fprintf(f, "# key %s\n", plans_key());
+        g_key_in_file = true;
+    }
     if (choice < 0)
         fprintf(f, "%d %d %d %d %d own\n", std::get<0>(k), std::get<1>(k), std::get<2>(k),
                 std::get<3>(k), std::get<4>(k));
@@ -234,6 +280,14 @@ void search(Plan &p, int M, int N, int K, int relu, const float *A, const float 
 }  // namespace
 
 size_t gemm_epi_workspace_bytes() { return kMaxWs; }
+
+int gemm_plans_key(char *buf, int n) {
+    std::lock_guard<std::mutex> g(g_mu);
+    const char *k = plans_key();
+    if (!k[0]) return VD_ERR_LAUNCH;
+    snprintf(buf, (size_t)n, "%s", k);
+    return VD_OK;
+}
 
 int launch_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,
                          const float *R, int relu, float *D, void *ws, size_t ws_bytes,

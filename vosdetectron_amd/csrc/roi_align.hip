@@ -649,10 +649,6 @@ int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, con
     if (C % 4 != 0) return VD_ERR_SHAPE;
     const int variant = roialign_variant();
     if (out_nhwc) {  // product path: [R][P][P][C] written straight from registers
-        if (variant == 20 && PH == PW) {  // LDS-staged windows (roi_align_lds.hip)
-            const int st = launch_roi_align_fpn_lds(fa, C, rois, lvl, order, R, PH, sr, out, s);
-            if (st != VD_ERR_SHAPE) return st;
-        }
         if (variant == 10 && sr == 2 && PH == PW) {  // register gathers
             const int st = launch_sep_buf(fa, C, rois, lvl, order, R, PH, out, s);
             if (st != VD_ERR_SHAPE) return st;

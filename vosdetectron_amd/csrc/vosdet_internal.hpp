@@ -28,8 +28,6 @@ int launch_roi_align_bwd_nchw(const float *top_diff, int B, int C, int H, int W,
 int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, const int *lvl,
                               const int *order, int R, int PH, int PW, int sr, int out_nhwc,
                               float *out, hipStream_t s);
-int launch_roi_align_fpn_lds(const FpnLevels &fa, int C, const float *rois, const int *lvl,
-                             const int *order, int R, int P, int sr, float *out, hipStream_t s);
 
 bool roi_align_tiled_supported(const FpnLevels &fa, int C, int P, int sr);
 size_t roi_align_tiled_workspace_bytes(const FpnLevels &fa, int R, int P, int C);
@@ -38,6 +36,7 @@ int launch_roi_align_fpn_tiled(const FpnLevels &fa, int C, const float *rois, co
                                hipStream_t s);
 
 size_t gemm_epi_workspace_bytes();
+int gemm_plans_key(char *buf, int n);
 int launch_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,
                          const float *R, int relu, float *D, void *ws, size_t ws_bytes,
                          hipStream_t s);
@@ -46,10 +45,6 @@ bool conv3x3_mfma_supported(int C, int Cout);
 int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float *W2, int Cout,
                         const float *bias, int relu, float *Y, hipStream_t s);
 bool conv3x3_wino_supported(int C, int Cout);
-bool conv3x3_wino4_supported(int C, int Cout);
-int launch_conv3x3_wino4_weight(const float *w, int Cout, int C, float *U, hipStream_t s);
-int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float *U, int Cout,
-                         const float *bias, int relu, float *Y, hipStream_t s);
 int launch_conv3x3_wino_weight(const float *w, int Cout, int C, float *U, hipStream_t s);
 int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float *U, int Cout,
                         const float *bias, int relu, float *Y, hipStream_t s, int seg_h = 0);

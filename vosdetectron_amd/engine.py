@@ -208,6 +208,8 @@ class FramePipeline:
             cfg.FPN.ROI_MAX_LEVEL)
         out["masks"], out["mask_feat"] = self._mask_batch(pyr, mrois, mlvl, mcls, fast)
         out["mask_rois"], out["mask_total"] = mrois, mtotal
+        # the pyramid stays referenced only until complete() (the rare overflow
+        # batch reads it); complete() drops it so a kept result does not pin ~1.5 GB
         out["_pyr"], out["_fast"] = pyr, fast
         self._mark("im_detect_mask")
         if sync:
@@ -256,6 +258,8 @@ class FramePipeline:
             out["masks"] = torch.cat([out["masks"], m2])
             out["mask_feat"] = torch.cat([out["mask_feat"], f2])
             out["mask_rois"] = torch.cat([out["mask_rois"], r2])
+        out.pop("_pyr", None)
+        out.pop("_fast", None)
         out["masks"] = out["masks"][:M]
         out["mask_feat"] = out["mask_feat"][:M]
         out["mask_rois"] = out["mask_rois"][:M]

@@ -109,42 +109,72 @@ def _pick_mosaic(N: int, H: int, W: int, allow=True):
     return best
 
 
+def conv3x3_route(N: int, Cin: int, Cout: int, H: int, W: int, mosaic=True):
+    """(algorithm, mosaic) the engine runs a 3x3 / stride-1 / pad-1 fp32 conv of an
+    N x Cin x H x W channels_last batch with: ('wino', layout) -- Winograd
+    F(2x2,3x3), csrc/conv3x3_wino.hip, from 2^12 output pixels where its blocks are
+    >= 60 % real output (Cout % 64, Cin % 8) -- else ('igemm', None), the implicit
+    GEMM (csrc/conv3x3.hip), from 2^18 pixels, else (None, None): MIOpen / CK.
+    One rule for the engine (_conv3x3_mfma) and the bench's executed-FLOP count."""
+    npx = N * H * W
+    mos, use = _pick_mosaic(N, H, W, mosaic)
+    if (os.environ.get("VOSDET_CONV3X3_ALGO", CONV3X3_ALGO) == "wino" and npx >= _WINO_MIN_PIXELS
+            and use >= _WINO_MIN_BLOCK_USE and Cout % 64 == 0 and Cin % 8 == 0 and Cout > 0):
+        return "wino", mos
+    if npx < _CONV3X3_MIN_PIXELS:
+        return None, None
+    return "igemm", None
+
+
+# conv3x3 launches per route since the last reset (host-side, also counted while a
+# hipGraph is captured): 'wino', 'wino_rows', 'wino_2d', 'igemm', 'miopen'
+ROUTE_COUNTS = {}
+
+
+def _count_route(name: str):
+    ROUTE_COUNTS[name] = ROUTE_COUNTS.get(name, 0) + 1
+
+
 def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=True):
     """conv (3x3, stride 1, pad 1) of a channels_last fp32 tensor on the
     hand-written MFMA kernels with the bias (+ ReLU) epilogue, or None where
-    they do not apply (other geometry, VOSDET_CONV3X3_MFMA=0).  Algorithm
-    (VOSDET_CONV3X3_ALGO): 'wino' -- Winograd F(2x2,3x3), csrc/conv3x3_wino.hip,
-    from 2^12 output pixels where its blocks are >= 60 % real output -- else the
-    implicit GEMM (csrc/conv3x3.hip) from 2^18 pixels, else MIOpen / CK.
-    mosaic=True lets Winograd run the batch as a mosaic of maps with per-map zero
-    padding (_pick_mosaic): the mask head's 14 x 14 RoI maps 8 side by side per
-    112-column row -- every 8 x 16-pixel block real output (77 % one map per block,
-    87.5 % stacked in one column) -- and the 16-frame P3 / P4 maps 2 / 4 per row;
-    bit-identical results.  The transformed weights are cached on the module."""
+    they do not apply (other geometry, VOSDET_CONV3X3_MFMA=0).  The algorithm
+    is conv3x3_route's.  mosaic=True lets Winograd run the batch as a mosaic of
+    maps with per-map zero padding (_pick_mosaic): the mask head's 14 x 14 RoI
+    maps 8 side by side per 112-column row -- every 8 x 16-pixel block real
+    output (77 % one map per block, 87.5 % stacked in one column) -- and the
+    16-frame P3 / P4 maps 2 / 4 per row; bit-identical results.  The transformed
+    weights are cached on the module."""
     if (os.environ.get("VOSDET_CONV3X3_MFMA", "1") == "0" or not x.is_cuda
             or conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1)
             or conv.dilation != (1, 1) or conv.groups != 1 or x.dtype != torch.float32
             or not x.is_contiguous(memory_format=torch.channels_last)):
+        if conv.kernel_size == (3, 3):
+            _count_route("miopen")
         return None
-    npx = x.shape[0] * x.shape[2] * x.shape[3]
     w = conv.weight
     key = (w.data_ptr(), w._version)
     b = conv.bias.detach() if (bias and conv.bias is not None) else None
-    mos, use = _pick_mosaic(x.shape[0], x.shape[2], x.shape[3], mosaic)
-    if (os.environ.get("VOSDET_CONV3X3_ALGO", CONV3X3_ALGO) == "wino" and npx >= _WINO_MIN_PIXELS
-            and use >= _WINO_MIN_BLOCK_USE):
+    algo, mos = conv3x3_route(x.shape[0], x.shape[1], w.shape[0], x.shape[2], x.shape[3],
+                              mosaic)
+    if algo == "wino":
         if getattr(conv, "_vd_u_key", None) != key:
             conv._vd_u = ops.conv3x3_wino_weight(w.detach())
             conv._vd_u_key = key
         y = ops.conv3x3_wino_bias_act(x, conv._vd_u, b, relu=relu, mosaic=mos)
         if y is not None:
+            _count_route({False: "wino", True: "wino_rows", "2d": "wino_2d"}[mos])
             return y
-    if npx < _CONV3X3_MIN_PIXELS:
+        algo = "igemm" if x.shape[0] * x.shape[2] * x.shape[3] >= _CONV3X3_MIN_PIXELS else None
+    if algo is None:
+        _count_route("miopen")
         return None
     if getattr(conv, "_vd_w2_key", None) != key:
         conv._vd_w2 = ops.conv3x3_weight(w.detach())
         conv._vd_w2_key = key
-    return ops.conv3x3_bias_act(x, conv._vd_w2, b, relu=relu)
+    y = ops.conv3x3_bias_act(x, conv._vd_w2, b, relu=relu)
+    _count_route("igemm" if y is not None else "miopen")
+    return y
 
 
 CONV3X3_ALGO = "wino"  # the 3x3 algorithm the engine uses (VOSDET_CONV3X3_ALGO overrides)

@@ -197,7 +197,7 @@ _ORDER_CACHE = {}
 
 # FPN RoIAlign kernel for NHWC in/out (VOSDET_ROIALIGN_VARIANT overrides):
 # "30" tile-binned LDS-staged (roi_align_tile.hip), "10" register-gather separable
-# (roi_align.hip), "20" per-RoI LDS windows (roi_align_lds.hip), "3" reference-order rows.
+# (roi_align.hip), "3" reference-order rows.
 ROI_ALIGN_DEFAULT_VARIANT = "10"
 
 
@@ -548,51 +548,6 @@ def conv3x3_wino_weight(w: torch.Tensor) -> Optional[torch.Tensor]:
     check(lib().vd_conv3x3_wino_weight(w_.data_ptr(), Cout, C, u.data_ptr(), _stream()),
           "vd_conv3x3_wino_weight")
     return u
-
-
-def conv3x3_wino4_weight(w: torch.Tensor) -> Optional[torch.Tensor]:
-    """PyTorch conv weight [Cout][Cin][3][3] -> the Winograd F(4x4,3x3) operand
-    U = G g G^T (36 x Cout x Cin fp32 in the kernel's chunk-blocked order, held
-    as an opaque [Cout][Cin][36] tensor; vd_conv3x3_wino4_weight; once per model).
-    None for a shape the kernel does not serve (Cout % 32, Cin % 4)."""
-    w_ = _need(w, "w")
-    if w_.dim() != 4 or tuple(w_.shape[2:]) != (3, 3):
-        raise ValueError("conv3x3_wino4_weight: weight %s" % (tuple(w_.shape),))
-    Cout, C = w_.shape[:2]
-    if Cout % 32 or C % 4 or Cout == 0 or C == 0:
-        return None
-    u = torch.empty((Cout, C, 36), dtype=torch.float32, device=w_.device)
-    check(lib().vd_conv3x3_wino4_weight(w_.data_ptr(), Cout, C, u.data_ptr(), _stream()),
-          "vd_conv3x3_wino4_weight")
-    return u
-
-
-def conv3x3_wino4_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch.Tensor],
-                           relu: bool = False, out: Optional[torch.Tensor] = None):
-    """act(conv3x3(x, pad 1) + bias) on a channels_last fp32 tensor by Winograd
-    F(4x4,3x3) on the MFMA pipes (vd_conv3x3_wino4_bias_act); u from
-    conv3x3_wino4_weight.  Returns None for a shape the kernel does not serve."""
-    if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 4 \
-            or not x.is_contiguous(memory_format=torch.channels_last):
-        raise ValueError("x must be a channels_last fp32 device tensor")
-    if u is None:
-        return None
-    u_ = _need(u, "u")
-    N, C, H, W = x.shape
-    if u_.dim() != 3 or tuple(u_.shape[1:]) != (C, 36) or C % 4:
-        raise ValueError("u must be [Cout][%d][36], got %s" % (C, tuple(u_.shape)))
-    Cout = u_.shape[0]
-    b_ = _need(bias, "bias") if bias is not None else None
-    if out is None:
-        out = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device,
-                          memory_format=torch.channels_last)
-    st = lib().vd_conv3x3_wino4_bias_act(x.data_ptr(), N, H, W, C, u_.data_ptr(), Cout,
-                                         b_.data_ptr() if b_ is not None else None, int(relu),
-                                         out.data_ptr(), _stream())
-    if st == VD_ERR_SHAPE:
-        return None
-    check(st, "vd_conv3x3_wino4_bias_act")
-    return out
 
 
 def conv3x3_wino_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch.Tensor],
