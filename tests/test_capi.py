@@ -74,3 +74,17 @@ def test_miopen_db_is_a_per_process_copy():
         assert names == repr(seed) or eval(names) == seed
         assert not os.path.exists(d)  # removed at exit
     assert outs[0][0] != outs[1][0]
+
+
+@pytest.mark.gpu
+def test_gemm_plans_are_keyed_for_this_device():
+    """pinned GEMM plans apply only under a '# key' line equal to the
+    running device / hipBLASLt build (vd_gemm_plans_key); the shipped file carries
+    the key of the MI355X image the pins were recorded on."""
+    from vosdetectron_amd import _lib
+    b = ctypes.create_string_buffer(256)
+    _lib.check(_lib.lib().vd_gemm_plans_key(b, 256), "vd_gemm_plans_key")
+    key = b.value.decode()
+    assert key.startswith("gfx950 hipblaslt-"), key
+    lines = open(_lib.GEMM_PLANS).read().splitlines()
+    assert "# key " + key in lines, key

@@ -8,6 +8,82 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("N,C,H,W,Cout", [(2, 64, 9, 13, 128), (1, 256, 14, 14, 256),
+                                          (3, 128, 1, 1, 128), (1, 256, 25, 42, 256),
+                                          (5, 256, 7, 7, 384), (2, 64, 30, 41, 64),
+                                          (1, 128, 5, 3, 64)])
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("variant", ["1", "2", "6"])
+def test_conv3x3_vs_torch(monkeypatch, N, C, H, W, Cout, relu, variant):
+    from vosdetectron_amd import ops
+    monkeypatch.setenv("VOSDET_CONV3X3_VARIANT", variant)
+    g = torch.Generator(device="cpu").manual_seed(N * 1000 + C + H + Cout)
+    x = torch.randn(N, C, H, W, generator=g).cuda().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** .5).cuda()
+    b = torch.randn(Cout, generator=g).cuda()
+    ref = F.conv2d(x, w, b, padding=1)
+    if relu:
+        ref = F.relu(ref)
+    got = ops.conv3x3_bias_act(x, ops.conv3x3_weight(w), b, relu=relu)
+    torch.cuda.synchronize()
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    assert float((got - ref).abs().max()) <= 2e-5 * max(1., float(ref.abs().max()))
+
+
+def test_conv3x3_no_bias_and_unsupported_shape():
+    from vosdetectron_amd import ops
+    x = torch.randn(1, 64, 5, 6, device="cuda").contiguous(memory_format=torch.channels_last)
+    w = torch.randn(128, 64, 3, 3, device="cuda") / 24
+    got = ops.conv3x3_bias_act(x, ops.conv3x3_weight(w), None)
+    ref = F.conv2d(x, w, None, padding=1)
+    assert float((got - ref).abs().max()) <= 2e-5 * max(1., float(ref.abs().max()))
+    w2 = torch.randn(96, 64, 3, 3, device="cuda")  # Cout neither 64 nor a multiple of 128
+    assert ops.conv3x3_bias_act(x, ops.conv3x3_weight(w2), None) is None
+
+
+@pytest.mark.parametrize("N,C,H,W,Cout", [(1, 256, 25, 42, 256), (2, 256, 14, 14, 128)])
+def test_conv3x3_mid_tiles_vs_torch(monkeypatch, N, C, H, W, Cout):
+    """The opt-in 64 x 128-tile variant (VOSDET_CONV3X3_MID=1, used below 4096
+    big tiles) vs torch fp32, with and without bias / ReLU."""
+    from vosdetectron_amd import ops
+    monkeypatch.setenv("VOSDET_CONV3X3_MID", "1")
+    g = torch.Generator(device="cpu").manual_seed(N + C + H + W)
+    x = torch.randn(N, C, H, W, generator=g).cuda().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** .5).cuda()
+    b = torch.randn(Cout, generator=g).cuda()
+    for bias, relu in ((b, True), (None, False)):
+        ref = F.conv2d(x, w, bias, padding=1)
+        if relu:
+            ref = F.relu(ref)
+        got = ops.conv3x3_bias_act(x, ops.conv3x3_weight(w), bias, relu=relu)
+        assert float((got - ref).abs().max()) <= 2e-5 * max(1., float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("N,C,H,W,Cout", [(2, 64, 9, 13, 128), (1, 256, 14, 14, 256),
+                                          (3, 128, 1, 1, 128), (1, 256, 25, 42, 256),
+                                          (5, 256, 7, 7, 64), (2, 64, 30, 41, 64),
+                                          (1, 8, 5, 3, 64), (1, 256, 17, 70, 192)])
+@pytest.mark.parametrize("relu", [False, True])
+def test_conv3x3_wino_vs_torch(N, C, H, W, Cout, relu):
+    """Winograd F(2x2,3x3) MFMA kernel (csrc/conv3x3_wino.hip) vs a plain torch
+    fp32 conv2d(pad 1) + bias (+ ReLU): odd sizes (partial tiles and tile
+    blocks; both block shapes), a 1x1 image, Cin 8..256, Cout 64..256."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(7 * N + C + H + W + Cout)
+    x = torch.randn(N, C, H, W, generator=g).cuda().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** .5).cuda()
+    b = torch.randn(Cout, generator=g).cuda()
+    for bias in (b, None):
+        ref = F.conv2d(x, w, bias, padding=1)
+        if relu:
+            ref = F.relu(ref)
+        got = ops.conv3x3_wino_bias_act(x, ops.conv3x3_wino_weight(w), bias, relu=relu)
+        torch.cuda.synchronize()
+        assert got.is_contiguous(memory_format=torch.channels_last)
+        err = float((got - ref).abs().max())
+        assert err <= 2e-5 * max(1., float(ref.abs().max())), err
+
+
 @pytest.mark.parametrize("N,C,H,W,Cout", [(37, 256, 14, 14, 256), (5, 64, 6, 20, 128),
                                           (3, 8, 2, 9, 64), (9, 128, 14, 14, 64),
                                           (1, 64, 14, 14, 64), (100, 256, 14, 14, 256),
