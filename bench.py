@@ -130,8 +130,6 @@ def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=Non
     rois_t = torch.from_numpy(rois_np).to(dev)
     lv_t = torch.from_numpy(lv_np).to(dev)
     variant = os.environ.get("VOSDET_ROIALIGN_VARIANT", "10")
-    if deal is None:
-        deal = 8
     order = ops.xcd_roi_order(rois_t, lv_t, n_xcd=deal, window=window) if use_order else None
     shape = (frames * R, P, P, C) if out_layout == "nhwc" else (frames * R, C, P, P)
     out = torch.empty(shape, device=dev)

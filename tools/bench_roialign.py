@@ -17,7 +17,7 @@ if __name__ == "__main__":
     order = os.environ.get("ORDER", "1") == "1"
     frames = int(os.environ.get("FRAMES", "8"))
     r = measure_roialign_roofline(torch.device("cuda"), frames=frames, R=R, P=P, use_order=order,
-                                  out_layout=os.environ.get("OUT", "nhwc"),
+                                  out_layout=os.environ.get("RA_OUT_LAYOUT", "nhwc"),
                                   deal=int(os.environ["XCD_DEAL"]) if "XCD_DEAL" in os.environ
                                   else None,
                                   window=int(os.environ["XCD_WINDOW"]) if "XCD_WINDOW" in os.environ

@@ -33,16 +33,15 @@
 //                 and of the tiles' chunk counts (chunks of <= 192 bins).
 //  3. bin_scatter each bin's 24-byte descriptor into per-tile contiguous storage;
 //                 one lane per tile writes its chunk records.
-//  4. ring kernel persistent, one 14-wave workgroup per CU.  Two LOADER waves
-//                 copy item windows (rows x cols x 64 B) and descriptors into a
-//                 5-slot LDS ring by LDS-DMA, each keeping its previous item in
-//                 flight while it issues the next (counted vmcnt), and publish a
-//                 slot by writing its sequence number.  Twelve CONSUMER waves
-//                 poll the slot, compute their share of its 16-bin tasks (task
-//                 t goes to consumer (t - item) mod 12) from LDS and count
-//                 themselves out of the slot; a loader refills a slot once all
-//                 twelve have left it.  No workgroup barrier: consumers drift up
-//                 to the ring depth apart, loaders run ahead of all of them.
+//  4. ring kernel persistent, one 16-wave workgroup per CU.  Five LOADER waves,
+//                 one per slot of a 5-slot LDS ring, copy item windows (rows x
+//                 cols x 64 B) and descriptors into their slot by LDS-DMA and
+//                 publish it by writing its sequence number once their own DMA
+//                 landed.  Eleven CONSUMER waves poll the slot, compute their
+//                 share of its 16-bin tasks (task t goes to consumer (t - item)
+//                 mod 11) from LDS and count themselves out of the slot; its
+//                 loader refills it once all eleven have left.  No workgroup
+//                 barrier: consumers drift up to the ring depth apart.
 //  5. direct      one wave per direct-list bin, taps from global memory.
 //
 // Kernels 4 and 5 write disjoint bins and nothing accumulates across waves, so
@@ -67,8 +66,8 @@ constexpr int kDescB = kMaxChunk * 24 + 32;  // 4,640 B: descriptors + alignment
 constexpr int kSlotB = 30720;            // window + descriptors, 1 KiB multiple
 static_assert(kWinB + kDescB <= kSlotB, "slot holds its window and descriptors");
 constexpr int kSlots = 5;                // 153,600 B of the CU's 160 KiB
-constexpr int kNL = 2;                   // loader waves
-constexpr int kNC = 12;                  // consumer waves
+constexpr int kNL = kSlots;              // loader waves: one per slot
+constexpr int kNC = 11;                  // consumer waves (16 waves per workgroup)
 constexpr int kTaskBins = 16;            // bins per consumer task (4 lanes per bin)
 
 // Bin kinds of the binning passes.
@@ -374,6 +373,7 @@ typedef __attribute__((address_space(3))) volatile int lds_vi;
 struct Ring {
     int seq[kSlots];    // item index + 1 once the slot's window and descriptors landed
     int done[kSlots];   // consumers that have left the slot's current item
+    int retired[kSlots];  // item index + 1 of the slot's last item every consumer left
     int count[kSlots];  // bins of the slot's item
     int ncols[kSlots];  // window columns
     int delta[kSlots];  // descriptor byte offset (16-B aligned DMA of the descriptors)
@@ -477,6 +477,17 @@ __device__ __forceinline__ void bin_task(int pk, const float4 lw, lds_f4 *win, i
 
 __device__ __forceinline__ void nap() { __builtin_amdgcn_s_sleep(1); }
 
+#ifdef VD_RESEARCH_PROBES
+// Per-wave cycle accounting of the ring (research build only; read by
+// vd_research_ring_stats): [workgroup][wave][total, wait, work, items]
+__device__ unsigned long long g_ring_stats[256][16][4];
+#define VD_T(x) const unsigned long long x = __builtin_amdgcn_s_memtime()
+#define VD_ACC(i, v) acc_[i] += (v)
+#else
+#define VD_T(x)
+#define VD_ACC(i, v)
+#endif
+
 // 4. Persistent ring kernel: grid = 8 x K workgroups, block b on XCD x = b % 8,
 // k = b / 8.  XCD x computes slices 2x, 2x + 1; its item list is (chunk, slice
 // parity) in chunk order, and workgroup k takes items k, k + K8, ... with K8 =
@@ -497,30 +508,40 @@ __global__ __launch_bounds__((kNL + kNC) * 64) void ring_kernel(
     const int n_mine = k < n_items ? (n_items - k + K - 1) / K : 0;
     const uint32_t lds_base = (uint32_t)(uintptr_t)lds;
     lds_vi *seqw = (lds_vi *)ring.seq;
-    lds_vi *donew = (lds_vi *)ring.done;
+    lds_vi *retw = (lds_vi *)ring.retired;
     if (threadIdx.x < kSlots) {
         ring.seq[threadIdx.x] = 0;
-        ring.done[threadIdx.x] = kNC;  // every slot starts free
+        ring.done[threadIdx.x] = 0;
+        ring.retired[threadIdx.x] = 0;
     }
     __syncthreads();
+#ifdef VD_RESEARCH_PROBES
+    unsigned long long acc_[4] = {0, 0, 0, 0};
+    VD_T(t_begin);
+#endif
     if (wave < kNL) {
-        // LOADER: items m = wave, wave + kNL, ...; item m's window stays in
-        // flight while item m + kNL is issued, then m is published.
-        int prev_m = -1, prev_j = 0;
-        for (int m = wave; m < n_mine; m += kNL) {
-            const int j = m % kSlots;
-            while (donew[j] != kNC) nap();  // all consumers left item m - kSlots
+        // LOADER w owns slot w: items m = w, w + kSlots, ...  It refills its slot
+        // once every consumer has left the slot's previous item, prefetches its
+        // next chunk record while the DMA is in flight, waits for its own DMA
+        // only and publishes.  kSlots loaders keep every free slot in flight.
+        const int j = wave;
+        ChunkRec it = {};
+        if (j < n_mine) it = chunks[(k + K * j) >> 1];
+        for (int m = j; m < n_mine; m += kSlots) {
+            VD_T(t0);
+            if (m >= kSlots)
+                while (retw[j] != m - kSlots + 1) nap();  // item m - kSlots retired
+            VD_T(t1);
+            VD_ACC(1, t1 - t0);
             const int idx = k + K * m;
-            const ChunkRec it = chunks[idx >> 1];
             const int sl = 2 * xcd + (idx & 1);
             int delta = 0;
-            int n = 0;
             if (MODE != 2) {
-                n = issue_item(C, it, sl, desc, lds_base + (uint32_t)j * kSlotB, lane, delta);
+                issue_item(C, it, sl, desc, lds_base + (uint32_t)j * kSlotB, lane, delta);
             } else {  // descriptors only
                 ChunkRec d = it;
                 d.nrc = 0;
-                n = issue_item(C, d, sl, desc, lds_base + (uint32_t)j * kSlotB, lane, delta);
+                issue_item(C, d, sl, desc, lds_base + (uint32_t)j * kSlotB, lane, delta);
             }
             if (lane == 0) {
                 ring.done[j] = 0;
@@ -528,15 +549,25 @@ __global__ __launch_bounds__((kNL + kNC) * 64) void ring_kernel(
                 ring.ncols[j] = (it.nrc >> 8) & 255;
                 ring.delta[j] = delta;
             }
-            if (prev_m >= 0) {
-                wait_vm(n);  // the previous item's DMA has landed (younger: this one's n)
-                if (lane == 0) seqw[prev_j] = prev_m + 1;
-            }
-            prev_m = m;
-            prev_j = j;
+            const int mn = m + kSlots;
+            ChunkRec nx = it;
+            if (mn < n_mine) nx = chunks[(k + K * mn) >> 1];  // lands during the DMA
+            VD_T(t2);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            VD_T(t3);
+            VD_ACC(2, t3 - t2);
+            VD_ACC(3, 1);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) seqw[j] = m + 1;
+            it = nx;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (prev_m >= 0 && lane == 0) seqw[prev_j] = prev_m + 1;
+#ifdef VD_RESEARCH_PROBES
+        VD_T(t_end);
+        if (lane == 0 && blockIdx.x < 256) {
+            g_ring_stats[blockIdx.x][wave][0] = t_end - t_begin;
+            for (int i = 1; i < 4; ++i) g_ring_stats[blockIdx.x][wave][i] = acc_[i];
+        }
+#endif
         return;
     }
     // CONSUMER c: tasks t of item m with (t - m) mod kNC == c
@@ -544,7 +575,10 @@ __global__ __launch_bounds__((kNL + kNC) * 64) void ring_kernel(
     const int q = lane & 3, bsub = lane >> 2;
     for (int m = 0; m < n_mine; ++m) {
         const int j = m % kSlots;
+        VD_T(t0);
         while (seqw[j] != m + 1) nap();
+        VD_T(t1);
+        VD_ACC(1, t1 - t0);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const int count = __builtin_amdgcn_readfirstlane(ring.count[j]);
         const int ncols = __builtin_amdgcn_readfirstlane(ring.ncols[j]);
@@ -568,9 +602,20 @@ __global__ __launch_bounds__((kNL + kNC) * 64) void ring_kernel(
                     bin_task(a.y, lw, win, ncols, q, out + (int64_t)a.x * C + sl * kG + q * 4);
             }
         }
-        // this wave's reads of the slot are done (LDS executes a wave's ops in order)
-        if (lane == 0) atomicAdd((int *)&ring.done[j], 1);
+        // this wave's reads of the slot are done; the last consumer out retires it
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0 && atomicAdd((int *)&ring.done[j], 1) == kNC - 1) retw[j] = m + 1;
+        VD_T(t2);
+        VD_ACC(2, t2 - t1);
+        VD_ACC(3, ntask > 0 ? (ntask - 1 - (c - m % kNC + kNC) % kNC) / kNC + 1 : 0);
     }
+#ifdef VD_RESEARCH_PROBES
+    VD_T(t_end);
+    if (lane == 0 && blockIdx.x < 256) {
+        g_ring_stats[blockIdx.x][wave][0] = t_end - t_begin;
+        for (int i = 1; i < 4; ++i) g_ring_stats[blockIdx.x][wave][i] = acc_[i];
+    }
+#endif
 }
 
 // 5. Direct-list bins: one wave per bin, every channel from global memory, the
@@ -700,6 +745,16 @@ int num_cus() {
 
 }  // namespace raring
 
+#ifdef VD_RESEARCH_PROBES
+// Research build: copy the last ring launch's per-wave cycle accounting out.
+extern "C" int vd_research_ring_stats(unsigned long long *host, int n) {
+    const size_t bytes = sizeof(raring::g_ring_stats);
+    if (!host || (size_t)n * 8 < bytes) return VD_ERR_ARG;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(raring::g_ring_stats), bytes, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+#endif
+
 bool roi_align_ring_supported(const FpnLevels &fa, int C, int P, int sr) {
     using namespace raring;
     // XCD x computes slices 2x, 2x + 1: exactly 16 slices of 16 channels
@@ -726,12 +781,15 @@ int launch_roi_align_fpn_ring(const FpnLevels &fa, int C, const float *rois, con
     if (hipMemsetAsync(w.ext, 0, w.zero_bytes, s) != hipSuccess) return VD_ERR_LAUNCH;
     const unsigned blk = (unsigned)((nb + 255) / 256);
     const int T = tg.base[fa.L];
+    const char *ec = getenv("VOSDET_RA_CHUNK");  // tests: smaller chunks, more items
+    int chunk = ec ? atoi(ec) : kMaxChunk;
+    if (chunk < 8 || chunk > kMaxChunk) chunk = kMaxChunk;
     hipLaunchKernelGGL(bin_count_kernel, dim3(blk), dim3(256), 0, s, fa, tg, C, rois, lvl, P,
                        w.cnt, w.ext, w.slot, w.dir_cnt, w.dir_list, out);
-    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, T, kMaxChunk, w.cnt,
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, T, chunk, w.cnt,
                        w.offset, w.chunk_pre);
     hipLaunchKernelGGL(bin_scatter_kernel, dim3(blk + (unsigned)((T + 255) / 256)), dim3(256), 0,
-                       s, fa, tg, C, kMaxChunk, rois, lvl, P, w.slot, w.cnt, w.ext, w.offset,
+                       s, fa, tg, C, chunk, rois, lvl, P, w.slot, w.cnt, w.ext, w.offset,
                        w.chunk_pre, blk, w.desc, w.chunks);
     int nblk = num_cus() / 16 * 16;  // K = nblk / 8 workgroups per XCD, K even
     if (nblk < 16) nblk = 16;

@@ -13,6 +13,10 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libvosdet.so")
+# research builds (make VD_RESEARCH=1 OUT=...) are loaded by tools/research via this
+# override; the product and the tests use the in-tree library
+if os.environ.get("VOSDET_RESEARCH_LIB"):
+    LIB_PATH = os.environ["VOSDET_RESEARCH_LIB"]
 # pinned per-shape GEMM kernel choices (csrc/gemm_epi.cpp): the same file for
 # every process -- GPU tests, bench, all ranks -- so they compute the same numbers
 GEMM_PLANS = os.path.join(_HERE, "gemm_plans.txt")

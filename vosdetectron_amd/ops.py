@@ -237,7 +237,7 @@ def _deal(n: int, n_xcd: int, window: Optional[int]) -> np.ndarray:
     return p
 
 
-def xcd_roi_order(rois: torch.Tensor, roi_level: torch.Tensor, n_xcd: int = 8,
+def xcd_roi_order(rois: torch.Tensor, roi_level: torch.Tensor, n_xcd: Optional[int] = None,
                   band: int = 8, window: Optional[int] = None,
                   curve: Optional[str] = None) -> torch.Tensor:
     """Scheduling permutation for roi_align_fpn (never changes results): RoIs
@@ -252,6 +252,7 @@ def xcd_roi_order(rois: torch.Tensor, roi_level: torch.Tensor, n_xcd: int = 8,
     `window` positions (e.g. one frame's RoIs), so all XCDs work on the same
     frame at a time; n_xcd=1 is the plain spatial sort."""
     curve = curve or os.environ.get("VOSDET_RA_CURVE", "morton")
+    n_xcd = 8 if n_xcd is None else n_xcd
     r = rois
     lv = roi_level.to(torch.int64)
     scale = torch.pow(2.0, -(lv + 2).to(torch.float32))
