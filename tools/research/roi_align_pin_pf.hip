@@ -7,6 +7,9 @@
 //  16       variant 10 in frame-window order + prefetch blocks streaming the next
 //           frame's pyramid into the Infinity Cache: 756-2945 us (stride 8..32);
 //           frame-window order alone 321-326 us
+//  18       variant 10 + one TOUCH wave per block loading one dword per 128-B line of
+//           the footprint of the RoI its XCD runs `ahead` positions later: 417-494 us
+//           (ahead 16..256) vs 293 us -- the eighth wave per block costs occupancy
 // Channel-pinned separable NHWC forward (variants 12: G = 2, 14: G = 4), C = 256.
 // The 8 XCDs form G groups of 8 / G; group g computes channels [g * 256 / G,
 // (g + 1) * 256 / G) of EVERY RoI, so a pixel's line set is split over the groups
@@ -245,3 +248,62 @@ __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_pf_kernel(
                 return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
             }
         }
+
+// ===================== variant 18: touch wave =====================
+__device__ float g_touch_sink;
+
+// TOUCH (experiment, variant 18): one extra wave per block that touches every
+// 128-B line of the footprint of the RoI its XCD will run `ahead` schedule
+// positions later (blocks b and b + 8 ahead run on the same XCD, its slice of
+// the dealt order), so that RoI's first-touch misses are taken by a wave nobody
+// waits on and its compute waves hit the Infinity Cache / L2
+// (profiles/r04/roialign: 299 us with the pyramid in HBM, 191 us cache-resident).
+__device__ __forceinline__ void touch_roi(const FpnLevels &fa, int C, const float *roi, int li,
+                                          int P) {
+    const RoiGeom g = roi_geom(fa, C, roi, li, P, P, 2);
+    const int y0 = max(0, (int)floorf(g.sh)), x0 = max(0, (int)floorf(g.sw));
+    const int y1 = min(g.H - 1, (int)floorf(g.sh + g.bh * P) + 1);
+    const int x1 = min(g.W - 1, (int)floorf(g.sw + g.bw * P) + 1);
+    if (y1 < y0 || x1 < x0 || g.sh < -1e29f) return;
+    const int nx = x1 - x0 + 1, np = (y1 - y0 + 1) * nx;
+    const int lines = C / 32;  // 128-B lines per pixel
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(g.feat), (short)0, g.H * g.W * C * 4, 0x00020000);
+    const int lane = lane_id(), total = np * lines;
+    float sum = 0.f;
+    for (int t0 = 0; t0 < total; t0 += 64 * 8) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int t = t0 + i * 64 + lane;
+            const int pix = t / lines, ln = t - (t / lines) * lines;
+            const int yy = y0 + pix / nx, xx = x0 + pix - (pix / nx) * nx;
+            const int voff = t < total ? ((yy * g.W + xx) * C + ln * 32) * 4 : 0x7ffffff0;
+            v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, 0, 0));
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sum += v[i];
+    }
+    if (__float_as_uint(sum) == 0x7fbadbadu) g_touch_sink = sum;  // keeps the loads alive
+}
+
+
+// ---- in the kernel, before the RoI geometry ----
+    if (TOUCH && wave_id() == P) {
+        const int pt = p + 8 * ahead;
+        if (pt < fa.R) {
+            const int rt = roi_order ? roi_order[pt] : pt;
+            if (rt >= 0 && rt < fa.R) {
+                const int lt = __builtin_amdgcn_readfirstlane(roi_level ? roi_level[rt] : 0);
+                if (lt >= 0 && lt < fa.L) touch_roi(fa, C, rois + (int64_t)rt * 5, lt, P);
+            }
+        }
+        return;
+    }
+
+// ---- launch ----
+    const char *et = getenv("VOSDET_RA_TOUCH_AHEAD");  // variant 18 (experiment)
+    if (roialign_variant() == 18 && segs == 1 && parts == 1 && C <= 256 && P <= 8)
+        hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_buf_kernel<2, true, true, true>), dim3(nblk),
+                           dim3(64 * (P + 1)), 0, s, fa, C, rois, lvl, order, P, 1, 1, out,
+                           et ? atoi(et) : 64);
