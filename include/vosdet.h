@@ -215,6 +215,37 @@ size_t vd_nms_workspace_size(int n);
 int vd_nms(const float *dets, int n, int det_stride, float thresh, int64_t *keep_out,
            int32_t *num_out, void *workspace, size_t workspace_bytes, void *stream);
 
+/* The VOS fork's mask-IoU NMS, lib_vos/tools/vos_test.py:985-1029
+ * nms_with_mask_iou (applied at :113-118 when TEST.NMS_WITH_MASK_IOU > 0) on one
+ * frame's n detections (n <= 1024) in cls_boxes (class-major) order:
+ * planes n x im_h x im_w uint8 (the pasted, thresholded segms, nonzero = set),
+ * dets n x det_stride fp32 (score at column 4), classes n int32.  Score order
+ * (np.argsort(-s), ties by index), position j discarded by an earlier kept i
+ * when inter / (|m_i| + 1e-6) or inter / (|m_j| + 1e-6) > iou_th (float64), then
+ * at most max_per_class (TEST.NUM_DET_PER_CLASS_POST) per class.  Writes the
+ * kept detection indices in the reference's output order (class ascending, then
+ * score order) to keep_out and their count to *num_out (device int32).
+ * workspace: >= vd_mask_iou_nms_workspace_size(n, im_h, im_w) bytes. */
+size_t vd_mask_iou_nms_workspace_size(int n, int im_h, int im_w);
+int vd_mask_iou_nms(const uint8_t *planes, int n, int im_h, int im_w, const float *dets,
+                    int det_stride, const int32_t *classes, double iou_th, int max_per_class,
+                    int64_t *keep_out, int32_t *num_out, void *workspace, size_t workspace_bytes,
+                    void *stream);
+
+/* TEST.NMS_SMALL_BOX_IOU of the fork's box_results_with_nms_and_limit
+ * (lib_vos/tools/vos_test.py:845-860), in place on the device detections of F
+ * frames (dets [F][det_cap][5], classes, counts, class-major as vd_box_detections
+ * writes them): for each class whose previous-frame result (prev_* of the same
+ * row, [F][prev_cap]) holds one box with score >= score_thresh, the class's
+ * boxes with IoU (bb_intersection_over_union, float32) < iou_thresh are dropped;
+ * order kept.  A class with several previous boxes (the reference asserts) sets
+ * the frame's count to -1.  det_cap <= 1024. */
+int vd_detections_prev_box_filter(float *dets, int32_t *classes, int32_t *counts, int F,
+                                  int det_cap, const float *prev_dets,
+                                  const int32_t *prev_classes, const int32_t *prev_counts,
+                                  int prev_cap, float iou_thresh, float score_thresh,
+                                  void *stream);
+
 /* FPN level of each RoI: utils/fpn.py:11-28 map_rois_to_fpn_levels
  * (floor(lvl0 + log2(sqrt(area)/s0 + 1e-6)) clipped to [k_min, k_max]).
  * rois: R x roi_stride, the box at columns [col0, col0+4). */

@@ -379,14 +379,82 @@ def roi_feature_transform(blobs_in, rpn_ret, blob_rois, resolution, spatial_scal
 # --------------------------------------------------------------------------- #
 # Detection post-processing                                                    #
 # --------------------------------------------------------------------------- #
+def bb_iou_vos(a, b):
+    """lib_vos/tools/vos_test.py:961-982 bb_intersection_over_union on float32 box
+    rows as numpy 2 evaluates it: every product / sum in float32 (Python ints and
+    the float() of a float32 are weak scalars), the division float32 too."""
+    a = [np.float32(v) for v in a[:4]]
+    b = [np.float32(v) for v in b[:4]]
+    xA, yA = max(a[0], b[0]), max(a[1], b[1])
+    xB, yB = min(a[2], b[2]), min(a[3], b[3])
+    inter = max(0, xB - xA + 1) * max(0, yB - yA + 1)
+    area_a = (a[2] - a[0] + 1) * (a[3] - a[1] + 1)
+    area_b = (b[2] - b[0] + 1) * (b[3] - b[1] + 1)
+    return inter / float(area_a + area_b - inter)
+
+
+def small_box_filter(cls_boxes, prev_cls_boxes, iou_thresh, score_thresh):
+    """lib_vos/tools/vos_test.py:845-860 (TEST.NMS_SMALL_BOX_IOU > 0): for every
+    class j whose previous-frame result holds exactly one box (the reference
+    asserts < 2) with score >= score_thresh, drop this frame's class-j boxes whose
+    IoU with it is below iou_thresh; order kept."""
+    if prev_cls_boxes is None:
+        return cls_boxes
+    for j in range(1, len(cls_boxes)):
+        pj = prev_cls_boxes[j] if j < len(prev_cls_boxes) else []
+        assert len(pj) < 2, "number of prev boxes should <2."
+        if len(pj) != 1 or pj[0][-1] < score_thresh:
+            continue
+        keep = [k for k in range(len(cls_boxes[j]))
+                if not bb_iou_vos(pj[0], cls_boxes[j][k]) < iou_thresh]
+        cls_boxes[j] = cls_boxes[j][keep, :] if len(cls_boxes[j]) else cls_boxes[j]
+    return cls_boxes
+
+
+def nms_with_mask_iou(dets, classes, masks, iou_th, max_per_class):
+    """lib_vos/tools/vos_test.py:985-1029 on a frame's detections in cls_boxes
+    (class-major) order: dets [n,5], classes [n], masks [n,H,W] binary (the
+    decoded segms).  Processing order = score descending (np.argsort(-s), read
+    stably); position j is discarded by an earlier kept position i when
+    inter / (|m_i| + 1e-6) > iou_th or inter / (|m_j| + 1e-6) > iou_th (float64,
+    as numpy divides its integer sums); the kept detections are appended to
+    their class while it holds fewer than max_per_class.  Returns the kept input
+    indices in the reference's output order (class ascending, then append order)."""
+    n = len(dets)
+    if n == 0:
+        return np.zeros(0, np.int64)
+    order = np.argsort(-np.asarray(dets)[:, -1], kind="stable")
+    m = np.asarray(masks).reshape(n, -1).astype(bool)[order]
+    area = m.sum(1).astype(np.int64)
+    discard = np.zeros(n, bool)
+    for i in range(n):
+        if discard[i]:
+            continue
+        inter = (m[i + 1:] & m[i]).sum(1).astype(np.int64)
+        iou1 = inter / (area[i] + 1e-6)
+        iou2 = inter / (area[i + 1:] + 1e-6)
+        discard[i + 1:] |= (iou1 > iou_th) | (iou2 > iou_th)
+    kept = order[~discard]
+    per = {}
+    out = []
+    for k in kept:
+        c = int(classes[k])
+        if per.get(c, 0) < max_per_class:
+            per[c] = per.get(c, 0) + 1
+            out.append(k)
+    out = sorted(out, key=lambda k: (int(classes[k]), out.index(k)))
+    return np.asarray(out, np.int64)
+
+
 def box_results_with_nms_and_limit(scores, boxes, num_classes=81, score_thresh=0.05,
                                    nms_thresh=0.5, dets_per_im=100, nms_cross_class=0.,
-                                   num_det_per_class_pre=0):
+                                   num_det_per_class_pre=0, prev_cls_boxes=None,
+                                   small_box_iou=0., small_box_score_thresh=0.):
     """lib/core/test.py:733-797 with the fork's NUM_DET_PER_CLASS fix and its
     post-limit steps (lib_vos/tools/vos_test.py:748-865): TEST.NMS_CROSS_CLASS
-    (:810-827) and TEST.NUM_DET_PER_CLASS_PRE (:829-833; np.argsort(-s) read
-    stably, kind="stable").  NMS_SMALL_BOX_IOU needs the previous frame's boxes
-    and is off in every shipped config (out of scope)."""
+    (:810-827), TEST.NUM_DET_PER_CLASS_PRE (:829-833; np.argsort(-s) read
+    stably, kind="stable") and TEST.NMS_SMALL_BOX_IOU against the previous
+    frame's result (:845-860, small_box_filter)."""
     cls_boxes = [[] for _ in range(num_classes)]
     for j in range(1, num_classes):
         inds = np.where(scores[:, j] >= score_thresh)[0]
@@ -414,6 +482,9 @@ def box_results_with_nms_and_limit(scores, boxes, num_classes=81, score_thresh=0
         for j in range(1, num_classes):
             keep = np.argsort(-cls_boxes[j][:, -1], kind="stable")[:num_det_per_class_pre]
             cls_boxes[j] = cls_boxes[j][keep, :]
+    if small_box_iou > 0:
+        cls_boxes = small_box_filter(cls_boxes, prev_cls_boxes, small_box_iou,
+                                     small_box_score_thresh)
     im_results = np.vstack([cls_boxes[j] for j in range(1, num_classes)])
     return im_results[:, -1], im_results[:, :-1], cls_boxes
 

@@ -48,7 +48,6 @@ def test_config_matches_reference_yaml(name):
 @pytest.mark.parametrize("yml,keys", [
     ("configs/baselines/e2e_mask_rcnn_X-152-32x8d-FPN-IN5k_1.44x.yaml",
      ["TEST.BBOX_VOTE.ENABLED", "TEST.BBOX_AUG.ENABLED", "TEST.MASK_AUG.ENABLED"]),
-    ("lib_vos/tools/R-101-FPN_3x_gn_train_online.yaml", ["TEST.NMS_WITH_MASK_IOU"]),
 ])
 def test_unsupported_options_raise(yml, keys):
     """A reference YAML that enables an inference option this path does not build
@@ -66,11 +65,31 @@ def test_unsupported_options_raise(yml, keys):
 
 
 def test_unsupported_overrides_raise():
-    for key, val in (("TEST.SOFT_NMS.ENABLED", True), ("TEST.NMS_SMALL_BOX_IOU", 0.5),
-                     ("MODEL.USE_DELTA_FLOW", True), ("TEST.KPS_AUG.ENABLED", True)):
+    for key, val in (("TEST.SOFT_NMS.ENABLED", True), ("MODEL.USE_DELTA_FLOW", True),
+                     ("TEST.KPS_AUG.ENABLED", True)):
         with pytest.raises(NotImplementedError, match=key.replace(".", r"\.")):
             vcfg.load_cfg(overrides={key: val})
-    with pytest.raises(NotImplementedError, match="NMS_WITH_MASK_IOU"):
-        vcfg.merge_cfg_from_list(["TEST.NMS_WITH_MASK_IOU", "1.0"])
+    with pytest.raises(NotImplementedError, match="BBOX_VOTE"):
+        vcfg.merge_cfg_from_list(["TEST.BBOX_VOTE.ENABLED", "True"])
     # disabled values are accepted
-    vcfg.load_cfg(overrides={"TEST.NMS_SMALL_BOX_IOU": 0., "TEST.BBOX_VOTE.ENABLED": False})
+    vcfg.load_cfg(overrides={"TEST.SOFT_NMS.ENABLED": False, "TEST.BBOX_VOTE.ENABLED": False})
+
+
+def test_vos_heuristics_are_built():
+    """TEST.NMS_WITH_MASK_IOU and TEST.NMS_SMALL_BOX_IOU (the VOS
+    frame loop's heuristics, lib_vos/tools/vos_test.py:113-118, 845-860) are
+    implemented by engine.VOSPipeline: enabling them loads."""
+    c = vcfg.load_cfg(overrides={"TEST.NMS_WITH_MASK_IOU": 0.9, "TEST.NMS_SMALL_BOX_IOU": 0.3,
+                                 "TEST.NMS_SMALL_BOX_SCORE_THRESHOLD": 0.2,
+                                 "TEST.NUM_DET_PER_CLASS_POST": 1})
+    assert c.TEST.NMS_WITH_MASK_IOU == 0.9 and c.TEST.NMS_SMALL_BOX_IOU == 0.3
+    assert c.TEST.NMS_SMALL_BOX_SCORE_THRESHOLD == 0.2
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree absent")
+def test_train_online_yaml_loads():
+    """The fork's online-training VOS config (NMS_WITH_MASK_IOU 1.0,
+    NUM_DET_PER_CLASS_POST 1, NMS_SMALL_BOX_SCORE_THRESHOLD 0.2) loads."""
+    c = vcfg.load_cfg(os.path.join(REF, "lib_vos/tools/R-101-FPN_3x_gn_train_online.yaml"))
+    assert c.TEST.NMS_WITH_MASK_IOU == 1.0 and c.TEST.NUM_DET_PER_CLASS_POST == 1
+    assert c.TEST.NMS_SMALL_BOX_SCORE_THRESHOLD == 0.2

@@ -155,3 +155,42 @@ def test_nms_vs_executed_reference(golden):
     for i in range(int(g["count"])):
         if str(g["kind_%d" % i]) == "exact_threshold":
             assert g["keep_%d" % i].tolist() == [0, 2, 3, 4]
+
+
+def _prev_cls_boxes(g, case, K=81):
+    prev = [[] for _ in range(K)]
+    for row, j in zip(g["small_%d_prev_dets" % case], g["small_%d_prev_cls" % case]):
+        prev[int(j)] = row[None]
+    return prev
+
+
+def test_nms_with_mask_iou_vs_executed_reference(golden):
+    """The fork's mask-IoU NMS (lib_vos/tools/vos_test.py:985-1029) as executed by
+    the reference module (tools/gen_goldens.py gen_vos_post_fixture): nested /
+    overlapping / empty masks, iou_th 0.3 .. 1.0, per-class caps 0 .. 3 -- the
+    restatement keeps the same detections in the same order."""
+    g = golden("vos_post")
+    for c in range(int(g["mask_count"])):
+        keep = orc.nms_with_mask_iou(g["mask_%d_dets" % c], g["mask_%d_classes" % c],
+                                     g["mask_%d_masks" % c], float(g["mask_%d_iou_th" % c]),
+                                     int(g["mask_%d_per_class" % c]))
+        assert keep.tolist() == g["mask_%d_keep" % c].tolist(), c
+        assert np.array_equal(g["mask_%d_dets" % c][keep], g["mask_%d_keep_dets" % c])
+        assert g["mask_%d_classes" % c][keep].tolist() == g["mask_%d_keep_cls" % c].tolist()
+
+
+def test_small_box_filter_vs_executed_reference(golden):
+    """TEST.NMS_SMALL_BOX_IOU inside the fork's box_results_with_nms_and_limit
+    (vos_test.py:845-860) as the reference executed it, with the per-class cap
+    and the cross-class NMS before it: detections bit-exact."""
+    g = golden("vos_post")
+    K = 81
+    for c in range(int(g["small_count"])):
+        iou, sthr, pre, cross = g["small_%d_cfg" % c]
+        _, _, cb = orc.box_results_with_nms_and_limit(
+            g["small_scores"], g["small_boxes"], K, nms_cross_class=cross,
+            num_det_per_class_pre=int(pre), prev_cls_boxes=_prev_cls_boxes(g, c),
+            small_box_iou=iou, small_box_score_thresh=sthr)
+        dets = np.vstack([cb[j] for j in range(1, K)]).reshape(-1, 5)
+        assert np.array_equal(dets, g["small_%d_dets" % c]), c
+        assert len(dets) < int(g["small_%d_unfiltered" % c])  # the filter removed boxes

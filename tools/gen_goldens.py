@@ -20,9 +20,13 @@ Runtime-only import shims (nothing under /root/reference is modified):
     ``nms.npz`` pins it directly.  ``utils.cython_bbox`` is not on the
     inference path and stays a stub.
   * ``cv2`` / ``pycocotools`` stubs (imported at module level by core/test.py,
-    never called on the functions used here).
+    never called on the functions used here; vos_post.npz's mask-IoU NMS gets a
+    decode / encode stub that carries binary masks, see gen_vos_post_fixture);
+  * ``np.delete`` accepting an integral float64 index array (vos_test.py:1011,
+    what numpy of the reference's era did), for vos_post.npz only.
 
 Usage: python tools/gen_goldens.py   (writes tests/golden/*.npz)
+       python tools/gen_goldens.py vos_post   (only tests/golden/vos_post.npz)
 """
 import os
 import sys
@@ -318,5 +322,178 @@ def gen_nms_fixture(cy):
     np.savez_compressed(os.path.join(OUT, "nms.npz"), **out)
 
 
+def _blob_mask(rng, H, W, box):
+    """A filled ellipse / rectangle inside box (x1, y1, x2, y2) on an H x W frame."""
+    m = np.zeros((H, W), np.uint8)
+    x1, y1, x2, y2 = [int(round(v)) for v in box]
+    x1, y1 = max(x1, 0), max(y1, 0)
+    x2, y2 = min(x2, W - 1), min(y2, H - 1)
+    if x2 < x1 or y2 < y1:
+        return m
+    if rng.uniform() < 0.5:
+        m[y1:y2 + 1, x1:x2 + 1] = 1
+    else:
+        yy, xx = np.mgrid[0:H, 0:W]
+        cy, cx = (y1 + y2) / 2, (x1 + x2) / 2
+        ry, rx = max((y2 - y1) / 2, .5), max((x2 - x1) / 2, .5)
+        m[((yy - cy) / ry) ** 2 + ((xx - cx) / rx) ** 2 <= 1] = 1
+    return m
+
+
+def gen_vos_post_fixture():
+    """tests/golden/vos_post.npz: the fork's two detection heuristics of the VOS
+    frame loop, executed by the reference's own lib_vos/tools/vos_test.py:
+      * nms_with_mask_iou (:985-1029; called at :113-118 when
+        TEST.NMS_WITH_MASK_IOU > 0): masks decoded from the segms, greedy in
+        score order discarding j when inter / |m_i| or inter / |m_j| > iou_th,
+        then at most TEST.NUM_DET_PER_CLASS_POST per class.  pycocotools is
+        absent: a runtime stub decodes a segm to the binary mask it carries and
+        encodes a mask back to the index of the input mask it equals, so the
+        fixture records which detections the reference keeps, in its order;
+      * box_results_with_nms_and_limit(..., prev_cls_boxes) with
+        TEST.NMS_SMALL_BOX_IOU > 0 (:845-860): a class's boxes whose IoU with the
+        previous frame's (single, confident) box of that class is below the
+        threshold are dropped, after the cross-class NMS and the per-class cap."""
+    install_shims()
+    from core.config import cfg
+    sys.path.insert(0, os.path.join(REF, "lib_vos", "tools"))
+    import vos_test
+    rng = np.random.default_rng(20261018)
+    out = {}
+    # ---- nms_with_mask_iou
+    H, W, K = 48, 64, 81
+    cfg.MODEL.NUM_CLASSES = K
+    masks_in = []
+
+    class _MaskUtil:
+        @staticmethod
+        def decode(segms):
+            return np.stack([sg["m"] for sg in segms], axis=2)
+
+        @staticmethod
+        def encode(arr):
+            m = np.asarray(arr)[:, :, 0]
+            idx = [i for i, mi in enumerate(masks_in) if np.array_equal(mi, m)]
+            return [{"counts": str(idx[0]).encode("ascii"), "size": [H, W]}]
+    vos_test.mask_util = _MaskUtil
+    # nms_with_mask_iou collects discarded positions in np.array([]) (float64) and
+    # passes it to np.delete (:999-1011), which numpy of the reference's era accepted
+    # (integral floats as indices) and numpy 2 rejects: a runtime shim casts such an
+    # index array to intp -- the positions the reference meant
+    _np_delete = np.delete
+
+    def _delete(arr, obj, axis=None):
+        if isinstance(obj, np.ndarray) and obj.dtype.kind == "f":
+            assert np.all(obj == np.round(obj))
+            obj = obj.astype(np.intp)
+        return _np_delete(arr, obj, axis)
+    np.delete = _delete
+    ci = 0
+    for case, (n, iou_th, per_cls) in enumerate(((40, 0.5, 1), (40, 0.7, 2), (60, 0.9, 0),
+                                                 (30, 1.0, 1), (50, 0.3, 3), (1, 0.5, 1))):
+        classes = np.sort(rng.choice([1, 2, 3, 7, 15, 40, 80], n))
+        centres = rng.uniform([4, 4], [W - 4, H - 4], (max(1, n // 3), 2))
+        c = centres[rng.integers(0, len(centres), n)] + rng.normal(0, 3, (n, 2))
+        wh = rng.uniform(3, 30, (n, 2))
+        boxes = np.hstack([c - wh / 2, c + wh / 2]).astype(np.float32)
+        scores = distinct_scores(rng, max(n, 2))[:n]
+        masks = [_blob_mask(rng, H, W, b) for b in boxes]
+        for i in range(1, n, 7):  # nested masks: a smaller copy inside another
+            j = i - 1
+            inner = masks[j].copy()
+            ys, xs = np.nonzero(inner)
+            if len(ys) > 4:
+                inner[ys.min():ys.min() + (ys.max() - ys.min()) // 2 + 1] = 0
+                masks[i] = inner
+        if n > 5:
+            masks[5] = np.zeros((H, W), np.uint8)  # an empty mask
+        # no two input masks equal (the encode stub identifies masks by value)
+        seen = []
+        for i in range(n):
+            while any(np.array_equal(masks[i], m) for m in seen):
+                y, x = rng.integers(0, H), rng.integers(0, W)
+                masks[i][y, x] ^= 1
+            seen.append(masks[i])
+        masks_in[:] = masks
+        cls_boxes = [[] for _ in range(K)]
+        cls_segms = [[] for _ in range(K)]
+        for j in range(1, K):
+            idx = np.where(classes == j)[0]
+            if len(idx):
+                cls_boxes[j] = np.hstack([boxes[idx], scores[idx, None]]).astype(np.float32)
+                cls_segms[j] = [{"m": masks[i]} for i in idx]
+        nb, ns = vos_test.nms_with_mask_iou(cls_boxes, cls_segms, iou_th=iou_th,
+                                            max_per_class=per_cls)
+        kept_idx, kept_cls, kept_box = [], [], []
+        for j in range(K):
+            for b, sg in zip(nb[j], ns[j]):
+                kept_idx.append(int(sg["counts"]))
+                kept_cls.append(j)
+                kept_box.append(np.asarray(b, np.float32))
+        out["mask_%d_classes" % case] = classes.astype(np.int32)
+        out["mask_%d_dets" % case] = np.hstack([boxes, scores[:, None]]).astype(np.float32)
+        out["mask_%d_masks" % case] = np.stack(masks).astype(np.uint8)
+        out["mask_%d_iou_th" % case] = np.float64(iou_th)
+        out["mask_%d_per_class" % case] = np.int32(per_cls)
+        out["mask_%d_keep" % case] = np.asarray(kept_idx, np.int32)
+        out["mask_%d_keep_cls" % case] = np.asarray(kept_cls, np.int32)
+        out["mask_%d_keep_dets" % case] = (np.stack(kept_box) if kept_box
+                                           else np.zeros((0, 5), np.float32))
+        ci = case + 1
+    out["mask_count"] = np.int32(ci)
+    # ---- NMS_SMALL_BOX_IOU inside box_results_with_nms_and_limit
+    R = 300
+    xy = rng.uniform(0, 700, (R, 2))
+    wh = rng.uniform(8, 200, (R, 2))
+    base = np.hstack([xy, xy + wh])
+    boxes_cls = (np.tile(base, K) + rng.normal(0, 6, (R, 4 * K))).astype(np.float32)
+    logits = rng.normal(0, 2.5, (R, K))
+    e = np.exp(logits - logits.max(1, keepdims=True))
+    scores = (e / e.sum(1, keepdims=True)).astype(np.float32)
+    cfg.TEST.SCORE_THRESH, cfg.TEST.NMS, cfg.TEST.DETECTIONS_PER_IM = 0.05, 0.5, 100
+    cfg.TEST.SOFT_NMS.ENABLED, cfg.TEST.BBOX_VOTE.ENABLED = False, False
+    out["small_scores"], out["small_boxes"] = scores, boxes_cls
+    cases = ((0.3, 0.2, 0, 0.), (0.5, 0.2, 2, 0.), (0.1, 0.0, 0, 0.4), (0.7, 0.5, 1, 0.))
+    for case, (iou, sthr, pre, cross) in enumerate(cases):
+        cfg.TEST.NMS_SMALL_BOX_IOU = 0.
+        cfg.TEST.NMS_CROSS_CLASS, cfg.TEST.NUM_DET_PER_CLASS_PRE = cross, pre
+        _, _, cls_b = vos_test.box_results_with_nms_and_limit(scores, boxes_cls)
+        prev = [[] for _ in range(K)]
+        pd, pc = [], []
+        for j in range(1, K):
+            u = rng.uniform()
+            if len(cls_b[j]) and u < 0.6:  # a jittered copy of one of this frame's boxes
+                b = cls_b[j][rng.integers(0, len(cls_b[j]))][:4] + rng.normal(0, 25, 4)
+            elif u < 0.7:  # a box anywhere
+                p0 = rng.uniform(0, 700, 2)
+                b = np.hstack([p0, p0 + rng.uniform(8, 200, 2)])
+            else:
+                continue
+            row = np.hstack([b, rng.uniform(0, 1)]).astype(np.float32)
+            prev[j] = row[None]
+            pd.append(row)
+            pc.append(j)
+        cfg.TEST.NMS_SMALL_BOX_IOU = iou
+        cfg.TEST.NMS_SMALL_BOX_SCORE_THRESHOLD = sthr
+        _, _, cls_f = vos_test.box_results_with_nms_and_limit(scores, boxes_cls,
+                                                             prev_cls_boxes=prev)
+        out["small_%d_cfg" % case] = np.array([iou, sthr, pre, cross], np.float64)
+        out["small_%d_prev_dets" % case] = np.asarray(pd, np.float32).reshape(-1, 5)
+        out["small_%d_prev_cls" % case] = np.asarray(pc, np.int32)
+        out["small_%d_dets" % case] = np.vstack(
+            [cls_f[j] for j in range(1, K)]).astype(np.float32).reshape(-1, 5)
+        out["small_%d_cls" % case] = np.concatenate(
+            [[j] * len(cls_f[j]) for j in range(1, K)]).astype(np.int32)
+        out["small_%d_unfiltered" % case] = np.int32(sum(len(cls_b[j]) for j in range(1, K)))
+    out["small_count"] = np.int32(len(cases))
+    cfg.TEST.NMS_SMALL_BOX_IOU, cfg.TEST.NMS_CROSS_CLASS, cfg.TEST.NUM_DET_PER_CLASS_PRE = 0., 0., 0
+    np.savez_compressed(os.path.join(OUT, "vos_post.npz"), **out)
+    print("wrote vos_post.npz:", {k: v.shape for k, v in out.items() if k.endswith(("keep", "_dets"))})
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["vos_post"]:
+        gen_vos_post_fixture()
+    else:
+        main()
+        gen_vos_post_fixture()

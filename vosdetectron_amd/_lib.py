@@ -85,6 +85,10 @@ SIGNATURES = {
     "vd_nchw_to_nhwc": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "vd_bias_act": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P]),
     "vd_detections_postfilter": (_I, [_P, _P, _P, _I, _I, _F, _I, _P]),
+    "vd_mask_iou_nms_workspace_size": (_S, [_I, _I, _I]),
+    "vd_mask_iou_nms": (_I, [_P, _I, _I, _I, _P, _I, _P, ctypes.c_double, _I, _P, _P, _P, _S,
+                             _P]),
+    "vd_detections_prev_box_filter": (_I, [_P, _P, _P, _I, _I, _P, _P, _P, _I, _F, _F, _P]),
     # segm_results (paste + binarize + RLE counts)
     "vd_paste_masks": (_I, [_P, _I, _I, _P, _I, _I, _I, _F, _P, _P]),
     "vd_mask_rle": (_I, [_P, _I, _I, _I, _P, _I, _P, _P]),

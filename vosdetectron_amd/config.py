@@ -74,10 +74,12 @@ def default_cfg() -> AttrDict:
             DETECTIONS_PER_IM=100, SCORE_THRESH=0.05, NUM_DET_PER_CLASS_PRE=0,
             NUM_DET_PER_CLASS_POST=0, NMS_CROSS_CLASS=0.,
             # inference options read only to be rejected when enabled (UNSUPPORTED)
+            # (NMS_WITH_MASK_IOU / NMS_SMALL_BOX_IOU below are built: VOSPipeline)
             SOFT_NMS=_d(ENABLED=False), BBOX_VOTE=_d(ENABLED=False),  # config.py:356-383
             BBOX_AUG=_d(ENABLED=False), MASK_AUG=_d(ENABLED=False),  # config.py:246-316
             KPS_AUG=_d(ENABLED=False),  # config.py:322-351
-            NMS_WITH_MASK_IOU=0., NMS_SMALL_BOX_IOU=0.),  # config.py:951-952
+            NMS_WITH_MASK_IOU=0., NMS_SMALL_BOX_IOU=0.,  # config.py:951-953: the VOS
+            NMS_SMALL_BOX_SCORE_THRESHOLD=0.),  # loop's heuristics (engine.VOSPipeline)
         PIXEL_MEANS=(102.9801, 115.9465, 122.7717),  # config.py:1015
         BBOX_XFORM_CLIP=math.log(1000. / 16.),  # config.py:1009
         CROP_RESIZE_WITH_MAX_POOL=True,  # config.py:1058
@@ -116,10 +118,6 @@ UNSUPPORTED = (
     ("TEST.BBOX_AUG.ENABLED", bool, "box test-time augmentation, lib/core/test.py:193-727"),
     ("TEST.MASK_AUG.ENABLED", bool, "mask test-time augmentation, lib/core/test.py:405-480"),
     ("TEST.KPS_AUG.ENABLED", bool, "keypoint test-time augmentation (keypoint heads out of scope)"),
-    ("TEST.NMS_WITH_MASK_IOU", lambda v: float(v) > 0,
-     "mask-IoU NMS, lib_vos/tools/vos_test.py:113-118"),
-    ("TEST.NMS_SMALL_BOX_IOU", lambda v: float(v) > 0,
-     "small-box NMS against the previous frame, lib_vos/tools/vos_test.py:845-860"),
     ("MODEL.USE_DELTA_FLOW", bool, "delta-flow VOS head, lib_vos/vos_modeling/vos_model_builder.py"),
     ("MODEL.KEYPOINTS_ON", bool, "keypoint heads (out of scope)"),
 )

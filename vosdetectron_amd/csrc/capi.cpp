@@ -509,4 +509,32 @@ int vd_detections_postfilter(float *dets, int32_t *classes, int32_t *counts, int
                                         VD_STREAM(stream));
 }
 
+size_t vd_mask_iou_nms_workspace_size(int n, int im_h, int im_w) {
+    return mask_iou_nms_workspace_bytes(n, im_h, im_w);
+}
+
+int vd_mask_iou_nms(const uint8_t *planes, int n, int im_h, int im_w, const float *dets,
+                    int det_stride, const int32_t *classes, double iou_th, int max_per_class,
+                    int64_t *keep_out, int32_t *num_out, void *workspace, size_t workspace_bytes,
+                    void *stream) {
+    if (n < 0 || !num_out || (n > 0 && (!planes || !dets || !classes || !keep_out)))
+        return VD_ERR_ARG;
+    return launch_mask_iou_nms(planes, n, im_h, im_w, dets, det_stride, classes, iou_th,
+                               max_per_class, keep_out, num_out, workspace, workspace_bytes,
+                               VD_STREAM(stream));
+}
+
+int vd_detections_prev_box_filter(float *dets, int32_t *classes, int32_t *counts, int F,
+                                  int det_cap, const float *prev_dets,
+                                  const int32_t *prev_classes, const int32_t *prev_counts,
+                                  int prev_cap, float iou_thresh, float score_thresh,
+                                  void *stream) {
+    if (F < 0 || (F > 0 && (!dets || !classes || !counts || !prev_counts ||
+                            (prev_cap > 0 && (!prev_dets || !prev_classes)))))
+        return VD_ERR_ARG;
+    return launch_prev_box_filter(dets, classes, counts, F, det_cap, prev_dets, prev_classes,
+                                  prev_counts, prev_cap, iou_thresh, score_thresh,
+                                  VD_STREAM(stream));
+}
+
 }  // extern "C"

@@ -35,6 +35,15 @@ int launch_roi_align_fpn_tiled(const FpnLevels &fa, int C, const float *rois, co
                                int R, int P, int sr, float *out, void *ws, size_t ws_bytes,
                                hipStream_t s);
 
+size_t mask_iou_nms_workspace_bytes(int n, int im_h, int im_w);
+int launch_mask_iou_nms(const uint8_t *planes, int n, int im_h, int im_w, const float *dets,
+                        int det_stride, const int32_t *classes, double iou_th, int max_per_class,
+                        int64_t *keep_out, int32_t *num_out, void *ws, size_t ws_bytes,
+                        hipStream_t s);
+int launch_prev_box_filter(float *dets, int32_t *classes, int32_t *counts, int F, int det_cap,
+                           const float *prev_dets, const int32_t *prev_classes,
+                           const int32_t *prev_counts, int prev_cap, float iou_thresh,
+                           float score_thresh, hipStream_t s);
 size_t gemm_epi_workspace_bytes();
 int gemm_plans_key(char *buf, int n);
 int launch_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,

@@ -193,6 +193,7 @@ class FramePipeline:
             self.im_scale_t[:F], self.im_hw[:F], tst.SCORE_THRESH, tst.NMS,
             tst.DETECTIONS_PER_IM, cfg.MODEL.BBOX_REG_WEIGHTS, self.det_cap,
             nms_cross_class=tst.NMS_CROSS_CLASS, num_det_per_class_pre=tst.NUM_DET_PER_CLASS_PRE)
+        self._post_detections(dets, dcls, dcnt)
         self._mark("misc_bbox")
         out = {"dets": dets, "classes": dcls, "counts": dcnt, "rois": rois, "roi_counts": rcnt,
                "cls_prob": cls_prob, "bbox_pred": bbox_pred}
@@ -215,6 +216,10 @@ class FramePipeline:
         if sync:
             self.complete(out)
         return out
+
+    def _post_detections(self, dets, classes, counts):
+        """Hook after box_results_with_nms_and_limit's device steps (the VOS loop
+        adds its previous-frame filter)."""
 
     def mask_rows(self, F: int) -> int:
         """Rows of the step's mask batch: F x DETECTIONS_PER_IM, a multiple of 64
@@ -301,9 +306,20 @@ class VOSPipeline(FramePipeline):
                  det_cap=256, device="cuda"):
         super().__init__(model, cfg, frame_hw, batch, channels_last, det_cap, device)
         self._flow = None
+        # each sequence row's previous-frame result (prev_cls_boxes of the
+        # reference loop, train_davis_online.py:591-592), for NMS_SMALL_BOX_IOU
+        F = batch
+        self.prev_dets = torch.zeros((F, det_cap, 5), dtype=torch.float32, device=self.device)
+        self.prev_classes = torch.zeros((F, det_cap), dtype=torch.int32, device=self.device)
+        self.prev_counts = torch.zeros((F,), dtype=torch.int32, device=self.device)
 
     def reset(self, rows=None):
-        """Zero the hidden states of batch rows `rows` (all when None)."""
+        """Zero the hidden states (and forget the previous-frame results) of batch
+        rows `rows` (all when None)."""
+        if rows is None:
+            self.prev_counts.zero_()
+        else:
+            self.prev_counts[list(rows)] = 0
         hs = self.model.hidden_states
         if rows is None or all(h is None for h in hs):
             self.model.clean_hidden_states()
@@ -311,6 +327,61 @@ class VOSPipeline(FramePipeline):
         for h in hs:
             if h is not None:
                 h[list(rows)] = 0
+
+    def _post_detections(self, dets, classes, counts):
+        """TEST.NMS_SMALL_BOX_IOU (lib_vos/tools/vos_test.py:845-860): each row's
+        detections against its previous frame's final result, on the device.  Rows
+        without a previous result (a new sequence) pass unchanged."""
+        tst = self.cfg.TEST
+        if float(tst.NMS_SMALL_BOX_IOU) > 0:
+            F = dets.shape[0]
+            ops.detections_prev_box_filter(dets, classes, counts, self.prev_dets[:F],
+                                           self.prev_classes[:F], self.prev_counts[:F],
+                                           tst.NMS_SMALL_BOX_IOU,
+                                           tst.NMS_SMALL_BOX_SCORE_THRESHOLD)
+
+    def frame_results(self, out: dict, num_classes: int = None):
+        """The tail of the VOS im_detect_all (lib_vos/tools/vos_test.py:50-120) for
+        every row of a completed step: segm_results, then nms_with_mask_iou when
+        TEST.NMS_WITH_MASK_IOU > 0 (:113-118: masks pasted on the device, the mask
+        IoU NMS and the per-class cap of NUM_DET_PER_CLASS_POST on the device).
+        Returns a list over rows of (cls_boxes, cls_segms) -- cls_boxes[j] an
+        [n_j, 5] float32 array -- and records each row's result as the previous
+        frame of its sequence (prev_cls_boxes, for NMS_SMALL_BOX_IOU)."""
+        from . import segm
+        K = num_classes or int(self.cfg.MODEL.NUM_CLASSES)
+        tst = self.cfg.TEST
+        self.complete(out)
+        ks = [int(k) for k in out["counts_host"]]
+        thr = self.cfg.MRCNN.THRESH_BINARIZE
+        res, start = [], 0
+        mask_nms = float(tst.NMS_WITH_MASK_IOU) > 0
+        for f, k in enumerate(ks):
+            dets = out["dets"][f, :k]
+            classes = out["classes"][f, :k]
+            masks = out["masks"][start:start + k]
+            start += k
+            rles = segm.encode_masks(masks, dets, self.H, self.W, thr)
+            keep = torch.arange(k, device=self.device)
+            if mask_nms and k:
+                planes = ops.paste_masks(masks, dets, self.H, self.W, thr)
+                keep = ops.mask_iou_nms(planes, dets, classes, float(tst.NMS_WITH_MASK_IOU),
+                                        int(tst.NUM_DET_PER_CLASS_POST))
+            kd, kc = dets[keep], classes[keep]
+            n = kd.shape[0]
+            self.prev_dets[f, :n] = kd
+            self.prev_classes[f, :n] = kc
+            self.prev_counts[f] = n
+            kd_h, kc_h = kd.cpu().numpy(), kc.cpu().tolist()
+            kept = keep.cpu().tolist()
+            cls_boxes = [np.zeros((0, 5), np.float32) for _ in range(K)]
+            cls_segms = [[] for _ in range(K)]
+            for j in sorted(set(kc_h)):
+                rows = [i for i, c in enumerate(kc_h) if c == j]
+                cls_boxes[j] = kd_h[rows]
+                cls_segms[j] = [rles[kept[i]] for i in rows]
+            res.append((cls_boxes, cls_segms))
+        return res
 
     def backbone(self, frames):
         feats = super().backbone(frames)

@@ -781,6 +781,52 @@ def box_detections(rois, cls_prob, bbox_pred, roi_count, im_scale, im_hw, score_
     return dets, cls, cnt
 
 
+def detections_prev_box_filter(dets: torch.Tensor, classes: torch.Tensor, counts: torch.Tensor,
+                               prev_dets: torch.Tensor, prev_classes: torch.Tensor,
+                               prev_counts: torch.Tensor, iou_thresh: float,
+                               score_thresh: float) -> None:
+    """TEST.NMS_SMALL_BOX_IOU (lib_vos/tools/vos_test.py:845-860) in place on the
+    device detections (vd_detections_prev_box_filter): dets [F,cap,5], classes /
+    counts as box_detections writes them; prev_* the previous frame's final result
+    of each row ([F,pcap,5], [F,pcap], [F]).  A row whose previous result holds
+    two boxes of one class gets count -1 (the reference asserts)."""
+    d, c, n = _need(dets, "dets"), _need(classes, "classes", torch.int32), \
+        _need(counts, "counts", torch.int32)
+    pd, pc, pn = _need(prev_dets, "prev_dets"), _need(prev_classes, "prev_classes", torch.int32), \
+        _need(prev_counts, "prev_counts", torch.int32)
+    F, cap = d.shape[0], d.shape[1]
+    if tuple(pd.shape[:1]) != (F,) or pd.shape[2] != 5 or tuple(pc.shape) != tuple(pd.shape[:2]) \
+            or pn.numel() != F:
+        raise ValueError("prev_* must be [F,pcap,5], [F,pcap], [F] for F = %d" % F)
+    check(lib().vd_detections_prev_box_filter(
+        d.data_ptr(), c.data_ptr(), n.data_ptr(), F, cap, pd.data_ptr(), pc.data_ptr(),
+        pn.data_ptr(), pd.shape[1], float(np.float32(iou_thresh)),
+        float(np.float32(score_thresh)), _stream()), "vd_detections_prev_box_filter")
+
+
+def mask_iou_nms(planes: torch.Tensor, dets: torch.Tensor, classes: torch.Tensor,
+                 iou_th: float, max_per_class: int) -> torch.Tensor:
+    """nms_with_mask_iou (lib_vos/tools/vos_test.py:985-1029) on one frame
+    (vd_mask_iou_nms): planes [n,H,W] uint8 binary masks, dets [n,>=5], classes
+    [n] int32, in cls_boxes order.  Returns the kept indices (int64) in the
+    reference's output order (class ascending, then score order)."""
+    pl = _need(planes, "planes", torch.uint8)
+    d, c = _need(dets, "dets"), _need(classes, "classes", torch.int32)
+    n = d.shape[0]
+    if pl.shape[0] != n or c.numel() != n:
+        raise ValueError("planes, dets and classes must have the same n")
+    H, W = (pl.shape[1], pl.shape[2]) if pl.dim() == 3 else (1, 1)
+    keep = torch.empty((max(n, 1),), dtype=torch.int64, device=d.device)
+    num = torch.zeros((1,), dtype=torch.int32, device=d.device)
+    ws = _ws(lib().vd_mask_iou_nms_workspace_size(n, H, W), d.device)
+    check(lib().vd_mask_iou_nms(pl.data_ptr() if n else None, n, H, W,
+                                d.data_ptr() if n else None, d.shape[1] if d.dim() == 2 else 5,
+                                c.data_ptr() if n else None, float(iou_th), int(max_per_class),
+                                keep.data_ptr(), num.data_ptr(), ws.data_ptr(), ws.numel(),
+                                _stream()), "vd_mask_iou_nms")
+    return keep[: int(num.item())]
+
+
 # --------------------------------------------------------------------------- #
 # segm_results: paste + binarize + RLE counts (SURVEY.md section 8f row 3)      #
 # --------------------------------------------------------------------------- #
