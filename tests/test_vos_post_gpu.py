@@ -131,6 +131,7 @@ def test_vos_pipeline_heuristics_stagewise(vos_seq):
     paste of the GPU masks; a reset row forgets its previous frame."""
     cfg, pipe, frames = vos_seq
     tst = cfg.TEST
+    K = int(cfg.MODEL.NUM_CLASSES)  # 145 (the fork's class-agnostic VOS heads)
     pipe.reset()
     prev = [None, None]
     filtered_any = False

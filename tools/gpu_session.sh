@@ -10,6 +10,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 python - > "$OUT/plans_key.txt" 2>&1 <<'PY'
 import ctypes
+import torch  # loads torch's hipBLASLt first, as every product process does
 from vosdetectron_amd import _lib
 b = ctypes.create_string_buffer(256)
 _lib.check(_lib.lib().vd_gemm_plans_key(b, 256), "vd_gemm_plans_key")
