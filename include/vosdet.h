@@ -331,6 +331,48 @@ int vd_box_detections(const float *rois, const float *cls_prob, const float *bbo
                       int32_t *det_count_out, void *workspace, size_t workspace_bytes,
                       void *stream);
 
+/* vd_box_detections with the inference options of box_results_with_nms_and_limit
+ * (lib/core/test.py:756-776):
+ *  soft_nms_method  -1 = the NMS above; 0 hard / 1 linear / 2 gaussian =
+ *                   TEST.SOFT_NMS (utils/boxes.py:336-355 -> cython_nms.soft_nms,
+ *                   cython_nms.pyx:98-203; overlap threshold nms_thresh, sigma,
+ *                   min score 0.0001 at test.py:760): the class's rows in soft-NMS
+ *                   output order with decayed scores;
+ *  bbox_vote_method -1 = off; 0 ID / 1 AVG / 2 IOU_AVG / 3 QUASI_SUM =
+ *                   TEST.BBOX_VOTE.SCORING_METHOD (utils/boxes.py:277-333, voters:
+ *                   bbox_overlaps >= bbox_vote_thresh among the class's candidates;
+ *                   QUASI_SUM's beta = bbox_vote_beta).  GENERALIZED_AVG at beta 1
+ *                   is AVG; TEMP_AVG is not offered.
+ * Bit-exact to the compiled reference in this container (tests/golden/soft_nms.npz). */
+int vd_box_detections_ex(const float *rois, const float *cls_prob, const float *bbox_pred,
+                         const int32_t *roi_count, int R_cap, int num_images, int num_classes,
+                         const float *im_scale, const int32_t *im_hw, float score_thresh,
+                         float nms_thresh, int dets_per_im, const float *bbox_reg_weights,
+                         int soft_nms_method, float soft_nms_sigma, float soft_nms_min_score,
+                         int bbox_vote_method, float bbox_vote_thresh, float bbox_vote_beta,
+                         int det_cap, float *dets_out, int32_t *det_cls_out,
+                         int32_t *det_count_out, void *workspace, size_t workspace_bytes,
+                         void *stream);
+
+/* utils.boxes.soft_nms (lib/utils/boxes.py:336-355 -> cython_nms.soft_nms,
+ * cython_nms.pyx:98-203) on the device: dets n x dets_stride (>= 5) float32
+ * [x1, y1, x2, y2, score]; method 0 hard / 1 linear / 2 gaussian.  Writes the
+ * count_out[0] = N surviving rows (dets_out N x 5, decayed scores, in the
+ * reference's output order) and their input indices (keep_out).  n <= 4096;
+ * one wavefront (the reference loop is sequential in its selections). */
+int vd_soft_nms(const float *dets, int n, int dets_stride, float sigma, float overlap_thresh,
+                float score_thresh, int method, float *dets_out, int64_t *keep_out,
+                int32_t *count_out, void *stream);
+
+/* utils.boxes.box_voting (lib/utils/boxes.py:277-333): every top row becomes
+ * the score-weighted average of the rows of all_dets whose bbox_overlaps
+ * (cython_bbox.pyx, float32) with it is >= thresh, in numpy's summation order;
+ * scoring_method 0 ID / 1 AVG / 2 IOU_AVG / 3 QUASI_SUM (beta).  out: n_top x 5.
+ * n_all <= 4096. */
+int vd_box_voting(const float *top_dets, int n_top, int top_stride, const float *all_dets,
+                  int n_all, int all_stride, float thresh, int scoring_method, float beta,
+                  float *out, void *stream);
+
 /* Frame preparation, lib/utils/blob.py:37-114 at identity scale (im_scale 1): u8 BGR frames
  * (F x H x W x 3) -> fp32 blob minus PIXEL_MEANS, zero-padded to Hp x Wp
  * (multiples of FPN.COARSEST_STRIDE).  lut[3*256] = float32(u - mean_c) for

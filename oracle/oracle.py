@@ -446,23 +446,175 @@ def nms_with_mask_iou(dets, classes, masks, iou_th, max_per_class):
     return np.asarray(out, np.int64)
 
 
+def _cy_area(x1, y1, x2, y2):
+    """(x2 - x1 + 1) * (y2 - y1 + 1) on C floats as the compiled .pyx evaluates it:
+    Cython 3 emits the literal 1 as 1.0, so each side is (double)(x2 - x1) + 1.0,
+    the product in double, rounded to float on assignment."""
+    f, d = np.float32, np.float64
+    return f((d(f(x2 - x1)) + 1.0) * (d(f(y2 - y1)) + 1.0))
+
+
+def _cy_iou(a, b, area_b):
+    """iw / ih / ua / ov of cython_nms.soft_nms (:166-171) and cython_bbox
+    (bbox_overlaps) for float32 boxes a (the kept / top box) and b: 0 when they
+    do not overlap (iw or ih <= 0)."""
+    f, d = np.float32, np.float64
+    iw = f(d(f(min(a[2], b[2]) - max(a[0], b[0]))) + 1.0)
+    if not iw > 0:
+        return None
+    ih = f(d(f(min(a[3], b[3]) - max(a[1], b[1]))) + 1.0)
+    if not ih > 0:
+        return None
+    ua = f((d(f(a[2] - a[0])) + 1.0) * (d(f(a[3] - a[1])) + 1.0) + d(area_b) - d(f(iw * ih)))
+    return f(f(iw * ih) / ua)
+
+
+def soft_nms(dets, sigma=0.5, overlap_thresh=0.3, score_thresh=0.001, method="linear"):
+    """lib/utils/boxes.py:336-355 -> cython_nms.soft_nms (lib/utils/cython_nms.pyx:
+    98-203) as compiled here (Cython 3, see _cy_area): repeatedly move the
+    highest remaining score (first maximum by position) to the front, decay the
+    scores of the boxes after it that overlap it (linear: 1 - ov when ov > Nt;
+    gaussian: exp(-ov^2 / sigma) in double, stored as float; hard: 0 when
+    ov > Nt), and drop a decayed box whose score falls below score_thresh by
+    moving the last box into its place.  Returns (dets [N,5] float32, inds)."""
+    f = np.float32
+    if len(dets) == 0:
+        return dets, []
+    meth = {"hard": 0, "linear": 1, "gaussian": 2}[method]
+    b = np.array(dets, np.float32)
+    sigma, Nt, thr = f(sigma), f(overlap_thresh), f(score_thresh)
+    N = len(b)
+    inds = np.arange(N)
+    for i in range(len(b)):  # range() is evaluated once; the iterations i >= N are no-ops
+        if i >= N:
+            break
+        mp = i + int(np.argmax(b[i:N, 4]))  # `maxscore < s`: the first maximum
+        b[[i, mp]] = b[[mp, i]]
+        inds[[i, mp]] = inds[[mp, i]]
+        t = b[i].copy()
+        pos = i + 1
+        while pos < N:
+            x = b[pos]
+            ov = _cy_iou(t, x, _cy_area(x[0], x[1], x[2], x[3]))
+            if ov is not None:
+                if meth == 1:
+                    w = f(1) - ov if ov > Nt else f(1)
+                elif meth == 2:
+                    w = f(np.exp(np.float64(f(-(ov * ov)) / sigma)))
+                else:
+                    w = f(0) if ov > Nt else f(1)
+                b[pos, 4] = f(w * b[pos, 4])
+                if b[pos, 4] < thr:
+                    b[pos] = b[N - 1]
+                    inds[pos] = inds[N - 1]
+                    N -= 1
+                    pos -= 1
+            pos += 1
+    return b[:N], inds[:N]
+
+
+def np_pairwise_sum_f32(x):
+    """numpy's float32 add-reduce along a contiguous axis (loops_utils.h
+    pairwise_sum: < 8 sequential; <= 128 eight strided accumulators combined
+    ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) then the tail; else halves split at a
+    multiple of 8), after the reduction's initial 0."""
+    f = np.float32
+    x = [f(v) for v in x]
+
+    def pw(a):
+        n = len(a)
+        if n < 8:
+            r = f(0)
+            for v in a:
+                r = f(r + v)
+            return r
+        if n <= 128:
+            r = list(a[:8])
+            i = 8
+            while i < n - n % 8:
+                for k in range(8):
+                    r[k] = f(r[k] + a[i + k])
+                i += 8
+            res = f(f(f(r[0] + r[1]) + f(r[2] + r[3])) + f(f(r[4] + r[5]) + f(r[6] + r[7])))
+            for v in a[i:]:
+                res = f(res + v)
+            return res
+        n2 = n // 2
+        n2 -= n2 % 8
+        return f(pw(a[:n2]) + pw(a[n2:]))
+    return f(f(0) + pw(x))
+
+
+def box_voting(top_dets, all_dets, thresh, scoring_method="ID", beta=1.0):
+    """lib/utils/boxes.py:277-333 on float32 rows: the voters of top box k are
+    the rows of all_dets with bbox_overlaps (cython_bbox, float32; _cy_iou) >=
+    thresh, in row order; the box becomes np.average(voters, weights=scores)
+    = (sequential float32 sum of box * w down the rows) / (pairwise float32 sum
+    of w).  Scores: ID keeps it; AVG = mean(w); IOU_AVG = np.average(w,
+    weights=overlaps) (both sums pairwise along the 1-D axis); QUASI_SUM =
+    sum(w) / float(n) ** beta; GENERALIZED_AVG at beta == 1 is AVG.  TEMP_AVG
+    (float32 log / exp of numpy's SIMD library) is not restated."""
+    f = np.float32
+    out = np.array(top_dets, np.float32)
+    a = np.asarray(all_dets, np.float32)
+    areas = [_cy_area(*r[:4]) for r in a]
+    for k in range(len(out)):
+        t = out[k].copy()
+        vi, vo = [], []
+        for i in range(len(a)):
+            ov = _cy_iou(t, a[i], areas[i])
+            ov = f(0) if ov is None else ov
+            if ov >= f(thresh):
+                vi.append(i)
+                vo.append(ov)
+        ws = [a[i, 4] for i in vi]
+        scl = np_pairwise_sum_f32(ws)
+        for c in range(4):
+            acc = f(0)
+            for i, w in zip(vi, ws):
+                acc = f(acc + f(a[i, c] * w))
+            out[k, c] = f(acc / scl)
+        n = len(ws)
+        if scoring_method == "ID":
+            pass
+        elif scoring_method == "AVG" or (scoring_method == "GENERALIZED_AVG" and beta == 1.0):
+            out[k, 4] = f(scl / f(n))
+        elif scoring_method == "IOU_AVG":
+            out[k, 4] = f(np_pairwise_sum_f32([f(w * o) for w, o in zip(ws, vo)])
+                          / np_pairwise_sum_f32(vo))
+        elif scoring_method == "QUASI_SUM":
+            out[k, 4] = f(scl / f(float(n) ** beta))
+        else:
+            raise NotImplementedError(scoring_method)
+    return out
+
+
 def box_results_with_nms_and_limit(scores, boxes, num_classes=81, score_thresh=0.05,
                                    nms_thresh=0.5, dets_per_im=100, nms_cross_class=0.,
                                    num_det_per_class_pre=0, prev_cls_boxes=None,
-                                   small_box_iou=0., small_box_score_thresh=0.):
+                                   small_box_iou=0., small_box_score_thresh=0.,
+                                   soft_nms_method=None, soft_nms_sigma=0.5,
+                                   bbox_vote=None, bbox_vote_th=0.8, bbox_vote_beta=1.0):
     """lib/core/test.py:733-797 with the fork's NUM_DET_PER_CLASS fix and its
     post-limit steps (lib_vos/tools/vos_test.py:748-865): TEST.NMS_CROSS_CLASS
     (:810-827), TEST.NUM_DET_PER_CLASS_PRE (:829-833; np.argsort(-s) read
     stably, kind="stable") and TEST.NMS_SMALL_BOX_IOU against the previous
-    frame's result (:845-860, small_box_filter)."""
+    frame's result (:845-860, small_box_filter).  TEST.SOFT_NMS (soft_nms_method
+    'hard' / 'linear' / 'gaussian', score_thresh 0.0001, test.py:756-763) and
+    TEST.BBOX_VOTE (bbox_vote = the scoring method, test.py:769-776)."""
     cls_boxes = [[] for _ in range(num_classes)]
     for j in range(1, num_classes):
         inds = np.where(scores[:, j] >= score_thresh)[0]
         sj = scores[inds, j]
         bj = boxes[inds, j * 4:(j + 1) * 4]
         dj = np.hstack((bj, sj[:, None])).astype(np.float32, copy=False)
-        keep = nms(dj, nms_thresh)
-        cls_boxes[j] = dj[keep, :]
+        if soft_nms_method is not None:
+            nms_dets, _ = soft_nms(dj, soft_nms_sigma, nms_thresh, 0.0001, soft_nms_method)
+        else:
+            nms_dets = dj[nms(dj, nms_thresh), :]
+        if bbox_vote is not None and len(nms_dets):
+            nms_dets = box_voting(nms_dets, dj, bbox_vote_th, bbox_vote, bbox_vote_beta)
+        cls_boxes[j] = nms_dets
     if dets_per_im > 0:
         image_scores = np.hstack([cls_boxes[j][:, -1] for j in range(1, num_classes)])
         if len(image_scores) > dets_per_im:

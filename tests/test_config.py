@@ -47,11 +47,11 @@ def test_config_matches_reference_yaml(name):
 @pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree absent")
 @pytest.mark.parametrize("yml,keys", [
     ("configs/baselines/e2e_mask_rcnn_X-152-32x8d-FPN-IN5k_1.44x.yaml",
-     ["TEST.BBOX_VOTE.ENABLED", "TEST.BBOX_AUG.ENABLED", "TEST.MASK_AUG.ENABLED"]),
+     ["TEST.BBOX_AUG.ENABLED", "TEST.MASK_AUG.ENABLED"]),
 ])
 def test_unsupported_options_raise(yml, keys):
     """A reference YAML that enables an inference option this path does not build
-    (box voting, TTA, mask-IoU NMS, ...) raises and names the keys, through both
+    (test-time augmentation, ...) raises and names the keys, through both
     load_cfg and merge_cfg_from_file; the global cfg is left unchanged."""
     path = os.path.join(REF, yml)
     with pytest.raises(NotImplementedError) as e:
@@ -65,14 +65,38 @@ def test_unsupported_options_raise(yml, keys):
 
 
 def test_unsupported_overrides_raise():
-    for key, val in (("TEST.SOFT_NMS.ENABLED", True), ("MODEL.USE_DELTA_FLOW", True),
-                     ("TEST.KPS_AUG.ENABLED", True)):
+    for key, val in (("MODEL.USE_DELTA_FLOW", True), ("TEST.KPS_AUG.ENABLED", True)):
         with pytest.raises(NotImplementedError, match=key.replace(".", r"\.")):
             vcfg.load_cfg(overrides={key: val})
     with pytest.raises(NotImplementedError, match="BBOX_VOTE"):
-        vcfg.merge_cfg_from_list(["TEST.BBOX_VOTE.ENABLED", "True"])
+        vcfg.merge_cfg_from_list(["TEST.BBOX_VOTE.ENABLED", "True",
+                                  "TEST.BBOX_VOTE.SCORING_METHOD", "TEMP_AVG"])
+    with pytest.raises(NotImplementedError, match="BBOX_VOTE"):
+        vcfg.load_cfg(overrides={"TEST.BBOX_VOTE.ENABLED": True,
+                                 "TEST.BBOX_VOTE.SCORING_METHOD": "GENERALIZED_AVG",
+                                 "TEST.BBOX_VOTE.SCORING_METHOD_BETA": 2.0})
+    with pytest.raises(NotImplementedError, match="SOFT_NMS"):
+        vcfg.load_cfg(overrides={"TEST.SOFT_NMS.ENABLED": True, "TEST.SOFT_NMS.METHOD": "cubic"})
     # disabled values are accepted
     vcfg.load_cfg(overrides={"TEST.SOFT_NMS.ENABLED": False, "TEST.BBOX_VOTE.ENABLED": False})
+
+
+def test_soft_nms_and_box_voting_are_built():
+    """TEST.SOFT_NMS (every method) and TEST.BBOX_VOTE (ID / AVG / IOU_AVG /
+    QUASI_SUM, GENERALIZED_AVG at beta 1) load and map onto vd_box_detections_ex."""
+    from vosdetectron_amd.engine import nms_options
+    for m in ("hard", "linear", "gaussian"):
+        c = vcfg.load_cfg(overrides={"TEST.SOFT_NMS.ENABLED": True, "TEST.SOFT_NMS.METHOD": m})
+        assert nms_options(c) == {"soft_nms": m, "soft_nms_sigma": 0.5}
+    for sm in ("ID", "AVG", "IOU_AVG", "QUASI_SUM", "GENERALIZED_AVG"):
+        c = vcfg.load_cfg(overrides={"TEST.BBOX_VOTE.ENABLED": True,
+                                     "TEST.BBOX_VOTE.SCORING_METHOD": sm})
+        assert nms_options(c)["bbox_vote"] == sm
+    assert nms_options(vcfg.load_cfg()) == {}
+    c = vcfg.load_cfg(os.path.join(REF, "lib_vos/tools/R-101-FPN_3x_gn_train_online.yaml")) \
+        if os.path.isdir(REF) else None
+    if c is not None:  # the fork's ablation setting (disabled there)
+        assert (c.TEST.BBOX_VOTE.VOTE_TH, c.TEST.BBOX_VOTE.SCORING_METHOD) == (0.5, "IOU_AVG")
 
 
 def test_vos_heuristics_are_built():

@@ -194,3 +194,45 @@ def test_small_box_filter_vs_executed_reference(golden):
         dets = np.vstack([cb[j] for j in range(1, K)]).reshape(-1, 5)
         assert np.array_equal(dets, g["small_%d_dets" % c]), c
         assert len(dets) < int(g["small_%d_unfiltered" % c])  # the filter removed boxes
+
+
+def test_soft_nms_vs_executed_reference(golden):
+    """oracle.soft_nms restates cython_nms.soft_nms as compiled here (Cython 3's
+    double `+ 1.0` sub-expressions): rows, decayed scores and keep indices
+    bit-exact on every fixture case (soft_nms.npz, tools/gen_goldens.py)."""
+    g = golden("soft_nms")
+    for c in range(int(g["soft_count"])):
+        d = g["soft_in_%d" % int(g["soft_%d_in" % c])]
+        m, th, sigma = g["soft_%d_cfg" % c]
+        rows, keep = orc.soft_nms(d, sigma, th, 0.0001, ["hard", "linear", "gaussian"][int(m)])
+        assert np.array_equal(rows, g["soft_%d_out" % c]), c
+        assert list(keep) == g["soft_%d_keep" % c].tolist(), c
+
+
+def test_box_voting_vs_executed_reference(golden):
+    """oracle.box_voting: numpy's sequential axis-0 box sums and pairwise 1-D
+    weight sums (> 128 voters in the dense set) bit-exact on every method."""
+    g = golden("soft_nms")
+    for c in range(int(g["vote_count"])):
+        si, ti = g["vote_%d_sets" % c]
+        vth, beta = g["vote_%d_cfg" % c]
+        out = orc.box_voting(g["vote_top_%d" % ti], g["vote_set_%d" % si], vth,
+                             str(g["vote_%d_method" % c]), beta)
+        assert np.array_equal(out, g["vote_%d_out" % c]), (c, str(g["vote_%d_method" % c]))
+
+
+def _det_opts(g, c):
+    soft, vote, vth = [str(v) for v in g["det_%d_cfg" % c]]
+    return dict(soft_nms_method=None if soft == "None" else soft,
+                bbox_vote=None if vote == "None" else vote, bbox_vote_th=float(vth))
+
+
+def test_box_results_soft_nms_vote_vs_executed_reference(golden):
+    g = golden("soft_nms")
+    boxes = orc.clip_tiled_boxes(orc.bbox_transform(g["det_rois"][:, 1:5], g["det_deltas"],
+                                                    (10., 10., 5., 5.)),
+                                 tuple(g["det_im_hw"]) + (3,))
+    for c in range(int(g["det_count"])):
+        _, _, cb = orc.box_results_with_nms_and_limit(g["det_scores"], boxes, **_det_opts(g, c))
+        dets = np.vstack([cb[j] for j in range(1, 81)]).reshape(-1, 5)
+        assert np.array_equal(dets, g["det_%d_dets" % c]), c

@@ -17,8 +17,8 @@ Runtime-only import shims (nothing under /root/reference is modified):
     integer on Linux; numpy 2's .pxd dropped the old spelling).  Every fixture
     that runs through NMS (proposals, C4 proposals, collect/distribute, the
     fork's post-filter) therefore runs the executed reference NMS, and
-    ``nms.npz`` pins it directly.  ``utils.cython_bbox`` is not on the
-    inference path and stays a stub.
+    ``nms.npz`` pins it directly.  ``utils.cython_bbox``: the reference's own
+    ``lib/utils/cython_bbox.pyx``, compiled unmodified the same way (box voting).
   * ``cv2`` / ``pycocotools`` stubs (imported at module level by core/test.py,
     never called on the functions used here; vos_post.npz's mask-IoU NMS gets a
     decode / encode stub that carries binary masks, see gen_vos_post_fixture);
@@ -27,6 +27,7 @@ Runtime-only import shims (nothing under /root/reference is modified):
 
 Usage: python tools/gen_goldens.py   (writes tests/golden/*.npz)
        python tools/gen_goldens.py vos_post   (only tests/golden/vos_post.npz)
+       python tools/gen_goldens.py soft_nms   (only tests/golden/soft_nms.npz)
 """
 import os
 import sys
@@ -52,11 +53,9 @@ def install_shims():
     if not hasattr(dl, "numpy_type_map"):
         dl.numpy_type_map = {}
     sys.path.insert(0, os.path.join(REPO, "tools"))
-    from ref_cython_nms import load as load_ref_nms
+    from ref_cython_nms import load as load_ref_nms, load_bbox
     sys.modules["utils.cython_nms"] = load_ref_nms()
-    cy_bbox = types.ModuleType("utils.cython_bbox")
-    cy_bbox.bbox_overlaps = None  # not on the inference path
-    sys.modules["utils.cython_bbox"] = cy_bbox
+    sys.modules["utils.cython_bbox"] = load_bbox()  # box voting's bbox_overlaps
     cv2 = types.ModuleType("cv2")
     cv2.INTER_LINEAR = 1
     sys.modules["cv2"] = cv2
@@ -491,9 +490,125 @@ def gen_vos_post_fixture():
     print("wrote vos_post.npz:", {k: v.shape for k, v in out.items() if k.endswith(("keep", "_dets"))})
 
 
+def gen_soft_nms_fixture():
+    """tests/golden/soft_nms.npz: TEST.SOFT_NMS and TEST.BBOX_VOTE executed by the
+    reference itself (lib/core/test.py:756-776):
+      * soft_%d: utils/boxes.py soft_nms -> the compiled cython_nms.soft_nms
+        (cython_nms.pyx:98-203) on clustered boxes with exact duplicates (scores
+        decayed to 0 and removed), tied scores, N up to 1000, each method at
+        overlap 0.3 / 0.5: output rows and keep indices;
+      * vote_%d: utils/boxes.py box_voting (bbox_overlaps = the compiled
+        cython_bbox.pyx) on the NMS / soft-NMS rows of a set, every scoring
+        method this path builds, including a 400-box cluster (> 128 voters:
+        numpy's pairwise summation splits);
+      * det_%d: box_results_with_nms_and_limit (the fork's, lib_vos/tools/vos_test.py:
+        748-865; core/test.py:789 reads TEST.NUM_DET_PER_CLASS, absent from the
+        config) on decoded boxes
+        (box_utils.bbox_transform + clip_tiled_boxes of rois / deltas, as
+        im_detect_bbox does) with SOFT_NMS / BBOX_VOTE enabled."""
+    install_shims()
+    from core.config import cfg
+    import utils.boxes as box_utils
+    sys.path.insert(0, os.path.join(REF, "lib_vos", "tools"))
+    import vos_test as ref_test  # the fork's box_results (core/test.py:789 names a missing key)
+    rng = np.random.default_rng(20261019)
+    out = {}
+    i = 0
+    for si, n in enumerate((1, 2, 9, 64, 300, 1000)):
+        d = _clustered_dets(rng, n)
+        d[:, 4] = distinct_scores(rng, n) if n > 1 else np.float32(0.5)
+        if n >= 64:
+            d[10:20, :4] = d[9, :4]                        # exact duplicates: ov = 1
+            d[30:40, 4] = np.round(d[30:40, 4] * 4) / 4    # tied scores
+        for method in ("hard", "linear", "gaussian"):
+            for th in (0.3, 0.5):
+                r, keep = box_utils.soft_nms(d, sigma=0.5, overlap_thresh=th,
+                                             score_thresh=0.0001, method=method)
+                out["soft_in_%d" % si] = d
+                out["soft_%d_in" % i] = np.int64(si)
+                out["soft_%d_cfg" % i] = np.array([["hard", "linear", "gaussian"].index(method),
+                                                   th, 0.5], np.float64)
+                out["soft_%d_out" % i] = np.asarray(r, np.float32)
+                out["soft_%d_keep" % i] = np.asarray(keep, np.int64)
+                i += 1
+    out["soft_count"] = np.int64(i)
+    # ---- box voting
+    i = 0
+    dense = np.array([[100, 100, 180, 160]], np.float64) + rng.normal(0, 1.0, (400, 4))
+    dense = np.hstack([dense, distinct_scores(rng, 400)[:, None]]).astype(np.float32)
+    sets = [("cluster300", _clustered_dets(rng, 300)), ("dense400", dense)]
+    sets[0][1][:, 4] = distinct_scores(rng, 300)
+    max_voters = 0
+    ntop = 0
+    for si, (name, d) in enumerate(sets):
+        out["vote_set_%d" % si] = d
+        tops = {"nms": d[box_utils.nms(d, 0.5), :],
+                "soft": box_utils.soft_nms(d, 0.5, 0.3, 0.0001, "linear")[0]}
+        for tname, top in tops.items():
+            out["vote_top_%d" % ntop] = np.asarray(top, np.float32)
+            ov = sys.modules["utils.cython_bbox"].bbox_overlaps(
+                np.ascontiguousarray(top[:, :4]), np.ascontiguousarray(d[:, :4]))
+            for vth in (0.5, 0.8, 0.95):
+                max_voters = max(max_voters, int((ov >= np.float32(vth)).sum(1).max()))
+                for sm, beta in (("ID", 1.0), ("AVG", 1.0), ("IOU_AVG", 1.0),
+                                 ("QUASI_SUM", 1.0), ("QUASI_SUM", 2.0),
+                                 ("GENERALIZED_AVG", 1.0)):
+                    v = box_utils.box_voting(top, d, vth, scoring_method=sm, beta=beta)
+                    out["vote_%d_sets" % i] = np.array([si, ntop], np.int64)
+                    out["vote_%d_cfg" % i] = np.array([vth, beta], np.float64)
+                    out["vote_%d_method" % i] = np.array(sm)
+                    out["vote_%d_out" % i] = np.asarray(v, np.float32)
+                    i += 1
+            ntop += 1
+    assert max_voters > 128, max_voters
+    out["vote_count"] = np.int64(i)
+    # ---- box_results_with_nms_and_limit with the options, on decoded boxes
+    R, K, im_h, im_w = 300, 81, 480, 854
+    xy = rng.uniform(0, 800, (R, 2))
+    wh = rng.uniform(8, 200, (R, 2))
+    rois = np.zeros((R, 5), np.float32)
+    rois[:, 1:3] = xy
+    rois[:, 3:5] = np.minimum(xy + wh, [im_w + 9, im_h - 1])
+    logits = rng.normal(0, 2.5, (R, K))
+    e = np.exp(logits - logits.max(1, keepdims=True))
+    scores = (e / e.sum(1, keepdims=True)).astype(np.float32)
+    deltas = rng.normal(0, 0.25, (R, 4 * K)).astype(np.float32)
+    boxes = box_utils.bbox_transform(rois[:, 1:5], deltas, (10., 10., 5., 5.))
+    boxes = box_utils.clip_tiled_boxes(boxes, (im_h, im_w, 3))
+    out.update(det_rois=rois, det_scores=scores, det_deltas=deltas,
+               det_im_hw=np.array([im_h, im_w], np.int32))
+    cfg.MODEL.NUM_CLASSES = K
+    cfg.TEST.SCORE_THRESH, cfg.TEST.NMS, cfg.TEST.DETECTIONS_PER_IM = 0.05, 0.5, 100
+    i = 0
+    for soft, vote, vth in ((None, None, 0.8), ("linear", None, 0.8), ("gaussian", None, 0.8),
+                            ("hard", None, 0.8), (None, "ID", 0.8), (None, "IOU_AVG", 0.5),
+                            ("linear", "AVG", 0.5), ("gaussian", "QUASI_SUM", 0.8)):
+        cfg.TEST.SOFT_NMS.ENABLED = soft is not None
+        cfg.TEST.SOFT_NMS.METHOD = soft or "linear"
+        cfg.TEST.SOFT_NMS.SIGMA = 0.5
+        cfg.TEST.BBOX_VOTE.ENABLED = vote is not None
+        cfg.TEST.BBOX_VOTE.SCORING_METHOD = vote or "ID"
+        cfg.TEST.BBOX_VOTE.VOTE_TH = vth
+        _, _, cls_b = ref_test.box_results_with_nms_and_limit(scores, boxes)
+        out["det_%d_cfg" % i] = np.array([str(soft), str(vote), str(vth)])
+        out["det_%d_dets" % i] = np.vstack([cls_b[j] for j in range(1, K)]).astype(
+            np.float32).reshape(-1, 5)
+        out["det_%d_cls" % i] = np.concatenate(
+            [[j] * len(cls_b[j]) for j in range(1, K)]).astype(np.int32)
+        i += 1
+    out["det_count"] = np.int64(i)
+    cfg.TEST.SOFT_NMS.ENABLED, cfg.TEST.BBOX_VOTE.ENABLED = False, False
+    np.savez_compressed(os.path.join(OUT, "soft_nms.npz"), **out)
+    print("wrote soft_nms.npz: %d soft, %d vote, %d det cases, max voters %d"
+          % (out["soft_count"], out["vote_count"], out["det_count"], max_voters))
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["vos_post"]:
         gen_vos_post_fixture()
+    elif sys.argv[1:] == ["soft_nms"]:
+        gen_soft_nms_fixture()
     else:
         main()
         gen_vos_post_fixture()
+        gen_soft_nms_fixture()

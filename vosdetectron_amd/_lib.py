@@ -79,6 +79,10 @@ SIGNATURES = {
     "vd_box_detections_workspace_size": (_S, [_I, _I, _I]),
     "vd_box_detections": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P, _F, _F, _I, _P, _I, _P, _P,
                                _P, _P, _S, _P]),
+    "vd_box_detections_ex": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P, _F, _F, _I, _P,
+                                  _I, _F, _F, _I, _F, _F, _I, _P, _P, _P, _P, _S, _P]),
+    "vd_soft_nms": (_I, [_P, _I, _I, _F, _F, _F, _I, _P, _P, _P, _P]),
+    "vd_box_voting": (_I, [_P, _I, _I, _P, _I, _I, _F, _I, _F, _P, _P]),
     "vd_image_to_blob": (_I, [_P, _I, _I, _I, _P, _I, _I, _I, _P, _P]),
     "vd_image_resize_to_blob": (_I, [_P, _I, _I, _I, _P, ctypes.c_double, _I, _I, _I, _I, _I,
                                      _P, _P]),

@@ -1,4 +1,5 @@
-"""Drop-ins for the reference's ``utils.boxes`` NMS entry point (lib/utils/boxes.py:329-333).
+"""Drop-ins for the reference's ``utils.boxes`` NMS entry points (lib/utils/boxes.py:
+277-355: nms, soft_nms, box_voting).
 
 ``nms(dets, thresh)`` keeps the reference's host signature -- dets an (N, >=5)
 float32 ndarray ``[x1, y1, x2, y2, score]``, thresh a float -- and returns the
@@ -8,6 +9,9 @@ with cython_nms.nms semantics (``+1`` areas, fp32 IoU, suppress on
 device (vd_nms: wave-ballot bitmask + single-wave resolve, nms.hip); the rows go
 up and the indices come back because the reference's callers hold ndarrays.
 Device tensors are accepted as well and stay on the device.
+
+``soft_nms`` (vd_soft_nms) and ``box_voting`` (vd_box_voting) keep the
+reference's signatures and return ndarrays the same way.
 """
 from __future__ import annotations
 
@@ -32,3 +36,25 @@ def nms(dets, thresh):
     t = torch.from_numpy(np.ascontiguousarray(d, np.float32)).to(
         torch.device("cuda", torch.cuda.current_device()))
     return ops.nms(t, thresh).cpu().numpy()
+
+
+def _dev(d):
+    return torch.from_numpy(np.ascontiguousarray(d, np.float32)).to(
+        torch.device("cuda", torch.cuda.current_device()))
+
+
+def soft_nms(dets, sigma=0.5, overlap_thresh=0.3, score_thresh=0.001, method="linear"):
+    """Apply the soft NMS algorithm from https://arxiv.org/abs/1704.04503 (device)."""
+    d = np.asarray(dets)
+    if d.shape[0] == 0:
+        return dets, []
+    rows, keep = ops.soft_nms(_dev(d), sigma, overlap_thresh, score_thresh, method)
+    return rows.cpu().numpy(), keep.cpu().numpy()
+
+
+def box_voting(top_dets, all_dets, thresh, scoring_method="ID", beta=1.0):
+    """Refine top_dets by voting with all_dets (https://arxiv.org/abs/1505.01749)."""
+    t = np.asarray(top_dets)
+    if t.shape[0] == 0:
+        return t.copy()
+    return ops.box_voting(_dev(t), _dev(all_dets), thresh, scoring_method, beta).cpu().numpy()

@@ -73,9 +73,12 @@ def default_cfg() -> AttrDict:
             RPN_PRE_NMS_TOP_N=12000, RPN_POST_NMS_TOP_N=2000, RPN_MIN_SIZE=0,
             DETECTIONS_PER_IM=100, SCORE_THRESH=0.05, NUM_DET_PER_CLASS_PRE=0,
             NUM_DET_PER_CLASS_POST=0, NMS_CROSS_CLASS=0.,
+            # config.py:356-383: soft-NMS and box voting (vd_box_detections_ex)
+            SOFT_NMS=_d(ENABLED=False, METHOD="linear", SIGMA=0.5),
+            BBOX_VOTE=_d(ENABLED=False, VOTE_TH=0.8, SCORING_METHOD="ID",
+                         SCORING_METHOD_BETA=1.0),
             # inference options read only to be rejected when enabled (UNSUPPORTED)
             # (NMS_WITH_MASK_IOU / NMS_SMALL_BOX_IOU below are built: VOSPipeline)
-            SOFT_NMS=_d(ENABLED=False), BBOX_VOTE=_d(ENABLED=False),  # config.py:356-383
             BBOX_AUG=_d(ENABLED=False), MASK_AUG=_d(ENABLED=False),  # config.py:246-316
             KPS_AUG=_d(ENABLED=False),  # config.py:322-351
             NMS_WITH_MASK_IOU=0., NMS_SMALL_BOX_IOU=0.,  # config.py:951-953: the VOS
@@ -113,8 +116,13 @@ def _merge(a, b):
 # Inference options of the reference that change detections and are not built
 # here: (dotted key, "enabled" predicate, where the reference implements it).
 UNSUPPORTED = (
-    ("TEST.SOFT_NMS.ENABLED", bool, "soft-NMS, lib/utils/cython_nms.pyx:98-203, lib/core/test.py:755-766"),
-    ("TEST.BBOX_VOTE.ENABLED", bool, "box voting, lib/core/test.py:769-776, lib/utils/boxes.py:277-326"),
+    ("TEST.BBOX_VOTE", lambda v: bool(v.get("ENABLED")) and not (
+        v.get("SCORING_METHOD") in ("ID", "AVG", "IOU_AVG", "QUASI_SUM") or (
+            v.get("SCORING_METHOD") == "GENERALIZED_AVG" and v.get("SCORING_METHOD_BETA") == 1.0)),
+     "box-voting scoring TEMP_AVG / GENERALIZED_AVG at beta != 1 (numpy float32 log / exp / "
+     "pow), lib/utils/boxes.py:300-331"),
+    ("TEST.SOFT_NMS", lambda v: bool(v.get("ENABLED")) and v.get("METHOD") not in (
+        "hard", "linear", "gaussian"), "soft-NMS method (boxes.py:344 asserts)"),
     ("TEST.BBOX_AUG.ENABLED", bool, "box test-time augmentation, lib/core/test.py:193-727"),
     ("TEST.MASK_AUG.ENABLED", bool, "mask test-time augmentation, lib/core/test.py:405-480"),
     ("TEST.KPS_AUG.ENABLED", bool, "keypoint test-time augmentation (keypoint heads out of scope)"),

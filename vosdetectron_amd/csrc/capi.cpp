@@ -283,8 +283,45 @@ int vd_box_detections(const float *rois, const float *cls_prob, const float *bbo
         return VD_ERR_ARG;
     return launch_box_detections(rois, cls_prob, bbox_pred, roi_count, R_cap, num_images,
                                  num_classes, im_scale, im_hw, score_thresh, nms_thresh,
-                                 dets_per_im, bbox_reg_weights, det_cap, dets_out, det_cls_out,
-                                 det_count_out, workspace, workspace_bytes, VD_STREAM(stream));
+                                 dets_per_im, bbox_reg_weights, -1, 0.5f, 0.0001f, -1, 0.8f,
+                                 1.0f, det_cap, dets_out, det_cls_out, det_count_out, workspace,
+                                 workspace_bytes, VD_STREAM(stream));
+}
+
+int vd_box_detections_ex(const float *rois, const float *cls_prob, const float *bbox_pred,
+                         const int32_t *roi_count, int R_cap, int num_images, int num_classes,
+                         const float *im_scale, const int32_t *im_hw, float score_thresh,
+                         float nms_thresh, int dets_per_im, const float *bbox_reg_weights,
+                         int soft_nms_method, float soft_nms_sigma, float soft_nms_min_score,
+                         int bbox_vote_method, float bbox_vote_thresh, float bbox_vote_beta,
+                         int det_cap, float *dets_out, int32_t *det_cls_out,
+                         int32_t *det_count_out, void *workspace, size_t workspace_bytes,
+                         void *stream) {
+    if (!rois || !cls_prob || !bbox_pred || !roi_count || !im_scale || !im_hw ||
+        !bbox_reg_weights || !dets_out || !det_cls_out || !det_count_out)
+        return VD_ERR_ARG;
+    return launch_box_detections(rois, cls_prob, bbox_pred, roi_count, R_cap, num_images,
+                                 num_classes, im_scale, im_hw, score_thresh, nms_thresh,
+                                 dets_per_im, bbox_reg_weights, soft_nms_method, soft_nms_sigma,
+                                 soft_nms_min_score, bbox_vote_method, bbox_vote_thresh,
+                                 bbox_vote_beta, det_cap, dets_out, det_cls_out, det_count_out,
+                                 workspace, workspace_bytes, VD_STREAM(stream));
+}
+
+int vd_soft_nms(const float *dets, int n, int dets_stride, float sigma, float overlap_thresh,
+                float score_thresh, int method, float *dets_out, int64_t *keep_out,
+                int32_t *count_out, void *stream) {
+    if ((n > 0 && (!dets || !dets_out || !keep_out)) || !count_out) return VD_ERR_ARG;
+    return launch_soft_nms(dets, n, dets_stride, sigma, overlap_thresh, score_thresh, method,
+                           dets_out, keep_out, count_out, VD_STREAM(stream));
+}
+
+int vd_box_voting(const float *top_dets, int n_top, int top_stride, const float *all_dets,
+                  int n_all, int all_stride, float thresh, int scoring_method, float beta,
+                  float *out, void *stream) {
+    if (n_top > 0 && (!top_dets || !all_dets || !out)) return VD_ERR_ARG;
+    return launch_box_voting(top_dets, n_top, top_stride, all_dets, n_all, all_stride, thresh,
+                             scoring_method, beta, out, VD_STREAM(stream));
 }
 
 int vd_image_to_blob(const uint8_t *frames, int F, int H, int W, const float *lut, int Hp,

@@ -103,10 +103,17 @@ int launch_box_detections(const float *rois, const float *cls_prob, const float 
                           const int32_t *roi_count, int R_cap, int num_images, int num_classes,
                           const float *im_scale, const int32_t *im_hw, float score_thresh,
                           float nms_thresh, int dets_per_im, const float *bbox_weights,
-                          int det_cap, float *dets_out, int32_t *det_cls_out,
-                          int32_t *det_count_out, void *workspace, size_t ws_bytes,
-                          hipStream_t s);
+                          int soft_method, float soft_sigma, float soft_min, int vote_method,
+                          float vote_th, float vote_beta, int det_cap, float *dets_out,
+                          int32_t *det_cls_out, int32_t *det_count_out, void *workspace,
+                          size_t ws_bytes, hipStream_t s);
 size_t box_detections_workspace_bytes(int R_cap, int num_images, int num_classes);
+int launch_soft_nms(const float *dets, int n, int stride, float sigma, float overlap_thresh,
+                    float score_thresh, int method, float *dets_out, int64_t *keep_out,
+                    int32_t *count_out, hipStream_t s);
+int launch_box_voting(const float *top, int n_top, int top_stride, const float *all, int n_all,
+                      int all_stride, float thresh, int method, float beta, float *out,
+                      hipStream_t s);
 
 int launch_image_to_blob(const uint8_t *frames, int F, int H, int W, const float *lut,
                          int Hp, int Wp, int nhwc, float *blob, hipStream_t s);

@@ -45,6 +45,20 @@ class StageTimer:
         self.average_time = self.total_time / self.calls
 
 
+def nms_options(cfg) -> dict:
+    """TEST.SOFT_NMS / TEST.BBOX_VOTE (lib/core/test.py:756-776) as box_detections
+    keywords (empty when both are off: the stock vd_box_detections)."""
+    tst = cfg.TEST
+    opts = {}
+    if tst.SOFT_NMS.ENABLED:
+        opts.update(soft_nms=tst.SOFT_NMS.METHOD, soft_nms_sigma=tst.SOFT_NMS.SIGMA)
+    if tst.BBOX_VOTE.ENABLED:
+        opts.update(bbox_vote=tst.BBOX_VOTE.SCORING_METHOD,
+                    bbox_vote_thresh=tst.BBOX_VOTE.VOTE_TH,
+                    bbox_vote_beta=tst.BBOX_VOTE.SCORING_METHOD_BETA)
+    return opts
+
+
 class FramePipeline:
     ASYNC = True  # run(sync=False) queues a step with no host read (see run())
     def __init__(self, model, cfg, frame_hw=(800, 1333), batch=1, channels_last=False,
@@ -56,6 +70,7 @@ class FramePipeline:
         self.device = torch.device(device)
         self.channels_last = channels_last
         self.det_cap = det_cap
+        self._nms_options = nms_options(cfg)
         # blob geometry (lib/utils/blob.py:37-161): get_target_scale, cv2.resize
         # to round(H*s) x round(W*s) (done on the device when s != 1), pad to
         # FPN.COARSEST_STRIDE (get_max_shape; the C4 pipeline does not pad)
@@ -192,7 +207,8 @@ class FramePipeline:
             rois, cls_prob.view(F, post, K), bbox_pred.view(F, post, 4 * K), rcnt,
             self.im_scale_t[:F], self.im_hw[:F], tst.SCORE_THRESH, tst.NMS,
             tst.DETECTIONS_PER_IM, cfg.MODEL.BBOX_REG_WEIGHTS, self.det_cap,
-            nms_cross_class=tst.NMS_CROSS_CLASS, num_det_per_class_pre=tst.NUM_DET_PER_CLASS_PRE)
+            nms_cross_class=tst.NMS_CROSS_CLASS, num_det_per_class_pre=tst.NUM_DET_PER_CLASS_PRE,
+            **self._nms_options)
         self._post_detections(dets, dcls, dcnt)
         self._mark("misc_bbox")
         out = {"dets": dets, "classes": dcls, "counts": dcnt, "rois": rois, "roi_counts": rcnt,

@@ -374,6 +374,40 @@ def nms(dets: torch.Tensor, thresh: float) -> torch.Tensor:
     return keep[: int(num.item())]
 
 
+def soft_nms(dets: torch.Tensor, sigma: float = 0.5, overlap_thresh: float = 0.3,
+             score_thresh: float = 0.001, method: str = "linear"):
+    """utils.boxes.soft_nms on the device (vd_soft_nms): dets N x (>=5) fp32 ->
+    (rows [N',5] with decayed scores in the reference's order, keep int64 [N'])."""
+    d = _need(dets, "dets")
+    n = d.shape[0]
+    if method not in SOFT_NMS_METHODS:
+        raise ValueError("Unknown soft_nms method: {}".format(method))  # boxes.py:344
+    out = torch.empty((max(n, 1), 5), dtype=torch.float32, device=d.device)
+    keep = torch.empty((max(n, 1),), dtype=torch.int64, device=d.device)
+    num = torch.zeros((1,), dtype=torch.int32, device=d.device)
+    check(lib().vd_soft_nms(d.data_ptr() if n else None, n, d.shape[1] if d.dim() == 2 else 5,
+                            float(np.float32(sigma)), float(np.float32(overlap_thresh)),
+                            float(np.float32(score_thresh)), SOFT_NMS_METHODS[method],
+                            out.data_ptr(), keep.data_ptr(), num.data_ptr(), _stream()),
+          "vd_soft_nms")
+    k = int(num.item())
+    return out[:k], keep[:k]
+
+
+def box_voting(top_dets: torch.Tensor, all_dets: torch.Tensor, thresh: float,
+               scoring_method: str = "ID", beta: float = 1.0) -> torch.Tensor:
+    """utils.boxes.box_voting on the device (vd_box_voting): top [n,>=5], all
+    [m,>=5] fp32 -> [n,5]."""
+    t, a = _need(top_dets, "top_dets"), _need(all_dets, "all_dets")
+    out = torch.empty((t.shape[0], 5), dtype=torch.float32, device=t.device)
+    if t.shape[0]:
+        check(lib().vd_box_voting(t.data_ptr(), t.shape[0], t.shape[1], a.data_ptr(),
+                                  a.shape[0], a.shape[1], float(np.float32(thresh)),
+                                  bbox_vote_method(scoring_method, beta), float(beta),
+                                  out.data_ptr(), _stream()), "vd_box_voting")
+    return out
+
+
 def map_rois_to_fpn_levels(rois: torch.Tensor, k_min: int, k_max: int, col0: int = 1,
                            canonical_scale: float = 224., canonical_level: float = 4.):
     """utils/fpn.py:11-28 on device; returns int32 levels (k_min..k_max)."""
@@ -745,12 +779,32 @@ def collect_distribute(level_rois, level_probs, level_counts, post_nms_topN: int
     return rois, lvl, cnt
 
 
+SOFT_NMS_METHODS = {"hard": 0, "linear": 1, "gaussian": 2}  # utils/boxes.py:344
+BBOX_VOTE_METHODS = {"ID": 0, "AVG": 1, "IOU_AVG": 2, "QUASI_SUM": 3}
+
+
+def bbox_vote_method(scoring_method: str, beta: float = 1.0) -> int:
+    """TEST.BBOX_VOTE.SCORING_METHOD -> vd_box_detections_ex's code; GENERALIZED_AVG
+    at beta 1 is AVG (mean(ws**1)**1).  TEMP_AVG (numpy's float32 log / exp) and
+    GENERALIZED_AVG at other betas raise NotImplementedError."""
+    if scoring_method == "GENERALIZED_AVG" and float(beta) == 1.0:
+        return BBOX_VOTE_METHODS["AVG"]
+    if scoring_method not in BBOX_VOTE_METHODS:
+        raise NotImplementedError("TEST.BBOX_VOTE.SCORING_METHOD=%r (beta %r) is not implemented"
+                                  % (scoring_method, beta))
+    return BBOX_VOTE_METHODS[scoring_method]
+
+
 def box_detections(rois, cls_prob, bbox_pred, roi_count, im_scale, im_hw, score_thresh=0.05,
                    nms_thresh=0.5, dets_per_im=100, bbox_reg_weights=(10., 10., 5., 5.),
-                   det_cap=256, out=None, nms_cross_class=0., num_det_per_class_pre=0):
+                   det_cap=256, out=None, nms_cross_class=0., num_det_per_class_pre=0,
+                   soft_nms=None, soft_nms_sigma=0.5, bbox_vote=None, bbox_vote_thresh=0.8,
+                   bbox_vote_beta=1.0):
     """Decode + clip + per-class NMS + detections limit.  rois [N,R,5],
     cls_prob [N,R,K], bbox_pred [N,R,4K] -> (dets [N,cap,5], cls int32 [N,cap],
-    counts int32 [N])."""
+    counts int32 [N]).  soft_nms: TEST.SOFT_NMS.METHOD ('hard' / 'linear' /
+    'gaussian') instead of the NMS; bbox_vote: TEST.BBOX_VOTE.SCORING_METHOD
+    (lib/core/test.py:756-776, vd_box_detections_ex)."""
     r = _need(rois, "rois")
     p = _need(cls_prob, "cls_prob")
     d = _need(bbox_pred, "bbox_pred")
@@ -767,12 +821,25 @@ def box_detections(rois, cls_prob, bbox_pred, roi_count, im_scale, im_hw, score_
     wsb = lib().vd_box_detections_workspace_size(R, N, K)
     ws = _ws(wsb, r.device)
     w = (ctypes.c_float * 4)(*[float(np.float32(x)) for x in bbox_reg_weights])
-    check(lib().vd_box_detections(r.data_ptr(), p.data_ptr(), d.data_ptr(), c.data_ptr(), R, N, K,
-                                  s.data_ptr(), hw.data_ptr(), float(np.float32(score_thresh)),
-                                  float(np.float32(nms_thresh)), int(dets_per_im),
-                                  ctypes.cast(w, ctypes.c_void_p), det_cap, dets.data_ptr(),
-                                  cls.data_ptr(), cnt.data_ptr(), ws.data_ptr(), ws.numel(),
-                                  _stream()), "vd_box_detections")
+    if soft_nms is None and bbox_vote is None:
+        check(lib().vd_box_detections(r.data_ptr(), p.data_ptr(), d.data_ptr(), c.data_ptr(), R,
+                                      N, K, s.data_ptr(), hw.data_ptr(),
+                                      float(np.float32(score_thresh)),
+                                      float(np.float32(nms_thresh)), int(dets_per_im),
+                                      ctypes.cast(w, ctypes.c_void_p), det_cap, dets.data_ptr(),
+                                      cls.data_ptr(), cnt.data_ptr(), ws.data_ptr(), ws.numel(),
+                                      _stream()), "vd_box_detections")
+    else:
+        sm = -1 if soft_nms is None else SOFT_NMS_METHODS[soft_nms]
+        vm = -1 if bbox_vote is None else bbox_vote_method(bbox_vote, bbox_vote_beta)
+        check(lib().vd_box_detections_ex(
+            r.data_ptr(), p.data_ptr(), d.data_ptr(), c.data_ptr(), R, N, K, s.data_ptr(),
+            hw.data_ptr(), float(np.float32(score_thresh)), float(np.float32(nms_thresh)),
+            int(dets_per_im), ctypes.cast(w, ctypes.c_void_p), sm,
+            float(np.float32(soft_nms_sigma)), float(np.float32(0.0001)), vm,
+            float(np.float32(bbox_vote_thresh)), float(bbox_vote_beta), det_cap, dets.data_ptr(),
+            cls.data_ptr(), cnt.data_ptr(), ws.data_ptr(), ws.numel(), _stream()),
+            "vd_box_detections_ex")
     if nms_cross_class > 0 or num_det_per_class_pre > 0:  # the fork's vos_test.py:805-833
         check(lib().vd_detections_postfilter(dets.data_ptr(), cls.data_ptr(), cnt.data_ptr(), N,
                                              det_cap, float(np.float32(nms_cross_class)),
