@@ -737,6 +737,40 @@ def dry_run(args, world, rank):
     return 0 if okt.item() else 1
 
 
+def make_pipeline(cfg, model, F, layout, dev):
+    """The engine the bench times for a config, and its frame size: the VOS loop
+    (configs[3]: DAVIS-shaped 480p sequences; batch row b = sequence b of this
+    rank, SURVEY.md §8e, a step = the next frame of every sequence), the C4
+    single-scale family (configs[0]) or the FPN engine, at 800 x 1333."""
+    from vosdetectron_amd.engine import FramePipeline
+    nhwc = layout == "nhwc"
+    if cfg.get("VOS", False):
+        from vosdetectron_amd.engine import VOSPipeline
+        return VOSPipeline(model, cfg, frame_hw=(480, 854), batch=F, channels_last=nhwc,
+                           device=dev), 480, 854
+    if not cfg.FPN.FPN_ON:
+        from vosdetectron_amd.c4 import C4FramePipeline
+        return C4FramePipeline(model, cfg, batch=F, channels_last=nhwc, device=dev), 800, 1333
+    return FramePipeline(model, cfg, batch=F, channels_last=nhwc, device=dev), 800, 1333
+
+
+def step_calls(pipe, vos):
+    """The pipeline calls the timed step makes (bench.main's step()), as
+    (callable, args, kwargs): a test binds them against the engines' signatures
+    on CPU (a drift in a VOS / C4 signature otherwise costs a GPU run)."""
+    asynchronous = getattr(pipe, "ASYNC", False)
+    frames = object()
+    calls = [(pipe.run, (frames,), {"sync": not asynchronous}), (pipe.run, (frames,), {}),
+             (pipe.run, (frames,), {"keep_intermediates": True}),
+             (pipe.enable_timers, (), {}), (pipe.enable_timers, (False,), {}),
+             (pipe.timer_summary, (), {})]
+    if vos:
+        calls.append((pipe.reset, (), {}))
+    if asynchronous:
+        calls += [(pipe.complete, ({},), {}), (pipe.mask_rows, (1,), {})]
+    return calls
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -809,7 +843,6 @@ def main():
     torch.backends.cudnn.benchmark = True
 
     from vosdetectron_amd import config as vcfg
-    from vosdetectron_amd.engine import FramePipeline
     from vosdetectron_amd.runner import FrameUploader, ResultGatherer
     from vosdetectron_amd.weights import build_model
 
@@ -818,23 +851,7 @@ def main():
     model, sd = build_model(cfg, seed=0, device=dev, channels_last=args.layout == "nhwc")
     F = args.batch or 16
     n_host = 4  # distinct pinned host batches cycled through
-    if vos:
-        # configs[3]: DAVIS-shaped 480p sequences; batch row b = sequence b of
-        # this rank (sequences shard across ranks), a step = the
-        # next frame of every sequence, hidden states reset every --seq-len steps
-        from vosdetectron_amd.engine import VOSPipeline
-        fh, fw = 480, 854
-        pipe = VOSPipeline(model, cfg, frame_hw=(fh, fw), batch=F,
-                           channels_last=args.layout == "nhwc", device=dev)
-    elif not cfg.FPN.FPN_ON:  # configs[0]: the C4 single-scale family
-        from vosdetectron_amd.c4 import C4FramePipeline
-        fh, fw = 800, 1333
-        pipe = C4FramePipeline(model, cfg, batch=F, channels_last=args.layout == "nhwc",
-                               device=dev)
-    else:
-        fh, fw = 800, 1333
-        pipe = FramePipeline(model, cfg, batch=F, channels_last=args.layout == "nhwc",
-                             device=dev)
+    pipe, fh, fw = make_pipeline(cfg, model, F, args.layout, dev)
     host = [synthetic_frames(F, 1 + rank * F * n_host + i * F + (7919 if vos else 0), fh, fw)
             for i in range(n_host)]
     uploader = FrameUploader(host, dev)

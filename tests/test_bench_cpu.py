@@ -140,3 +140,24 @@ def test_winograd_mosaic_choice():
             os.environ.pop("VOSDET_WINO_MOSAIC", None)
         else:
             os.environ["VOSDET_WINO_MOSAIC"] = old
+
+
+def test_bench_engines_accept_the_step_calls():
+    """Weak r3 #9: bench.make_pipeline builds the engine each BASELINE config is
+    timed on (C4 configs[0], FPN configs[1], VOS configs[3]) on CPU, and every
+    call the timed step makes binds against that engine's signature (the round-3
+    `VOSPipeline.run() got an unexpected keyword argument 'sync'` cost a GPU run)."""
+    import inspect
+    from vosdetectron_amd import config as vcfg
+    from vosdetectron_amd.weights import build_model
+    for name in ("e2e_mask_rcnn_R-50-C4_1x", "e2e_mask_rcnn_R-50-FPN_1x",
+                 "vos_R-101-FPN_3x_gn_dynamic_davis"):
+        cfg = vcfg.get(name)
+        model, _ = build_model(cfg, device="cpu", fold=False)
+        pipe, fh, fw = bench.make_pipeline(cfg, model, 2, "nchw", "cpu")
+        vos = bool(cfg.get("VOS", False))
+        assert (fh, fw) == ((480, 854) if vos else (800, 1333)), name
+        assert type(pipe).__name__ == ("VOSPipeline" if vos else "C4FramePipeline"
+                                       if not cfg.FPN.FPN_ON else "FramePipeline"), name
+        for fn, args, kw in bench.step_calls(pipe, vos):
+            inspect.signature(fn).bind(*args, **kw)  # raises TypeError on a drift
