@@ -354,6 +354,17 @@ int vd_box_detections_ex(const float *rois, const float *cls_prob, const float *
                          int32_t *det_count_out, void *workspace, size_t workspace_bytes,
                          void *stream);
 
+/* ResNet stem in one pass (basic_bn_stem, lib/modeling/ResNet.py:224-230, with
+ * the AffineChannel folded into the bias): MaxPool 3x3/2 pad 1 (ReLU (conv1 7x7/2
+ * pad 3 (x) + bias)), conv1 3 -> 64 channels on the MFMA pipes; the conv output
+ * stays in LDS.  x: N x H x W x 3 fp32 (NHWC, the channels_last blob); y: N x Ho x
+ * Wo x 64 (Ho = ((H - 1) / 2) / 2 + 1 ...).  vd_stem_weight_pack reorders the
+ * PyTorch weight [64][3][7][7] into vd_stem_weight_size() bytes once. */
+size_t vd_stem_weight_size(void);
+int vd_stem_weight_pack(const float *w, float *packed, void *stream);
+int vd_stem_conv_pool(const float *x, int N, int H, int W, const float *packed, const float *bias,
+                      float *y, void *stream);
+
 /* utils.boxes.soft_nms (lib/utils/boxes.py:336-355 -> cython_nms.soft_nms,
  * cython_nms.pyx:98-203) on the device: dets n x dets_stride (>= 5) float32
  * [x1, y1, x2, y2, score]; method 0 hard / 1 linear / 2 gaussian.  Writes the

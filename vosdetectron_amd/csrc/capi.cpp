@@ -308,6 +308,19 @@ int vd_box_detections_ex(const float *rois, const float *cls_prob, const float *
                                  workspace, workspace_bytes, VD_STREAM(stream));
 }
 
+size_t vd_stem_weight_size(void) { return stem_weight_floats() * sizeof(float); }
+
+int vd_stem_weight_pack(const float *w, float *packed, void *stream) {
+    if (!w || !packed) return VD_ERR_ARG;
+    return launch_stem_weight(w, packed, VD_STREAM(stream));
+}
+
+int vd_stem_conv_pool(const float *x, int N, int H, int W, const float *packed, const float *bias,
+                      float *y, void *stream) {
+    if ((int64_t)N * H * W > 0 && (!x || !packed || !bias || !y)) return VD_ERR_ARG;
+    return launch_stem_conv_pool(x, N, H, W, packed, bias, y, 0, VD_STREAM(stream));
+}
+
 int vd_soft_nms(const float *dets, int n, int dets_stride, float sigma, float overlap_thresh,
                 float score_thresh, int method, float *dets_out, int64_t *keep_out,
                 int32_t *count_out, void *stream) {

@@ -464,12 +464,16 @@ __global__ __launch_bounds__(1024) void det_limit_kernel(const int32_t *__restri
         if (threadIdx.x == 0) det_count_out[img] = -1;
         return;
     }
-    // prefix over classes 1..K-1 (K <= 1024)
+    // prefix over classes 1..K-1 (K <= 1024): the counts loaded by K threads at
+    // once (a serial loop waited out one global-load latency per class), then one
+    // thread sums them in LDS
+    for (int j = threadIdx.x; j < K; j += blockDim.x)
+        offs[j] = j ? ws.cls_count[(size_t)img * K + j] : 0;
+    __syncthreads();
     if (threadIdx.x == 0) {
         int o = 0;
-        offs[0] = 0;
         for (int j = 1; j < K; ++j) {
-            o += ws.cls_count[(size_t)img * K + j];
+            o += offs[j];
             offs[j] = o;
         }
     }

@@ -364,14 +364,29 @@ def _fold(conv: nn.Conv2d, aff: AffineChannel2d) -> nn.Conv2d:
 
 
 class _StemEpilogue(nn.Module):
-    """Folded stem: conv1 (+ bias + ReLU in one epilogue pass) + max-pool."""
+    """Folded stem: conv1 + bias + ReLU + max-pool in one MFMA kernel
+    (vd_stem_conv_pool; VOSDET_STEM=miopen: conv1 on MIOpen + one epilogue pass)."""
 
     def __init__(self, conv1, maxpool):
         super().__init__()
         self.conv1, self.maxpool = conv1, maxpool
 
+    def _fused_ok(self, x):
+        c = self.conv1
+        return (os.environ.get("VOSDET_STEM", "miopen") == "fused" and c.bias is not None
+                and tuple(c.weight.shape) == (64, 3, 7, 7) and c.stride == (2, 2)
+                and c.padding == (3, 3) and c.dilation == (1, 1) and c.groups == 1
+                and x.shape[1] == 3 and x.is_contiguous(memory_format=torch.channels_last)
+                and x.dtype == torch.float32)
+
     def forward(self, x):
         if x.is_cuda:
+            if self._fused_ok(x):  # conv + bias + ReLU + max-pool in one MFMA kernel
+                key = (self.conv1.weight.data_ptr(), self.conv1.weight._version)
+                if getattr(self, "_stem_key", None) != key:
+                    self._stem_packed = ops.stem_pack(self.conv1.weight)
+                    self._stem_key = key
+                return ops.stem_conv_pool(x, self._stem_packed, self.conv1.bias)
             h = _conv_nb(self.conv1, x)
             if (h.is_contiguous(memory_format=torch.channels_last) and not h.is_contiguous()
                     and h.shape[1] % 4 == 0 and os.environ.get("VOSDET_STEM_FUSED", "1") != "0"):

@@ -951,6 +951,37 @@ def bias_relu_maxpool(x_raw: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def stem_pack(weight: torch.Tensor) -> torch.Tensor:
+    """conv1's weight [64, 3, 7, 7] in vd_stem_conv_pool's register order (once)."""
+    w = _need(weight, "weight")
+    if tuple(w.shape) != (64, 3, 7, 7):
+        raise ValueError("stem weight must be 64 x 3 x 7 x 7, got %s" % (tuple(w.shape),))
+    out = torch.empty((lib().vd_stem_weight_size() // 4,), dtype=torch.float32, device=w.device)
+    check(lib().vd_stem_weight_pack(w.data_ptr(), out.data_ptr(), _stream()),
+          "vd_stem_weight_pack")
+    return out
+
+
+def stem_conv_pool(x: torch.Tensor, packed: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    """ResNet stem in one kernel (vd_stem_conv_pool): MaxPool2d(3, 2, 1)(relu(conv1 7x7/2
+    pad 3 (x) + bias)) for a channels_last N x 3 x H x W blob; returns channels_last
+    N x 64 x Ho x Wo (the conv output never leaves LDS)."""
+    N, C, H, W = x.shape
+    if not (x.is_cuda and x.dtype == torch.float32 and C == 3
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        raise ValueError("x must be a channels_last float32 N x 3 x H x W device tensor")
+    b = _need(bias, "bias")
+    if b.numel() != 64:
+        raise ValueError("bias must have 64 entries")
+    Hc, Wc = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    Ho, Wo = (Hc - 1) // 2 + 1, (Wc - 1) // 2 + 1
+    out = torch.empty((N, 64, Ho, Wo), dtype=torch.float32, device=x.device,
+                      memory_format=torch.channels_last)
+    check(lib().vd_stem_conv_pool(x.data_ptr(), N, H, W, packed.data_ptr(), b.data_ptr(),
+                                  out.data_ptr(), _stream()), "vd_stem_conv_pool")
+    return out
+
+
 def rpn_head(x_raw: torch.Tensor, conv_bias: torch.Tensor, w: torch.Tensor, b: torch.Tensor,
              num_anchors: int):
     """FPN RPN head of one level (vd_rpn_head): x_raw = the shared 3x3 conv's
