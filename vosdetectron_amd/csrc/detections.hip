@@ -303,12 +303,18 @@ struct ClsLds {
     int *cand;
     float *cx1, *cy1, *cx2, *cy2, *csc, *ox1, *oy1, *ox2, *oy2, *oar;
     uint8_t *keep_rank, *keep_t;
+    uint64_t *lmask;  // kClsLdsRows x kClsLdsRows / 64 words
     float *wts;
     int *scratch;
 };
 
+// classes with at most kClsLdsRows candidates (the common case) build and
+// resolve their suppression mask in LDS instead of the global workspace
+static constexpr int kClsLdsRows = 256;
+
 __host__ __device__ inline size_t cls_lds_bytes(int cap) {
-    return (size_t)cap * (8 + 4 + 10 * 4 + 2) + 4 * 4 + 32 * 4;
+    return (size_t)cap * (8 + 4 + 10 * 4 + 2) + 4 * 4 + 32 * 4 + 16 +
+           (size_t)kClsLdsRows * (kClsLdsRows / 64) * 8;
 }
 
 __device__ inline ClsLds cls_lds(char *p, int cap) {
@@ -328,6 +334,9 @@ __device__ inline ClsLds cls_lds(char *p, int cap) {
     p += 128;
     L.keep_rank = reinterpret_cast<uint8_t *>(p);
     L.keep_t = L.keep_rank + cap;
+    p += 2 * (size_t)cap;
+    p = reinterpret_cast<char *>((reinterpret_cast<uintptr_t>(p) + 15) & ~(uintptr_t)15);
+    L.lmask = reinterpret_cast<uint64_t *>(p);
     return L;
 }
 
@@ -407,7 +416,7 @@ __global__ __launch_bounds__(1024) void class_nms_kernel(
         }
         __syncthreads();
         const size_t words = (size_t)(R_cap + 63) / 64;
-        uint64_t *mask = ws.mask + slot * (size_t)R_cap * words;
+        uint64_t *mask = m <= kClsLdsRows ? L.lmask : ws.mask + slot * (size_t)R_cap * words;
         nms_build_mask_rows(L.ox1, L.oy1, L.ox2, L.oy2, L.oar, m, nms_thresh, mask, wave_id(),
                             num_waves());
         __threadfence_block();

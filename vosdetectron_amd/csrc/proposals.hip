@@ -160,9 +160,12 @@ struct RpnLds {
 #define PROF_DUMP(tag)
 #endif
 
+#ifndef VD_SWEEP_U
+#define VD_SWEEP_U 8
+#endif
 template <class F>
 __device__ inline void sweep_probs(const float *__restrict__ probs, int n, F f) {
-    constexpr int U = 8;
+    constexpr int U = VD_SWEEP_U;
     const int bd = blockDim.x;
     int m = threadIdx.x;
     // full batches: every lane of the block has all U elements
