@@ -373,7 +373,7 @@ class _StemEpilogue(nn.Module):
 
     def _fused_ok(self, x):
         c = self.conv1
-        return (os.environ.get("VOSDET_STEM", "miopen") == "fused" and c.bias is not None
+        return (os.environ.get("VOSDET_STEM", "fused") == "fused" and c.bias is not None
                 and tuple(c.weight.shape) == (64, 3, 7, 7) and c.stride == (2, 2)
                 and c.padding == (3, 3) and c.dilation == (1, 1) and c.groups == 1
                 and x.shape[1] == 3 and x.is_contiguous(memory_format=torch.channels_last)
