@@ -303,18 +303,12 @@ struct ClsLds {
     int *cand;
     float *cx1, *cy1, *cx2, *cy2, *csc, *ox1, *oy1, *ox2, *oy2, *oar;
     uint8_t *keep_rank, *keep_t;
-    uint64_t *lmask;  // kClsLdsRows x kClsLdsRows / 64 words
     float *wts;
     int *scratch;
 };
 
-// classes with at most kClsLdsRows candidates (the common case) build and
-// resolve their suppression mask in LDS instead of the global workspace
-static constexpr int kClsLdsRows = 256;
-
 __host__ __device__ inline size_t cls_lds_bytes(int cap) {
-    return (size_t)cap * (8 + 4 + 10 * 4 + 2) + 4 * 4 + 32 * 4 + 16 +
-           (size_t)kClsLdsRows * (kClsLdsRows / 64) * 8;
+    return (size_t)cap * (8 + 4 + 10 * 4 + 2) + 4 * 4 + 32 * 4;
 }
 
 __device__ inline ClsLds cls_lds(char *p, int cap) {
@@ -334,9 +328,6 @@ __device__ inline ClsLds cls_lds(char *p, int cap) {
     p += 128;
     L.keep_rank = reinterpret_cast<uint8_t *>(p);
     L.keep_t = L.keep_rank + cap;
-    p += 2 * (size_t)cap;
-    p = reinterpret_cast<char *>((reinterpret_cast<uintptr_t>(p) + 15) & ~(uintptr_t)15);
-    L.lmask = reinterpret_cast<uint64_t *>(p);
     return L;
 }
 
@@ -416,7 +407,7 @@ __global__ __launch_bounds__(1024) void class_nms_kernel(
         }
         __syncthreads();
         const size_t words = (size_t)(R_cap + 63) / 64;
-        uint64_t *mask = m <= kClsLdsRows ? L.lmask : ws.mask + slot * (size_t)R_cap * words;
+        uint64_t *mask = ws.mask + slot * (size_t)R_cap * words;
         nms_build_mask_rows(L.ox1, L.oy1, L.ox2, L.oy2, L.oar, m, nms_thresh, mask, wave_id(),
                             num_waves());
         __threadfence_block();
@@ -459,6 +450,8 @@ __global__ __launch_bounds__(1024) void class_nms_kernel(
     if (threadIdx.x == 0) ws.cls_count[slot] = kept;
 }
 
+static constexpr int kLimStage = 16384;  // scores staged in LDS by det_limit_kernel
+
 __global__ __launch_bounds__(1024) void det_limit_kernel(const int32_t *__restrict__ roi_count,
                                                           int R_cap, int K, int dets_per_im,
                                                           int det_cap, DetWs ws,
@@ -468,6 +461,7 @@ __global__ __launch_bounds__(1024) void det_limit_kernel(const int32_t *__restri
     __shared__ int offs[1025];
     __shared__ uint32_t hist[256];
     __shared__ int scratch[32];
+    __shared__ float stage[kLimStage];
     const int img = blockIdx.x;
     if (roi_count[img] < 0) {  // proposal selection failed upstream: propagate, never hide
         if (threadIdx.x == 0) det_count_out[img] = -1;
@@ -497,7 +491,19 @@ __global__ __launch_bounds__(1024) void det_limit_kernel(const int32_t *__restri
         jj = lo;
         u = q - offs[lo - 1];
     };
+    // the radix select reads every score four times and the compaction once:
+    // staged in LDS (one parallel gather) when they fit, else read in place
+    const bool staged = total <= kLimStage;
+    if (staged) {
+        for (int q = threadIdx.x; q < total; q += blockDim.x) {
+            int jj, u;
+            at(q, jj, u);
+            stage[q] = ws.cls_dets[(((size_t)img * K + jj) * R_cap + u) * 5 + 4];
+        }
+        __syncthreads();
+    }
     auto score = [&](int q) -> float {
+        if (staged) return stage[q];
         int jj, u;
         at(q, jj, u);
         return ws.cls_dets[(((size_t)img * K + jj) * R_cap + u) * 5 + 4];
