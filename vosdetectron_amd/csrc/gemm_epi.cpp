@@ -50,7 +50,19 @@ namespace vd {
 
 namespace {
 
-constexpr int kMaxAlgos = 16, kSearchReps = 3;
+constexpr int kMaxAlgos = 64, kSearchReps = 3;
+// candidates asked of the heuristic (VOSDET_GEMM_MAXALGOS, default 16, <= kMaxAlgos):
+// pinned indices name entries of this list
+int max_algos() {
+    static int n = 0;
+    if (!n) {
+        const char *e = getenv("VOSDET_GEMM_MAXALGOS");
+        n = e ? atoi(e) : 16;
+        if (n < 1) n = 1;
+        if (n > kMaxAlgos) n = kMaxAlgos;
+    }
+    return n;
+}
 
 struct Plan {
     hipblasLtMatmulDesc_t op = nullptr;
@@ -187,7 +199,7 @@ Plan *plan_for(int M, int N, int K, int relu, int has_res) {
                                           sizeof(wsmax));
     int n = 0;
     const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(h, p.op, p.a, p.b, p.c, p.c, pref,
-                                                               kMaxAlgos, p.cand, &n);
+                                                               max_algos(), p.cand, &n);
     hipblasLtMatmulPreferenceDestroy(pref);
     if (st != HIPBLAS_STATUS_SUCCESS || n < 1) return nullptr;
     p.ncand = n;
