@@ -222,14 +222,38 @@ __device__ inline uint32_t block_kth_largest(int n, int k, Key key, uint32_t *hi
             }
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            int acc = 0, digit = 0;
-            for (int b = 255; b >= 0; --b) {
-                if (acc + (int)hist[b] >= need) { digit = b; break; }
-                acc += hist[b];
+        if (threadIdx.x < 64) {
+            // the digit holding the need-th largest key, by the first wave: lane l
+            // owns bins 255 - 4l .. 252 - 4l (highest first), a wave prefix sum over
+            // the lanes' totals, and the first lane whose prefix reaches `need`
+            // walks its four bins (one thread walking all 256 bins serially cost
+            // ~40 us per launch in LDS round trips)
+            const int l = threadIdx.x;
+            int h[4], tot = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                h[i] = (int)hist[255 - 4 * l - i];
+                tot += h[i];
             }
-            scratch[0] = digit;
-            scratch[1] = need - acc;
+            int incl = tot;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(incl, o);
+                if (l >= o) incl += v;
+            }
+            const int excl = incl - tot;
+            const uint64_t hit = ballot(incl >= need);
+            const int first = hit ? __ffsll((unsigned long long)hit) - 1 : 63;
+            if (l == first) {
+                int acc = excl, digit = 255 - 4 * l - 3;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (acc + h[i] >= need) { digit = 255 - 4 * l - i; break; }
+                    acc += h[i];
+                }
+                scratch[0] = digit;
+                scratch[1] = need - acc;
+            }
         }
         __syncthreads();
         prefix |= (uint32_t)scratch[0] << shift;

@@ -28,7 +28,6 @@
 namespace vd {
 
 static constexpr int kSelCap = 8192;      // candidate keys held in LDS
-static constexpr int kCollectCand = 2048;  // collect: keys at or above the top-R score
 static constexpr int kPreMax = 2048;      // pre_nms_topN per level
 static constexpr int kSampleMax = 2048;
 // Large variant (single-scale C4 RPN: 15 anchors, TEST.RPN_PRE_NMS_TOP_N 6000,
@@ -589,9 +588,6 @@ __global__ __launch_bounds__(1024) void collect_distribute_kernel(
     int k_min, int k_max, float *__restrict__ rois_out, int32_t *__restrict__ lvl_out,
     int32_t *__restrict__ count_out) {
     __shared__ uint64_t keys[kSelCap];
-    __shared__ uint64_t cand[kCollectCand];
-    __shared__ uint32_t hist[256];
-    __shared__ int scratch[32];
     __shared__ int offs[VD_MAX_LEVELS + 1];
     __shared__ int failed;
     const int img = blockIdx.x;
@@ -623,30 +619,10 @@ __global__ __launch_bounds__(1024) void collect_distribute_kernel(
         keys[q] = k;
     }
     __syncthreads();
+    bitonic_sort_desc(keys, np2);
     const int R = min(n, post_nms_topN);
-    // the top R by the unique key: a radix select of the R-th largest score
-    // bounds the candidates (ties at it included), which alone are sorted; a
-    // tie-heavy input that overflows the candidate buffer sorts everything
-    const uint64_t *top = keys;
-    bool full = true;
-    if (n > R) {
-        const uint32_t t32 = block_kth_largest(
-            n, R, [&](int i) { return (uint32_t)(keys[i] >> 32); }, hist, scratch);
-        const int c = block_compact(
-            n, [&](int i) { return (uint32_t)(keys[i] >> 32) >= t32; },
-            [&](int pos, int i) { if (pos < kCollectCand) cand[pos] = keys[i]; }, scratch);
-        if (c <= kCollectCand) {
-            const int cp2 = next_pow2(c < 1 ? 1 : c);
-            for (int i = c + threadIdx.x; i < cp2; i += blockDim.x) cand[i] = 0ull;
-            __syncthreads();
-            bitonic_sort_desc(cand, cp2);
-            top = cand;
-            full = false;
-        }
-    }
-    if (full) bitonic_sort_desc(keys, np2);
     for (int r = threadIdx.x; r < R; r += blockDim.x) {
-        const int q = (int)(0xffffffffu - (uint32_t)top[r]);
+        const int q = (int)(0xffffffffu - (uint32_t)keys[r]);
         int l = 0;
         while (q >= offs[l + 1]) ++l;
         const int t = q - offs[l];

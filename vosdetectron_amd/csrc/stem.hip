@@ -35,7 +35,6 @@ constexpr int kThreads = 256;
 constexpr int kPB = 4;                                // conv-pixel blocks per wave
 constexpr int kPer = (kPatch + kThreads - 1) / kThreads;  // 16 patch floats per thread
 constexpr int kOutPitch = 68;                         // floats per conv pixel in LDS
-constexpr int kCo = 64;
 
 // patch offset (floats) of k = (ky, kx, ci) = 21 ky + 3 kx + ci; k = 147 is the
 // zero-weight pad and reads k = 146's (finite) value
