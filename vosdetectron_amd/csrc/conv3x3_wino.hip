@@ -157,16 +157,21 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
         psrc[i] = ok ? X + pix * C + 4 * h : X;
     }
     const float *zero = reinterpret_cast<const float *>(&g_wino_zero);
-#define VD_W2_DMA(CH, ST)                                                                    \
+#define VD_W2_DMA_U(CH, ST)                                                                  \
     {                                                                                        \
         const uint32_t d_ = sbase + (uint32_t)(ST) * k2StageB + (uint32_t)wave * 1024u;      \
         const float *u_ = usrc + (int64_t)(CH) * (16 * kCo * kKC);                           \
         _Pragma("unroll") for (int i = 0; i < 8; ++i)                                        \
             wino_dma_1k(u_ + i * 1024, d_ + (uint32_t)i * 4096u);                            \
+    }
+#define VD_W2_DMA_P(CH, ST)                                                                  \
+    {                                                                                        \
+        const uint32_t d_ = sbase + (uint32_t)(ST) * k2StageB + (uint32_t)wave * 1024u;      \
         _Pragma("unroll") for (int i = 0; i < 2; ++i)                                        \
             wino_dma_1k(pok[i] ? psrc[i] + (CH) * kKC : zero,                                \
                         d_ + (uint32_t)(k2USlots * 16) + (uint32_t)i * 4096u);               \
     }
+#define VD_W2_DMA(CH, ST) { VD_W2_DMA_U(CH, ST) VD_W2_DMA_P(CH, ST) }
     // transform reads: lane (j, q) -> tile 16 tg + j, channels 2q, 2q + 1 (half
     // q >> 1, dwords 2 (q & 1) ..): byte offsets within a stage
     const int vt = tg * 16 + j, tr = vt / TC, tc = vt % TC;
@@ -205,7 +210,10 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     wino_wait_barrier();
     for (int ch = 0; ch < nch; ++ch) {
         const int s = ch & 1;
-        if (!(PR & 1) && ch + 1 < nch) VD_W2_DMA(ch + 1, s ^ 1)
+        if (!(PR & 1) && ch + 1 < nch) {
+            if (!(PR & 16)) VD_W2_DMA_U(ch + 1, s ^ 1)
+            if (!(PR & 32)) VD_W2_DMA_P(ch + 1, s ^ 1)
+        }
         const char *stb = reinterpret_cast<const char *>(sm) + s * k2StageB;
         // V = B^T d B for the lane's two channels, B^T = [1 0 -1 0; 0 1 1 0;
         // 0 -1 1 0; 0 1 0 -1]
@@ -266,6 +274,8 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
         if (!(PR & 4)) wino_wait_barrier();  // DMA of chunk ch + 1 landed; stage s read
     }
 #undef VD_W2_DMA
+#undef VD_W2_DMA_U
+#undef VD_W2_DMA_P
     // output transform (lane-local): A^T = [1 1 1 0; 0 1 -1 -1]; lane (j, q),
     // accumulator slot r holds channel n0 + cg*32 + 16 t2 + 4 q + r of tile 16 tg + j
     const int oy = oy0 + 2 * tr, ox = ox0 + 2 * tc;
@@ -383,18 +393,17 @@ int launch_wino(const float *X, int N, int H, int W, int C, const float *U, int 
     auto kern = sq ? (relu ? conv3x3_wino2_kernel<true, 8> : conv3x3_wino2_kernel<false, 8>)
                    : (relu ? conv3x3_wino2_kernel<true, 16> : conv3x3_wino2_kernel<false, 16>);
 #ifdef VD_RESEARCH_PROBES
-    // speed-of-light probes (wrong results; tools/wino_sol_probe.py): 1 no DMA, 2 no
-    // patch reads, 4 no barrier, 8 no U reads.  Only in a research build
+    // speed-of-light probes (wrong results; tools/research/wino_sol_probe.py): 1 no DMA,
+    // 2 no patch reads, 4 no barrier, 8 no U reads, 16 no U DMA, 32 no patch DMA.  Only in a research build
     // (make VD_RESEARCH=1), never in the product library: a stray environment
     // variable must not be able to corrupt a product convolution.
     const char *pe = getenv("VOSDET_WINO_PROBE");
-    switch (pe && !sq && !relu ? atoi(pe) : 0) {
-        case 1: kern = conv3x3_wino2_kernel<false, 16, 1>; break;
-        case 2: kern = conv3x3_wino2_kernel<false, 16, 2>; break;
-        case 4: kern = conv3x3_wino2_kernel<false, 16, 4>; break;
-        case 8: kern = conv3x3_wino2_kernel<false, 16, 8>; break;
-        case 5: kern = conv3x3_wino2_kernel<false, 16, 5>; break;
-        case 15: kern = conv3x3_wino2_kernel<false, 16, 15>; break;
+    switch (pe && !relu ? atoi(pe) : 0) {
+#define VD_PROBE_CASE(B) \
+        case B: kern = sq ? conv3x3_wino2_kernel<false, 8, B> : conv3x3_wino2_kernel<false, 16, B>; break;
+        VD_PROBE_CASE(1) VD_PROBE_CASE(2) VD_PROBE_CASE(4) VD_PROBE_CASE(8) VD_PROBE_CASE(5)
+        VD_PROBE_CASE(15) VD_PROBE_CASE(16) VD_PROBE_CASE(32) VD_PROBE_CASE(20) VD_PROBE_CASE(36)
+#undef VD_PROBE_CASE
         default: break;
     }
 #endif
