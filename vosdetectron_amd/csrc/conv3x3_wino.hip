@@ -13,7 +13,7 @@
 //
 // Workgroup = 4 waves, 32 tiles (2 x 16 tiles = 4 x 32 output pixels of one
 // image, or 4 x 8 tiles = 8 x 16 pixels for maps <= 16 wide: the 14 x 14 mask-head
-// RoIs) x 64 output channels, 80 KiB of LDS, so TWO workgroups share a CU and the
+// RoIs) x 64 output channels, two waves per SIMD (240-246 VGPRs), so TWO workgroups share a CU and the
 // barrier / transform gaps of one are filled by the MFMAs of the other (the
 // round-3 one-per-CU 8-wave form, 64 tiles and 150 KiB, ran 7-12 % slower on every
 // benched shape in one-process A/B: profiles/r03_wino_ab.json).  Wave w owns 16 tiles (w & 1) x
@@ -21,10 +21,16 @@
 // and a lane's 16 position values of one (channel, tile) sit in the same register
 // slot of its 16 accumulators, so the output transform is lane-local.
 //
-// K is walked in chunks of 8 input channels.  Per chunk U's slice [16][64][8] and
-// the raw input patch are copied HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4,
-// no VGPR round trip; inline asm so hipcc does not drain it at every LDS read),
-// double-buffered, one barrier per chunk.  The input transform needs no LDS round
+// K is walked in chunks of 8 input channels.  Per chunk the raw input patch is
+// copied HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip),
+// double-buffered (16 KiB), one barrier per chunk; each wave's U operand (the 16
+// positions x its 32 channels x 8 input channels, 64 VGPRs) comes straight from L2
+// into registers, each fragment reloaded for the next chunk right after its MFMAs
+// consumed it.  (U through LDS -- its 32 KiB slice LDS-DMA'd per chunk and read back
+// -- ran 5-13 % slower on every benched shape, bit-identical:
+// profiles/r04/wino_ureg_ab.jsonl.)  All of the loop's vector-memory ops are inline
+// asm, so hipcc neither drains them at LDS reads nor counts them: the loop waits
+// with its own vmcnt.  The input transform needs no LDS round
 // trip: the MFMA B fragment of lane (j, q) is V[pos][channels 2q, 2q + 1][tile j]
 // -- the 4 x 4 transform of tile j's patch for those two channels -- so every lane
 // transforms its own fragment from the patch into registers (v_pk_add_f32 on the
@@ -46,18 +52,11 @@ constexpr int kCo = 64;  // output channels per workgroup
 constexpr int kKC = 8;   // input channels per chunk
 constexpr int k2Tiles = 32;
 constexpr int k2Threads = 256;
-constexpr int k2USlots = 16 * kCo * 2;                // 16-B slots: U slice [pos][co][8]
-constexpr int k2PSlots = 512;                         // patch slots (480 used)
-constexpr int k2StageB = (k2USlots + k2PSlots) * 16;  // 40,960 B; two stages = 80 KiB
+constexpr int k2PSlots = 512;              // patch slots (480 used)
+constexpr int k2StageB = k2PSlots * 16;  // 8 KiB; two stages
+constexpr int kUChunk = 16 * kCo * kKC;  // floats of U per (channel block, chunk)
 
 __device__ float4 g_wino_zero;  // the source of out-of-image patch taps
-
-// U's channel order within each 8-channel block (the weight transform writes it,
-// the DMA copies it verbatim): 8-byte unit u of row co holds channels 2 (u ^
-// sw_unit(co)) and 2 (u ^ sw_unit(co)) + 1, so the 16 lanes of a paired fragment
-// read (ds_read2st64_b64: 16 lanes over 32 banks; rows co = j, 32 B apart) hit 16
-// distinct 8-byte bank pairs -- unswizzled they are 4-way conflicted
-__device__ __forceinline__ int sw_unit(int co) { return (co >> 2) & 3; }
 
 template <int TC>
 struct Patch2 {  // patch [row][half][column] in 16-B slots
@@ -95,6 +94,22 @@ __device__ __forceinline__ void wino_wait_barrier() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// One 16-B U fragment per lane, global -> VGPR: wave-uniform SGPR base + lane
+// offset (no per-load 64-bit VALU address arithmetic).  Inline asm so the
+// compiler neither drains it nor moves it around the LDS-DMAs; the tied operand
+// keeps the fragment in the register its MFMAs read.  The caller counts vmcnt.
+__device__ __forceinline__ void wino_load_u(f4v &r, const float *ub, uint32_t voff) {
+    asm volatile("global_load_dwordx4 %0, %1, %2" : "+v"(r) : "v"(voff), "s"(ub) : "memory");
+}
+// All but the last 16 vector-memory ops of this wave retired; the two fragments
+// pass through so their MFMAs cannot be scheduled above the wait.
+__device__ __forceinline__ void wino_wait_u(f4v &a, f4v &b) {
+    asm volatile("s_waitcnt vmcnt(16)" : "+v"(a), "+v"(b) : : "memory");
+}
+__device__ __forceinline__ void wino_wait16_barrier() {
+    asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 template <bool RELU, int TC, int PR = 0>
 __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
@@ -128,11 +143,7 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     const int tg = wave & 1, cg = wave >> 1;  // wave: tiles 16 tg .. + 15, 32-channel group
     const uint32_t sbase = (uint32_t)(uintptr_t)sm;
 
-    // U DMA: U is stored chunk-blocked, [Cout / 64][C / 8][16][64][8], so a
-    // chunk's slice is one contiguous 32 KiB run copied verbatim (whole cache
-    // lines per wave instruction); blocks b = wave + 4 i (i < 8) of 64 slots
     const int nch = C / kKC;
-    const float *usrc = U + (int64_t)cb * nch * (16 * kCo * kKC) + wave * 256 + lane * 4;
     // patch DMA: blocks b = wave + 4 i (i < 2); slots outside the patch or the
     // image copy zeros
     const float *psrc[2];
@@ -157,21 +168,12 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
         psrc[i] = ok ? X + pix * C + 4 * h : X;
     }
     const float *zero = reinterpret_cast<const float *>(&g_wino_zero);
-#define VD_W2_DMA_U(CH, ST)                                                                  \
-    {                                                                                        \
-        const uint32_t d_ = sbase + (uint32_t)(ST) * k2StageB + (uint32_t)wave * 1024u;      \
-        const float *u_ = usrc + (int64_t)(CH) * (16 * kCo * kKC);                           \
-        _Pragma("unroll") for (int i = 0; i < 8; ++i)                                        \
-            wino_dma_1k(u_ + i * 1024, d_ + (uint32_t)i * 4096u);                            \
-    }
 #define VD_W2_DMA_P(CH, ST)                                                                  \
-    {                                                                                        \
+    if (!(PR & 32)) {                                                                        \
         const uint32_t d_ = sbase + (uint32_t)(ST) * k2StageB + (uint32_t)wave * 1024u;      \
         _Pragma("unroll") for (int i = 0; i < 2; ++i)                                        \
-            wino_dma_1k(pok[i] ? psrc[i] + (CH) * kKC : zero,                                \
-                        d_ + (uint32_t)(k2USlots * 16) + (uint32_t)i * 4096u);               \
+            wino_dma_1k(pok[i] ? psrc[i] + (CH) * kKC : zero, d_ + (uint32_t)i * 4096u);     \
     }
-#define VD_W2_DMA(CH, ST) { VD_W2_DMA_U(CH, ST) VD_W2_DMA_P(CH, ST) }
     // transform reads: lane (j, q) -> tile 16 tg + j, channels 2q, 2q + 1 (half
     // q >> 1, dwords 2 (q & 1) ..): byte offsets within a stage
     const int vt = tg * 16 + j, tr = vt / TC, tc = vt % TC;
@@ -192,13 +194,7 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     for (int a = 0; a < 4; ++a) {
         const int r = 2 * tr + a, p = 2 * tc + a;
         roff[a] = 16 * (r * PG::kRP + ((r >> 1) & 1));
-        coff[a] = 16 * (p + (p >> 4)) + 16 * (q >> 1) * PG::kHP + 8 * (q & 1) + k2USlots * 16;
-    }
-    int ufo[2];  // U fragment float offsets: channel cg*32 + 16 tc + j, channels 2q, 2q + 1
-#pragma unroll
-    for (int t2 = 0; t2 < 2; ++t2) {
-        const int co = cg * 32 + 16 * t2 + j;
-        ufo[t2] = co * kKC + 2 * (q ^ sw_unit(co));
+        coff[a] = 16 * (p + (p >> 4)) + 16 * (q >> 1) * PG::kHP + 8 * (q & 1);
     }
     f4v acc[16][2];
 #pragma unroll
@@ -206,14 +202,25 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
 #pragma unroll
         for (int t2 = 0; t2 < 2; ++t2) acc[p][t2] = f4v{0.f, 0.f, 0.f, 0.f};
 
-    VD_W2_DMA(0, 0)
+    // the wave's U fragments of one chunk (weight order [Cout / 64][C / 8][cg][l][lane][4],
+    // wino_weight_kernel): fragment l = 2 pp + t2 holds positions 2 pp, 2 pp + 1 x
+    // channels 2q, 2q + 1 of output channel cg*32 + 16 t2 + j -- 1 KiB per wave load
+    f4v ur[16];
+    const float *ursrc = U + ((int64_t)cb * nch * 2 + cg) * (kUChunk / 2);
+    const uint32_t uvoff = (uint32_t)lane * 16u;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) ur[l] = f4v{0.f, 0.f, 0.f, 0.f};
+    VD_W2_DMA_P(0, 0)
+#pragma unroll
+    for (int l = 0; l < 16; ++l) wino_load_u(ur[l], ursrc + l * 256, uvoff);
     wino_wait_barrier();
     for (int ch = 0; ch < nch; ++ch) {
         const int s = ch & 1;
-        if (!(PR & 1) && ch + 1 < nch) {
-            if (!(PR & 16)) VD_W2_DMA_U(ch + 1, s ^ 1)
-            if (!(PR & 32)) VD_W2_DMA_P(ch + 1, s ^ 1)
-        }
+        // every chunk issues 2 patch DMAs, then 16 U loads (the last chunk re-copies
+        // itself into the idle stage and reloads its own U), so in-order vmcnt
+        // makes every wait below vmcnt(16)
+        const int nxt = ch + 1 < nch ? ch + 1 : ch;
+        VD_W2_DMA_P(nxt, s ^ 1)
         const char *stb = reinterpret_cast<const char *>(sm) + s * k2StageB;
         // V = B^T d B for the lane's two channels, B^T = [1 0 -1 0; 0 1 1 0;
         // 0 -1 1 0; 0 1 0 -1]
@@ -248,33 +255,38 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
             b[4 * a + 2] = d[a][2] - d[a][1];
             b[4 * a + 3] = d[a][1] - d[a][3];
         }
-        const float *st = reinterpret_cast<const float *>(stb);
+        {
+            const float *un = ursrc + (int64_t)nxt * kUChunk;
 #pragma unroll
-        for (int p0 = 0; p0 < 16; p0 += 2) {
-            f2v af[2][2];
+            for (int pp = 0; pp < 8; ++pp) {
+                // fragments 2 pp, 2 pp + 1 of this chunk landed: after them this wave
+                // issued the other 14, the next chunk's 2 patch DMAs and 2 pp U loads
+                wino_wait_u(ur[2 * pp], ur[2 * pp + 1]);
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int t2 = 0; t2 < 2; ++t2)
-                    af[i][t2] = (PR & 8) ? b[p0 + i + t2]
-                                         : *reinterpret_cast<const f2v *>(st + (p0 + i) * kCo * kKC + ufo[t2]);
+                    for (int t2 = 0; t2 < 2; ++t2)
+                        acc[2 * pp + i][t2] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                            i ? ur[2 * pp + t2].z : ur[2 * pp + t2].x, b[2 * pp + i].x,
+                            acc[2 * pp + i][t2], 0, 0, 0);
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int t2 = 0; t2 < 2; ++t2)
-                    acc[p0 + i][t2] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                        af[i][t2].x, b[p0 + i].x, acc[p0 + i][t2], 0, 0, 0);
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int t2 = 0; t2 < 2; ++t2)
-                    acc[p0 + i][t2] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                        af[i][t2].y, b[p0 + i].y, acc[p0 + i][t2], 0, 0, 0);
+                    for (int t2 = 0; t2 < 2; ++t2)
+                        acc[2 * pp + i][t2] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                            i ? ur[2 * pp + t2].w : ur[2 * pp + t2].y, b[2 * pp + i].y,
+                            acc[2 * pp + i][t2], 0, 0, 0);
+                if (!(PR & 8)) {
+                    wino_load_u(ur[2 * pp], un + (2 * pp) * 256, uvoff);
+                    wino_load_u(ur[2 * pp + 1], un + (2 * pp + 1) * 256, uvoff);
+                }
+            }
         }
-        if (!(PR & 4)) wino_wait_barrier();  // DMA of chunk ch + 1 landed; stage s read
+        // the next chunk's patch DMAs landed (16 U loads were issued after them) and
+        // stage s read by every wave
+        if (!(PR & 4)) wino_wait16_barrier();
     }
-#undef VD_W2_DMA
-#undef VD_W2_DMA_U
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the wave
 #undef VD_W2_DMA_P
     // output transform (lane-local): A^T = [1 1 1 0; 0 1 -1 -1]; lane (j, q),
     // accumulator slot r holds channel n0 + cg*32 + 16 t2 + 4 q + r of tile 16 tg + j
@@ -322,17 +334,17 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
 }
 
 // U = G g G^T of the PyTorch weight w[co][ci][3][3], G = [1 0 0; .5 .5 .5;
-// .5 -.5 .5; 0 0 1], float64, rounded once; stored chunk-blocked as
-// [co / 64][ci / 8][pos][co % 64][ci'] with ci' = ci % 8 with its 8-byte unit
-// swizzled by sw_unit(co).
+// .5 -.5 .5; 0 0 1], float64, rounded once; stored in the kernel's register-fragment
+// order [co / 64][ci / 8][cg][l][lane][4]: cg = co % 64 / 32, fragment l = 2 (pos / 2)
+// + co % 32 / 16, lane = 16 (ci % 8 / 2) + co % 16, element 2 (pos & 1) + (ci & 1).
 __global__ void wino_weight_kernel(const float *__restrict__ w, int Cout, int C,
                                    float *__restrict__ U) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)Cout * C) return;
     const int co = (int)(i / C), ci = (int)(i - (int64_t)(i / C) * C);
-    const int cs = ((((ci >> 1) & 3) ^ sw_unit(co)) << 1) | (ci & 1);
-    float *dst = U + ((int64_t)(co / kCo) * (C / kKC) + ci / kKC) * (16 * kCo * kKC) +
-                 (co % kCo) * kKC + cs;
+    const int cl = co % kCo;
+    float *dst = U + ((int64_t)(co / kCo) * (C / kKC) + ci / kKC) * kUChunk + (cl >> 5) * 4096 +
+                 ((cl >> 4) & 1) * 256 + (16 * ((ci & 7) >> 1) + (cl & 15)) * 4 + (ci & 1);
     const float *g = w + i * 9;
     double t[4][3];  // G g
     for (int c = 0; c < 3; ++c) {
@@ -345,8 +357,10 @@ __global__ void wino_weight_kernel(const float *__restrict__ w, int Cout, int C,
     for (int a = 0; a < 4; ++a) {
         const double u[4] = {t[a][0], 0.5 * (t[a][0] + t[a][1] + t[a][2]),
                              0.5 * (t[a][0] - t[a][1] + t[a][2]), t[a][2]};
-        for (int b = 0; b < 4; ++b)
-            dst[(4 * a + b) * kCo * kKC] = (float)u[b];
+        for (int b = 0; b < 4; ++b) {
+            const int pos = 4 * a + b;
+            dst[(pos >> 1) * 512 + (pos & 1) * 2] = (float)u[b];
+        }
     }
 }
 
@@ -393,16 +407,16 @@ int launch_wino(const float *X, int N, int H, int W, int C, const float *U, int 
     auto kern = sq ? (relu ? conv3x3_wino2_kernel<true, 8> : conv3x3_wino2_kernel<false, 8>)
                    : (relu ? conv3x3_wino2_kernel<true, 16> : conv3x3_wino2_kernel<false, 16>);
 #ifdef VD_RESEARCH_PROBES
-    // speed-of-light probes (wrong results; tools/research/wino_sol_probe.py): 1 no DMA,
-    // 2 no patch reads, 4 no barrier, 8 no U reads, 16 no U DMA, 32 no patch DMA.  Only in a research build
+    // speed-of-light probes (wrong results; tools/research/wino_sol_probe.py): 2 no
+    // patch reads, 4 no barrier, 8 no U loads, 32 no patch DMA.  Only in a research build
     // (make VD_RESEARCH=1), never in the product library: a stray environment
     // variable must not be able to corrupt a product convolution.
     const char *pe = getenv("VOSDET_WINO_PROBE");
     switch (pe && !relu ? atoi(pe) : 0) {
 #define VD_PROBE_CASE(B) \
         case B: kern = sq ? conv3x3_wino2_kernel<false, 8, B> : conv3x3_wino2_kernel<false, 16, B>; break;
-        VD_PROBE_CASE(1) VD_PROBE_CASE(2) VD_PROBE_CASE(4) VD_PROBE_CASE(8) VD_PROBE_CASE(5)
-        VD_PROBE_CASE(15) VD_PROBE_CASE(16) VD_PROBE_CASE(32) VD_PROBE_CASE(20) VD_PROBE_CASE(36)
+        VD_PROBE_CASE(2) VD_PROBE_CASE(4) VD_PROBE_CASE(8) VD_PROBE_CASE(32) VD_PROBE_CASE(36)
+        VD_PROBE_CASE(12) VD_PROBE_CASE(46)
 #undef VD_PROBE_CASE
         default: break;
     }

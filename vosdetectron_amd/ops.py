@@ -570,8 +570,9 @@ def conv3x3_bias_act(x: torch.Tensor, w2: torch.Tensor, bias: Optional[torch.Ten
 
 def conv3x3_wino_weight(w: torch.Tensor) -> Optional[torch.Tensor]:
     """PyTorch conv weight [Cout][Cin][3][3] -> the Winograd F(2x2,3x3) operand
-    U = G g G^T, chunk-blocked as [Cout/64][Cin/8][16][64][8] (channel pairs
-    swizzled within a row; vd_conv3x3_wino_weight; once per model).  None for
+    U = G g G^T in the kernel's register-fragment order [Cout/64][Cin/8][2][16][64][4]
+    (32-channel group, fragment, lane, 2 positions x 2 channels;
+    vd_conv3x3_wino_weight; once per model).  None for
     a shape the kernel does not serve (Cout % 64, Cin % 8)."""
     w_ = _need(w, "w")
     if w_.dim() != 4 or tuple(w_.shape[2:]) != (3, 3):
@@ -579,7 +580,7 @@ def conv3x3_wino_weight(w: torch.Tensor) -> Optional[torch.Tensor]:
     Cout, C = w_.shape[:2]
     if Cout % 64 or C % 8 or Cout == 0 or C == 0:
         return None
-    u = torch.empty((Cout // 64, C // 8, 16, 64, 8), dtype=torch.float32, device=w_.device)
+    u = torch.empty((Cout // 64, C // 8, 2, 16, 64, 4), dtype=torch.float32, device=w_.device)
     check(lib().vd_conv3x3_wino_weight(w_.data_ptr(), Cout, C, u.data_ptr(), _stream()),
           "vd_conv3x3_wino_weight")
     return u
@@ -603,8 +604,8 @@ def conv3x3_wino_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch
         return None
     u_ = _need(u, "u")
     N, C, H, W = x.shape
-    if u_.dim() != 5 or tuple(u_.shape[1:]) != (C // 8, 16, 64, 8) or C % 8:
-        raise ValueError("u must be [Cout/64][%d][16][64][8], got %s" % (C // 8, tuple(u_.shape)))
+    if u_.dim() != 6 or tuple(u_.shape[1:]) != (C // 8, 2, 16, 64, 4) or C % 8:
+        raise ValueError("u must be [Cout/64][%d][2][16][64][4], got %s" % (C // 8, tuple(u_.shape)))
     Cout = u_.shape[0] * 64
     b_ = _need(bias, "bias") if bias is not None else None
     if out is None:
