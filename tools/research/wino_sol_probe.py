@@ -27,8 +27,8 @@ N, C, H, W = 16, 256, 200, 336
 x = torch.randn(N, C, H, W, device="cuda").contiguous(memory_format=torch.channels_last)
 u = ops.conv3x3_wino_weight(torch.randn(C, C, 3, 3, device="cuda"))
 rec = {}
-for pr in ["0", "1", "16", "32", "4", "20", "36", "5", "2", "8", "15"]:
+for pr in os.environ.get("PROBES", "0,2,4,8,32,36,12,46").split(","):
     os.environ["VOSDET_WINO_PROBE"] = pr
     rec[pr] = round(timed(lambda: ops.conv3x3_wino_bias_act(x, u, None)), 3)
 print(json.dumps({"shape": [N, C, H, W], "probe_ms": rec,
-                  "legend": "1 no DMA, 2 no patch reads, 4 no barrier, 8 no U reads, 16 no U DMA, 32 no patch DMA"}))
+                  "legend": "2 no patch reads, 4 no barrier, 8 no U loads, 32 no patch DMA"}))

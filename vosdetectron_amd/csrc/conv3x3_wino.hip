@@ -52,8 +52,9 @@ constexpr int kCo = 64;  // output channels per workgroup
 constexpr int kKC = 8;   // input channels per chunk
 constexpr int k2Tiles = 32;
 constexpr int k2Threads = 256;
-constexpr int k2PSlots = 512;              // patch slots (480 used)
-constexpr int k2StageB = k2PSlots * 16;  // 8 KiB; two stages
+constexpr int k2PDma = 512;               // patch slots copied per chunk (480 used)
+constexpr int k2PSlots = 576;             // + the all-zero row the masked taps read
+constexpr int k2StageB = k2PSlots * 16;  // 9 KiB; two stages
 constexpr int kUChunk = 16 * kCo * kKC;  // floats of U per (channel block, chunk)
 
 __device__ float4 g_wino_zero;  // the source of out-of-image patch taps
@@ -62,7 +63,11 @@ template <int TC>
 struct Patch2 {  // patch [row][half][column] in 16-B slots
     static constexpr int kTR = k2Tiles / TC, kPR = 2 * kTR + 2, kPC = 2 * TC + 2;
     static constexpr int kHP = TC == 16 ? 37 : 20, kRP = TC == 16 ? 80 : 48;
-    static_assert(kPR * kRP <= k2PSlots, "patch fits its LDS region");
+    static_assert(kPR * kRP <= k2PDma, "patch fits its DMA'd LDS region");
+    static_assert(kPR * kRP + kRP <= k2PSlots, "the zero row fits past it");
+    // first slot of a row past both halves (unused, so the DMA copies zeros there)
+    static constexpr int kZC = 2 * kHP;
+    static_assert(kZC + 3 <= kRP && kHP >= 2 * TC + 4, "zero column slots (+ half + row skew)");
     static_assert(kRP % 16 == 0, "row pitch: whole bank sweeps");
     // (p >> 4): columns 16 apart land 17 slots apart, so the 16 tiles of one
     // fragment read (pixel columns 2j + c) fall in distinct 16-B bank groups (one
@@ -94,6 +99,20 @@ __device__ __forceinline__ void wino_wait_barrier() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Packed fp32 a + b / a - b on a channel pair (v_pk_add_f32: both halves IEEE adds,
+// bit-identical to two v_add_f32; hipcc otherwise splits half the transform into
+// scalar adds)
+__device__ __forceinline__ f2v pk_add(f2v a, f2v b) {
+    f2v r;
+    asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f2v pk_sub(f2v a, f2v b) {
+    f2v r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // One 16-B U fragment per lane, global -> VGPR: wave-uniform SGPR base + lane
 // offset (no per-load 64-bit VALU address arithmetic).  Inline asm so the
 // compiler neither drains it nor moves it around the LDS-DMAs; the tied operand
@@ -109,6 +128,7 @@ __device__ __forceinline__ void wino_wait_u(f4v &a, f4v &b) {
 __device__ __forceinline__ void wino_wait16_barrier() {
     asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
+
 
 template <bool RELU, int TC, int PR = 0>
 __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
@@ -196,6 +216,18 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
         roff[a] = 16 * (r * PG::kRP + ((r >> 1) & 1));
         coff[a] = 16 * (p + (p >> 4)) + 16 * (q >> 1) * PG::kHP + 8 * (q & 1);
     }
+    // the masked taps read zeros from LDS rather than being zeroed per chunk: a masked
+    // row reads the all-zero row kPR (past the DMA'd slots, zeroed once here), a
+    // masked column the unused, DMA-zeroed slots kZC, kZC + 1 of its row (bit-identical
+    // to the per-chunk v_cndmask form it replaced, 2-6 % faster with the packed
+    // transform: profiles/r04/wino_zs/)
+    if (zero_top) roff[0] = 16 * PG::kPR * PG::kRP;
+    if (zero_bot) roff[3] = 16 * PG::kPR * PG::kRP;
+    if (zero_left) coff[0] = 16 * (PG::kZC + (q >> 1)) + 8 * (q & 1);
+    if (zero_right) coff[3] = 16 * (PG::kZC + (q >> 1)) + 8 * (q & 1);
+    if (tid < 2 * (k2PSlots - k2PDma))
+        reinterpret_cast<float4 *>(sm)[(tid / (k2PSlots - k2PDma)) * k2PSlots + k2PDma +
+                                       tid % (k2PSlots - k2PDma)] = make_float4(0.f, 0.f, 0.f, 0.f);
     f4v acc[16][2];
 #pragma unroll
     for (int p = 0; p < 16; ++p)
@@ -210,39 +242,22 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     const uint32_t uvoff = (uint32_t)lane * 16u;
 #pragma unroll
     for (int l = 0; l < 16; ++l) ur[l] = f4v{0.f, 0.f, 0.f, 0.f};
-    VD_W2_DMA_P(0, 0)
-#pragma unroll
-    for (int l = 0; l < 16; ++l) wino_load_u(ur[l], ursrc + l * 256, uvoff);
-    wino_wait_barrier();
-    for (int ch = 0; ch < nch; ++ch) {
-        const int s = ch & 1;
-        // every chunk issues 2 patch DMAs, then 16 U loads (the last chunk re-copies
-        // itself into the idle stage and reloads its own U), so in-order vmcnt
-        // makes every wait below vmcnt(16)
-        const int nxt = ch + 1 < nch ? ch + 1 : ch;
-        VD_W2_DMA_P(nxt, s ^ 1)
-        const char *stb = reinterpret_cast<const char *>(sm) + s * k2StageB;
-        // V = B^T d B for the lane's two channels, B^T = [1 0 -1 0; 0 1 1 0;
-        // 0 -1 1 0; 0 1 0 -1]
-        f2v d[4][4];
+    // the lane's 4 x 4 patch of one chunk (its two channels), LDS -> registers
+    auto read_d = [&](f2v(&d)[4][4], const char *stb) {
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
             for (int c = 0; c < 4; ++c)
                 d[a][c] = (PR & 2) ? f2v{(float)roff[a], (float)coff[c]}
                                    : *reinterpret_cast<const f2v *>(stb + roff[a] + coff[c]);
+    };
+    // V = B^T d B for the lane's two channels, B^T = [1 0 -1 0; 0 1 1 0;
+    // 0 -1 1 0; 0 1 0 -1]
+    auto transform = [&](f2v(&d)[4][4], f2v(&b)[16]) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            if (zero_top) d[0][c] = f2v{0.f, 0.f};
-            if (zero_bot) d[3][c] = f2v{0.f, 0.f};
-            if (zero_left) d[c][0] = f2v{0.f, 0.f};
-            if (zero_right) d[c][3] = f2v{0.f, 0.f};
-        }
-        f2v b[16];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const f2v r0 = d[0][c] - d[2][c], r1 = d[1][c] + d[2][c];
-            const f2v r2 = d[2][c] - d[1][c], r3 = d[1][c] - d[3][c];
+            const f2v r0 = pk_sub(d[0][c], d[2][c]), r1 = pk_add(d[1][c], d[2][c]);
+            const f2v r2 = pk_sub(d[2][c], d[1][c]), r3 = pk_sub(d[1][c], d[3][c]);
             d[0][c] = r0;
             d[1][c] = r1;
             d[2][c] = r2;
@@ -250,38 +265,55 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
         }
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
-            b[4 * a + 0] = d[a][0] - d[a][2];
-            b[4 * a + 1] = d[a][1] + d[a][2];
-            b[4 * a + 2] = d[a][2] - d[a][1];
-            b[4 * a + 3] = d[a][1] - d[a][3];
+            b[4 * a + 0] = pk_sub(d[a][0], d[a][2]);
+            b[4 * a + 1] = pk_add(d[a][1], d[a][2]);
+            b[4 * a + 2] = pk_sub(d[a][2], d[a][1]);
+            b[4 * a + 3] = pk_sub(d[a][1], d[a][3]);
         }
-        {
-            const float *un = ursrc + (int64_t)nxt * kUChunk;
+    };
+    // positions 2 pp, 2 pp + 1 of one chunk: their U fragments landed (after them this
+    // wave issued the other 14, the current chunk's 2 patch DMAs and 2 pp U loads:
+    // vmcnt(16)), 8 MFMAs, then the fragments' reload for chunk `un`
+    auto mfma_pair = [&](int pp, const f2v(&b)[16], const float *un) {
+        wino_wait_u(ur[2 * pp], ur[2 * pp + 1]);
 #pragma unroll
-            for (int pp = 0; pp < 8; ++pp) {
-                // fragments 2 pp, 2 pp + 1 of this chunk landed: after them this wave
-                // issued the other 14, the next chunk's 2 patch DMAs and 2 pp U loads
-                wino_wait_u(ur[2 * pp], ur[2 * pp + 1]);
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
+            for (int t2 = 0; t2 < 2; ++t2)
+                acc[2 * pp + i][t2] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                    i ? ur[2 * pp + t2].z : ur[2 * pp + t2].x, b[2 * pp + i].x,
+                    acc[2 * pp + i][t2], 0, 0, 0);
 #pragma unroll
-                    for (int t2 = 0; t2 < 2; ++t2)
-                        acc[2 * pp + i][t2] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                            i ? ur[2 * pp + t2].z : ur[2 * pp + t2].x, b[2 * pp + i].x,
-                            acc[2 * pp + i][t2], 0, 0, 0);
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
-#pragma unroll
-                    for (int t2 = 0; t2 < 2; ++t2)
-                        acc[2 * pp + i][t2] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                            i ? ur[2 * pp + t2].w : ur[2 * pp + t2].y, b[2 * pp + i].y,
-                            acc[2 * pp + i][t2], 0, 0, 0);
-                if (!(PR & 8)) {
-                    wino_load_u(ur[2 * pp], un + (2 * pp) * 256, uvoff);
-                    wino_load_u(ur[2 * pp + 1], un + (2 * pp + 1) * 256, uvoff);
-                }
-            }
+            for (int t2 = 0; t2 < 2; ++t2)
+                acc[2 * pp + i][t2] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                    i ? ur[2 * pp + t2].w : ur[2 * pp + t2].y, b[2 * pp + i].y,
+                    acc[2 * pp + i][t2], 0, 0, 0);
+        if (!(PR & 8)) {
+            wino_load_u(ur[2 * pp], un + (2 * pp) * 256, uvoff);
+            wino_load_u(ur[2 * pp + 1], un + (2 * pp + 1) * 256, uvoff);
         }
+    };
+    VD_W2_DMA_P(0, 0)
+#pragma unroll
+    for (int l = 0; l < 16; ++l) wino_load_u(ur[l], ursrc + l * 256, uvoff);
+    wino_wait_barrier();
+    for (int ch = 0; ch < nch; ++ch) {
+        const int s = ch & 1;
+        // every chunk issues 2 patch DMAs, then 16 U loads (the last chunk re-copies
+        // itself into the idle stage and reloads its own U), so in-order vmcnt makes
+        // every wait vmcnt(16).  (A three-stage ring with the next chunk's patch read
+        // into registers during this chunk's MFMAs: bit-identical, 0-1 %, not kept:
+        // profiles/r04/wino_pf/.)
+        const int nxt = ch + 1 < nch ? ch + 1 : ch;
+        VD_W2_DMA_P(nxt, s ^ 1)
+        f2v d[4][4], b[16];
+        read_d(d, reinterpret_cast<const char *>(sm) + s * k2StageB);
+        transform(d, b);
+        const float *un = ursrc + (int64_t)nxt * kUChunk;
+#pragma unroll
+        for (int pp = 0; pp < 8; ++pp) mfma_pair(pp, b, un);
         // the next chunk's patch DMAs landed (16 U loads were issued after them) and
         // stage s read by every wave
         if (!(PR & 4)) wino_wait16_barrier();
