@@ -232,8 +232,17 @@ class Bottleneck(nn.Module):
         epilogue fused -- conv1: relu(x W1^T + b1); conv3: relu(h W3^T + b3 + r)
         with the residual r (identity, or the downsample conv whose bias is
         folded into b3) read by the GEMM itself (ops.gemm_bias_act)."""
+        # a stage's first block (stride 2 on the 1x1s): the strided 1x1 convs are
+        # GEMMs over the every-other-pixel copy of x (a quarter of its bytes, one
+        # copy kernel) instead of MIOpen / CK strided convs: 2.78 -> 2.27 ms per
+        # 16-frame step over res3-res5 (profiles/r04/stride2/ab.jsonl)
+        xs = None
+        if self.downsample is not None and self.fd.stride != (1, 1) and _is_1x1(self.fd):
+            xs = _subsample(x, self.fd.stride)
         if self.f1.stride == (1, 1):
             out = _gemm_conv1x1(x, self.w1, self.f1.bias, relu=True)
+        elif xs is not None and self.f1.stride == self.fd.stride and _is_1x1(self.f1):
+            out = _gemm_conv1x1(xs, self.w1, self.f1.bias, relu=True)
         else:
             out = _conv_epi(self.f1, x)
         y = _conv3x3_mfma(self.f2, out, relu=True)  # res2 / res3 3x3s (>= 2^18 px)
@@ -245,8 +254,21 @@ class Bottleneck(nn.Module):
                 y = ops.gemm_dual_bias_act(_nhwc2d(out), _nhwc2d(x), self.w3d, self.b3d)
                 if y is not None:
                     return y.view(N, H, W, -1).permute(0, 3, 1, 2)
+            if xs is not None:  # relu(h W3^T + b3 + (xs Wd^T + bd))
+                r = _gemm_conv1x1(xs, self.wd, self.fd.bias, relu=False)
+                return _gemm_conv1x1(out, self.w3, self.f3.bias, relu=True, res=r)
             return _gemm_conv1x1(out, self.w3, self.b3d, relu=True, res=_conv_nb(self.fd, x))
         return _gemm_conv1x1(out, self.w3, self.f3.bias, relu=True, res=x)
+
+
+def _is_1x1(conv: nn.Conv2d) -> bool:
+    return conv.kernel_size == (1, 1) and conv.padding == (0, 0) and conv.groups == 1
+
+
+def _subsample(x, stride):
+    """x[:, :, ::sh, ::sw] as a channels_last tensor: the pixels a pad-0 strided 1x1
+    conv reads (output size ceil(H / s), as the conv's)."""
+    return x[:, :, ::stride[0], ::stride[1]].contiguous(memory_format=torch.channels_last)
 
 
 def _gemm_ok(x) -> bool:
@@ -898,8 +920,8 @@ def prepare_bottlenecks(blocks, epilogue: bool = True):
             blk.w1 = blk.f1.weight.reshape(blk.f1.out_channels, -1).contiguous()
             blk.w3 = blk.f3.weight.reshape(blk.f3.out_channels, -1).contiguous()
             if blk.downsample is not None:  # [W3 | Wd] for the two-operand GEMM
-                blk.w3d = torch.cat([blk.w3, blk.fd.weight.reshape(blk.fd.out_channels, -1)],
-                                    1).contiguous()
+                blk.wd = blk.fd.weight.reshape(blk.fd.out_channels, -1).contiguous()
+                blk.w3d = torch.cat([blk.w3, blk.wd], 1).contiguous()
             blk.fused = True
         blk.epilogue = epilogue
 
