@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Steady-state per-step kernel breakdown from a rocprofv3 --kernel-trace CSV of
-bench.py: the span between the last two launches of the step's first kernel
-(image_to_blob) is one step; kernels are aggregated by name.
+bench.py: the span between two consecutive launches of the step's first kernel
+(image_to_blob) is one step -- the shortest such span among the last ones, so the
+bench's own measurement launches after the timed loop stay out; kernels are
+aggregated by name.
 
 usage: tools/analyze_trace.py run_kernel_trace.csv [marker] [top]
 """
@@ -20,7 +22,10 @@ def main():
     if len(idx) < 3:
         print("not enough steps in trace")
         return
-    a, b = idx[-3], idx[-2]
+    spans = [(int(rows[idx[k + 1]]["Start_Timestamp"]) - int(rows[idx[k]]["Start_Timestamp"]), k)
+             for k in range(max(0, len(idx) - 6), len(idx) - 1)]
+    k = min(spans)[1]
+    a, b = idx[k], idx[k + 1]
     step = rows[a:b]
     t0 = int(step[0]["Start_Timestamp"])
     t1 = int(rows[b]["Start_Timestamp"])

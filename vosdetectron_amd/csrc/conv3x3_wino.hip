@@ -38,6 +38,8 @@
 // channel 2q + s, so each fragment is one 8-byte LDS read.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.hpp"
 #include "vosdet_internal.hpp"
 
@@ -57,7 +59,8 @@ constexpr int k2PSlots = 576;             // + the all-zero row the masked taps 
 constexpr int k2StageB = k2PSlots * 16;  // 9 KiB; two stages
 constexpr int kUChunk = 16 * kCo * kKC;  // floats of U per (channel block, chunk)
 
-__device__ float4 g_wino_zero;  // the source of out-of-image patch taps
+constexpr int kZeroF4 = 1024;  // 4096 floats: the zero lanes' DMA source for C <= 4096
+__device__ float4 g_wino_zero[kZeroF4];  // the source of out-of-image patch taps
 
 template <int TC>
 struct Patch2 {  // patch [row][half][column] in 16-B slots
@@ -120,10 +123,32 @@ __device__ __forceinline__ f2v pk_sub(f2v a, f2v b) {
 __device__ __forceinline__ void wino_load_u(f4v &r, const float *ub, uint32_t voff) {
     asm volatile("global_load_dwordx4 %0, %1, %2" : "+v"(r) : "v"(voff), "s"(ub) : "memory");
 }
+template <int OFF>  // + an immediate byte offset (< 4 KiB): one SGPR base per 4 fragments
+__device__ __forceinline__ void wino_load_u_off(f4v &r, const float *ub, uint32_t voff) {
+    asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3"
+                 : "+v"(r)
+                 : "v"(voff), "s"(ub), "i"(OFF)
+                 : "memory");
+}
 // All but the last 16 vector-memory ops of this wave retired; the two fragments
 // pass through so their MFMAs cannot be scheduled above the wait.
 __device__ __forceinline__ void wino_wait_u(f4v &a, f4v &b) {
     asm volatile("s_waitcnt vmcnt(16)" : "+v"(a), "+v"(b) : : "memory");
+}
+// One 8-byte LDS read per lane at a precomputed address + an immediate (the stage);
+// inline asm so the stage offset stays an immediate -- the caller waits lgkmcnt.
+template <int OFF>
+__device__ __forceinline__ f2v wino_ds_read(uint32_t addr) {
+    f2v r;
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+    return r;
+}
+__device__ __forceinline__ void wino_wait_lds(f2v (&d)[4][4]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(d[0][0]), "+v"(d[0][1]), "+v"(d[0][2]), "+v"(d[0][3]), "+v"(d[1][0]),
+                   "+v"(d[1][1]), "+v"(d[1][2]), "+v"(d[1][3]), "+v"(d[2][0]), "+v"(d[2][1]),
+                   "+v"(d[2][2]), "+v"(d[2][3]), "+v"(d[3][0]), "+v"(d[3][1]), "+v"(d[3][2]),
+                   "+v"(d[3][3]));
 }
 __device__ __forceinline__ void wino_wait16_barrier() {
     asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -167,7 +192,6 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     // patch DMA: blocks b = wave + 4 i (i < 2); slots outside the patch or the
     // image copy zeros
     const float *psrc[2];
-    bool pok[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int s = 64 * (wave + 4 * i) + lane;
@@ -184,15 +208,7 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
             ok = m < nmaps && my < map_h && mx < map_w;  // a map's phantom row / column: 0
             pix = ((int64_t)m * map_h + my) * map_w + mx;
         }
-        pok[i] = ok;
-        psrc[i] = ok ? X + pix * C + 4 * h : X;
-    }
-    const float *zero = reinterpret_cast<const float *>(&g_wino_zero);
-#define VD_W2_DMA_P(CH, ST)                                                                  \
-    if (!(PR & 32)) {                                                                        \
-        const uint32_t d_ = sbase + (uint32_t)(ST) * k2StageB + (uint32_t)wave * 1024u;      \
-        _Pragma("unroll") for (int i = 0; i < 2; ++i)                                        \
-            wino_dma_1k(pok[i] ? psrc[i] + (CH) * kKC : zero, d_ + (uint32_t)i * 4096u);     \
+        psrc[i] = ok ? X + pix * C + 4 * h : reinterpret_cast<const float *>(g_wino_zero);
     }
     // transform reads: lane (j, q) -> tile 16 tg + j, channels 2q, 2q + 1 (half
     // q >> 1, dwords 2 (q & 1) ..): byte offsets within a stage
@@ -242,15 +258,6 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     const uint32_t uvoff = (uint32_t)lane * 16u;
 #pragma unroll
     for (int l = 0; l < 16; ++l) ur[l] = f4v{0.f, 0.f, 0.f, 0.f};
-    // the lane's 4 x 4 patch of one chunk (its two channels), LDS -> registers
-    auto read_d = [&](f2v(&d)[4][4], const char *stb) {
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                d[a][c] = (PR & 2) ? f2v{(float)roff[a], (float)coff[c]}
-                                   : *reinterpret_cast<const f2v *>(stb + roff[a] + coff[c]);
-    };
     // V = B^T d B for the lane's two channels, B^T = [1 0 -1 0; 0 1 1 0;
     // 0 -1 1 0; 0 1 0 -1]
     auto transform = [&](f2v(&d)[4][4], f2v(&b)[16]) {
@@ -291,35 +298,66 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
                     i ? ur[2 * pp + t2].w : ur[2 * pp + t2].y, b[2 * pp + i].y,
                     acc[2 * pp + i][t2], 0, 0, 0);
         if (!(PR & 8)) {
-            wino_load_u(ur[2 * pp], un + (2 * pp) * 256, uvoff);
-            wino_load_u(ur[2 * pp + 1], un + (2 * pp + 1) * 256, uvoff);
+            const float *ub = un + (pp >> 1) * 1024;
+            if (pp & 1) {
+                wino_load_u_off<2048>(ur[2 * pp], ub, uvoff);
+                wino_load_u_off<3072>(ur[2 * pp + 1], ub, uvoff);
+            } else {
+                wino_load_u_off<0>(ur[2 * pp], ub, uvoff);
+                wino_load_u_off<1024>(ur[2 * pp + 1], ub, uvoff);
+            }
         }
     };
-    VD_W2_DMA_P(0, 0)
+    // The chunk loop, unrolled by the two stages: the stage is an immediate of the 16
+    // LDS reads (their addresses precomputed), the zero lanes' DMA reads the zero
+    // buffer at the chunk's offset (no per-chunk select), one SGPR base per 4 U
+    // fragments.  Every chunk issues 2 patch DMAs, then 16 U loads (the last chunk
+    // re-copies itself into the idle stage and reloads its own U), so in-order vmcnt
+    // makes every wait vmcnt(16).  (Loop VALU 56 -> 34, SALU 80 -> 47 per chunk:
+    // bit-identical, 1-5 % faster, profiles/r04/wino_v2/.  A three-stage ring with
+    // the next chunk's patch read during this chunk's MFMAs: 0-1 %, not kept:
+    // profiles/r04/wino_pf/.)
+    {
+        uint32_t radr[4][4];
 #pragma unroll
-    for (int l = 0; l < 16; ++l) wino_load_u(ur[l], ursrc + l * 256, uvoff);
-    wino_wait_barrier();
-    for (int ch = 0; ch < nch; ++ch) {
-        const int s = ch & 1;
-        // every chunk issues 2 patch DMAs, then 16 U loads (the last chunk re-copies
-        // itself into the idle stage and reloads its own U), so in-order vmcnt makes
-        // every wait vmcnt(16).  (A three-stage ring with the next chunk's patch read
-        // into registers during this chunk's MFMAs: bit-identical, 0-1 %, not kept:
-        // profiles/r04/wino_pf/.)
-        const int nxt = ch + 1 < nch ? ch + 1 : ch;
-        VD_W2_DMA_P(nxt, s ^ 1)
-        f2v d[4][4], b[16];
-        read_d(d, reinterpret_cast<const char *>(sm) + s * k2StageB);
-        transform(d, b);
-        const float *un = ursrc + (int64_t)nxt * kUChunk;
+        for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int pp = 0; pp < 8; ++pp) mfma_pair(pp, b, un);
-        // the next chunk's patch DMAs landed (16 U loads were issued after them) and
-        // stage s read by every wave
-        if (!(PR & 4)) wino_wait16_barrier();
+            for (int c = 0; c < 4; ++c) radr[a][c] = sbase + roff[a] + coff[c];
+        const uint32_t dbase = sbase + (uint32_t)wave * 1024u;
+        auto chunk = [&](int ch, auto stc) {
+            constexpr int S = decltype(stc)::value;
+            const int nxt = ch + 1 < nch ? ch + 1 : ch;
+            if (!(PR & 32)) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    wino_dma_1k(psrc[i] + nxt * kKC, dbase + (uint32_t)((S ^ 1) * k2StageB + i * 4096));
+            }
+            f2v d[4][4], b[16];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    d[a][c] = (PR & 2) ? f2v{(float)radr[a][c], 0.f}
+                                       : wino_ds_read<S * k2StageB>(radr[a][c]);
+            wino_wait_lds(d);
+            transform(d, b);
+            const float *un = ursrc + (int64_t)nxt * kUChunk;
+#pragma unroll
+            for (int pp = 0; pp < 8; ++pp) mfma_pair(pp, b, un);
+            // the next chunk's patch DMAs landed (16 U loads were issued after them)
+            // and stage S read by every wave
+            if (!(PR & 4)) wino_wait16_barrier();
+        };
+        for (int l = 0; l < 2; ++l) wino_dma_1k(psrc[l], dbase + (uint32_t)(l * 4096));
+#pragma unroll
+        for (int l = 0; l < 16; ++l) wino_load_u(ur[l], ursrc + l * 256, uvoff);
+        wino_wait_barrier();
+        for (int ch = 0; ch < nch; ch += 2) {
+            chunk(ch, std::integral_constant<int, 0>{});
+            if (ch + 1 < nch) chunk(ch + 1, std::integral_constant<int, 1>{});
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outlives the wave
-#undef VD_W2_DMA_P
     // output transform (lane-local): A^T = [1 1 1 0; 0 1 -1 -1]; lane (j, q),
     // accumulator slot r holds channel n0 + cg*32 + 16 t2 + 4 q + r of tile 16 tg + j
     const int oy = oy0 + 2 * tr, ox = ox0 + 2 * tc;
@@ -399,7 +437,7 @@ __global__ void wino_weight_kernel(const float *__restrict__ w, int Cout, int C,
 }  // namespace
 
 bool conv3x3_wino_supported(int C, int Cout) {
-    return C % kKC == 0 && C >= kKC && Cout % kCo == 0 && Cout >= kCo;
+    return C % kKC == 0 && C >= kKC && C <= 4 * kZeroF4 && Cout % kCo == 0 && Cout >= kCo;
 }
 
 int launch_conv3x3_wino_weight(const float *w, int Cout, int C, float *U, hipStream_t s) {
