@@ -62,7 +62,7 @@ constexpr int kUChunk = 16 * kCo * kKC;  // floats of U per (channel block, chun
 constexpr int kZeroF4 = 1024;  // 4096 floats: the zero lanes' DMA source for C <= 4096
 __device__ float4 g_wino_zero[kZeroF4];  // the source of out-of-image patch taps
 
-template <int TC>
+template <int TC, bool SK = (TC == 16)>
 struct Patch2 {  // patch [row][half][column] in 16-B slots
     static constexpr int kTR = k2Tiles / TC, kPR = 2 * kTR + 2, kPC = 2 * TC + 2;
     static constexpr int kHP = TC == 16 ? 37 : 20, kRP = TC == 16 ? 80 : 48;
@@ -72,12 +72,17 @@ struct Patch2 {  // patch [row][half][column] in 16-B slots
     static constexpr int kZC = 2 * kHP;
     static_assert(kZC + 3 <= kRP && kHP >= 2 * TC + 4, "zero column slots (+ half + row skew)");
     static_assert(kRP % 16 == 0, "row pitch: whole bank sweeps");
-    // (p >> 4): columns 16 apart land 17 slots apart, so the 16 tiles of one
+    // TC = 16, (p >> 4): columns 16 apart land 17 slots apart, so the 16 tiles of one
     // fragment read (pixel columns 2j + c) fall in distinct 16-B bank groups (one
     // 2-way pair for c >= 2); ((r >> 1) & 1): rows two apart are shifted by one
-    // slot (the two tile rows of a TC = 8 read)
+    // slot, so a TC = 8 read (8 tiles on each of two tile rows) is conflict-free
+    // with no column skew at all (the skew there cost a 2-way conflict on half the
+    // reads: SQ_LDS_BANK_CONFLICT = 1 cycle per ds_read, profiles/r04/wino_pmc/;
+    // without it bit-identical, 0.5-2 % faster, profiles/r04/wino_noskew/)
+    __device__ static int col(int p) { return SK ? p + (p >> 4) : p; }
+    __device__ static int col_inv(int u) { return !SK || u < 16 ? u : (u < 33 ? u - 1 : u - 2); }
     __device__ static int slot(int r, int h, int p) {
-        return r * kRP + h * kHP + p + (p >> 4) + ((r >> 1) & 1);
+        return r * kRP + h * kHP + col(p) + ((r >> 1) & 1);
     }
 };
 
@@ -155,12 +160,12 @@ __device__ __forceinline__ void wino_wait16_barrier() {
 }
 
 
-template <bool RELU, int TC, int PR = 0>
+template <bool RELU, int TC, int PR = 0, bool SK = (TC == 16)>
 __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
     int cb_per_xcd, int seg_h, int seg_w, int gx, int nmaps, int map_h, int map_w) {
-    using PG = Patch2<TC>;
+    using PG = Patch2<TC, SK>;
     __shared__ __attribute__((aligned(16))) float sm[2 * k2StageB / 4];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -198,7 +203,7 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
         const int r = s / PG::kRP, t = s - (s / PG::kRP) * PG::kRP;
         const int h = t >= PG::kHP;
         const int u = t - h * PG::kHP - ((r >> 1) & 1);
-        const int p = u < 16 ? u : (u < 33 ? u - 1 : u - 2);
+        const int p = PG::col_inv(u);
         const int y = iy0 + r, x = ix0 + p;
         bool ok = r < PG::kPR && u >= 0 && p < PG::kPC && PG::slot(r, h, p) == s &&
                   (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
@@ -230,7 +235,7 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     for (int a = 0; a < 4; ++a) {
         const int r = 2 * tr + a, p = 2 * tc + a;
         roff[a] = 16 * (r * PG::kRP + ((r >> 1) & 1));
-        coff[a] = 16 * (p + (p >> 4)) + 16 * (q >> 1) * PG::kHP + 8 * (q & 1);
+        coff[a] = 16 * PG::col(p) + 16 * (q >> 1) * PG::kHP + 8 * (q & 1);
     }
     // the masked taps read zeros from LDS rather than being zeroed per chunk: a masked
     // row reads the all-zero row kPR (past the DMA'd slots, zeroed once here), a
