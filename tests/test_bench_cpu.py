@@ -161,3 +161,13 @@ def test_bench_engines_accept_the_step_calls():
                                        if not cfg.FPN.FPN_ON else "FramePipeline"), name
         for fn, args, kw in bench.step_calls(pipe, vos):
             inspect.signature(fn).bind(*args, **kw)  # raises TypeError on a drift
+
+
+def test_winograd_input_channel_limit():
+    """The Winograd kernel's zero lanes read a 4096-float zero buffer at the chunk's
+    channel offset (csrc/conv3x3_wino.hip), so conv3x3_route keeps a conv with more
+    input channels off it (the implicit GEMM or MIOpen / CK take it)."""
+    from vosdetectron_amd import modeling, ops
+    assert ops.WINO_MAX_CIN == 4096
+    assert modeling.conv3x3_route(16, 4096, 256, 200, 336)[0] == "wino"
+    assert modeling.conv3x3_route(16, 4104, 256, 200, 336)[0] != "wino"

@@ -119,7 +119,8 @@ def conv3x3_route(N: int, Cin: int, Cout: int, H: int, W: int, mosaic=True):
     npx = N * H * W
     mos, use = _pick_mosaic(N, H, W, mosaic)
     if (os.environ.get("VOSDET_CONV3X3_ALGO", CONV3X3_ALGO) == "wino" and npx >= _WINO_MIN_PIXELS
-            and use >= _WINO_MIN_BLOCK_USE and Cout % 64 == 0 and Cin % 8 == 0 and Cout > 0):
+            and use >= _WINO_MIN_BLOCK_USE and Cout % 64 == 0 and Cin % 8 == 0 and Cout > 0
+            and Cin <= ops.WINO_MAX_CIN):
         return "wino", mos
     if npx < _CONV3X3_MIN_PIXELS:
         return None, None

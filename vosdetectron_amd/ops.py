@@ -568,17 +568,20 @@ def conv3x3_bias_act(x: torch.Tensor, w2: torch.Tensor, bias: Optional[torch.Ten
     return out
 
 
+WINO_MAX_CIN = 4096  # csrc/conv3x3_wino.hip: the zero lanes' DMA source holds 4096 floats
+
+
 def conv3x3_wino_weight(w: torch.Tensor) -> Optional[torch.Tensor]:
     """PyTorch conv weight [Cout][Cin][3][3] -> the Winograd F(2x2,3x3) operand
     U = G g G^T in the kernel's register-fragment order [Cout/64][Cin/8][2][16][64][4]
     (32-channel group, fragment, lane, 2 positions x 2 channels;
     vd_conv3x3_wino_weight; once per model).  None for
-    a shape the kernel does not serve (Cout % 64, Cin % 8)."""
+    a shape the kernel does not serve (Cout % 64, Cin % 8, Cin > WINO_MAX_CIN)."""
     w_ = _need(w, "w")
     if w_.dim() != 4 or tuple(w_.shape[2:]) != (3, 3):
         raise ValueError("conv3x3_wino_weight: weight %s" % (tuple(w_.shape),))
     Cout, C = w_.shape[:2]
-    if Cout % 64 or C % 8 or Cout == 0 or C == 0:
+    if Cout % 64 or C % 8 or Cout == 0 or C == 0 or C > WINO_MAX_CIN:
         return None
     u = torch.empty((Cout // 64, C // 8, 2, 16, 64, 4), dtype=torch.float32, device=w_.device)
     check(lib().vd_conv3x3_wino_weight(w_.data_ptr(), Cout, C, u.data_ptr(), _stream()),
