@@ -1,15 +1,15 @@
 """The configuration bench.py measures, tested as benched (VERDICT r2 item 2,
 VERDICT r3 weak #2).
 
-bench.py runs e2e_mask_rcnn_R-50-FPN_1x at 16 synthetic 800x1333 frames per
-step on the channels_last engine.  At that batch the 3x3 convolutions route to
+bench.py runs e2e_mask_rcnn_R-50-FPN_1x at BATCH = bench.DEFAULT_FRAMES (32)
+synthetic 800x1333 frames per step on the channels_last engine.  At that batch the 3x3 convolutions route to
 the hand-written Winograd F(2x2,3x3) MFMA kernel (csrc/conv3x3_wino.hip;
 modeling.conv3x3_route: >= 2^12 batch pixels, blocks >= 60 % real output) --
 P2 as one launch per batch, P3 / P4 / res5 / P5 / P6 and the mask head's
-1600 RoI maps as 2-D mosaics -- and the 1x1 GEMMs run at M = 1,075,200 pixels;
+BATCH x 100 RoI maps as 2-D mosaics -- and the 1x1 GEMMs run at M = BATCH x 200 x 336;
 batch-1 pipeline tests never reach those routes.  Here:
 
-* FramePipeline(batch=16) on 16 distinct frames (bench.synthetic_frames, the
+* FramePipeline(batch=BATCH) on BATCH distinct frames (bench.synthetic_frames, the
   bench's own seeds and routes): the route counters show Winograd ran and the
   implicit GEMM / MIOpen did not take a benched 3x3; stage-wise parity on
   frames 0, 7 and 15 (proposals + collect and detections bit-exact, box / mask
@@ -29,7 +29,7 @@ from tests.engine_checks import e2e_vs_cpu, stagewise
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
-BATCH = 16
+BATCH = __import__("bench").DEFAULT_FRAMES  # the batch bench.py times
 
 
 @pytest.fixture(scope="module")
@@ -52,7 +52,7 @@ def bench_setup():
 
 def test_bench_batch_routes(bench_setup):
     """The benched shapes take the hand-written routes (not a silent fallback):
-    every 3x3 conv of the 16-frame step ran on the Winograd kernel -- res2 / res3
+    every 3x3 conv of the benched step ran on the Winograd kernel -- res2 / res3
     / res4 / res5 conv2 (stride-1 blocks), FPN posthoc P2-P5, the RPN conv on
     P2-P6 and the mask head's four convs -- P2 per image, the rest as mosaics."""
     from vosdetectron_amd import modeling
@@ -70,14 +70,14 @@ def test_bench_batch_routes(bench_setup):
     assert n_wino >= 13 and routes.get("wino_2d", 0) >= 8, routes
 
 
-@pytest.mark.parametrize("f", [0, 7, 15])
+@pytest.mark.parametrize("f", [0, 7, BATCH - 1])
 def test_bench_batch_stagewise(bench_setup, f):
     cfg, sd, pipe, frames, out, _ = bench_setup
     rois, _ = stagewise(cfg, pipe, out, frames[f], f=f)
     assert len(rois) == 1000
 
 
-@pytest.mark.parametrize("f", [0, 15])
+@pytest.mark.parametrize("f", [0, BATCH - 1])
 def test_bench_batch_e2e_vs_cpu(bench_setup, f):
     from oracle.pipeline import RefCPUPipeline
     cfg, sd, pipe, frames, out, _ = bench_setup
@@ -86,16 +86,15 @@ def test_bench_batch_e2e_vs_cpu(bench_setup, f):
     e2e_vs_cpu(out, ref_out, f=f)
 
 
-@pytest.mark.parametrize("N,C,H,W", [(16, 256, 200, 336), (16, 256, 100, 168), (16, 256, 50, 84),
-                                     (1600, 256, 14, 14), (16, 64, 200, 336),
-                                     (16, 512, 25, 42)])
+@pytest.mark.parametrize("N,C,H,W", [(BATCH, 256, 200, 336), (BATCH, 256, 100, 168),
+                                     (BATCH, 256, 50, 84), (BATCH * 100, 256, 14, 14),
+                                     (BATCH, 64, 200, 336), (BATCH, 512, 25, 42)])
 @pytest.mark.parametrize("bias", [True, False])
 def test_conv3x3_wino_benched_shapes(N, C, H, W, bias):
     """vd_conv3x3_wino_* (the kernel the step runs) at the benched sizes in the
     layout the engine picks (modeling.conv3x3_route: P2 / res2 per image, the
     P3 / P4 2-D mosaics, the mask head's 1600-map mosaic, res5's odd-sided 25 x 42
-    mosaic) vs torch fp32 at 2e-5 of the output range; (16,256,200,336) is
-    1,075,200 pixels."""
+    mosaic) vs torch fp32 at 2e-5 of the output range."""
     from vosdetectron_amd import modeling, ops
     algo, mos = modeling.conv3x3_route(N, C, C, H, W)
     assert algo == "wino", (N, C, H, W, algo)
@@ -119,7 +118,7 @@ def test_conv3x3_wino_benched_shapes(N, C, H, W, bias):
                                      (256, 256, False)])
 def test_gemm1x1_benched_M(K, N, res):
     """The 1x1-conv GEMM epilogue (default search: hipBLASLt or the MFMA kernel,
-    whichever the per-shape timing picks) at M = 16 x 200 x 336 vs torch fp32."""
+    whichever the per-shape timing picks) at M = BATCH x 200 x 336 vs torch fp32."""
     from vosdetectron_amd import ops
     M = BATCH * 200 * 336
     g = torch.Generator(device="cuda").manual_seed(K + N)
@@ -134,7 +133,7 @@ def test_gemm1x1_benched_M(K, N, res):
 
 
 def test_gemm_dual_benched_M():
-    """res2's first block tail as one two-operand GEMM at M = 1,075,200."""
+    """res2's first block tail as one two-operand GEMM at M = BATCH x 200 x 336."""
     from vosdetectron_amd import ops
     M = BATCH * 200 * 336
     g = torch.Generator(device="cuda").manual_seed(5)

@@ -64,8 +64,8 @@ def test_no_fraction_above_one():
 def test_winograd_flop_classifier():
     """bench._WinoFlops counts exactly the 3x3 / stride-1 / pad-1 convolutions
     the engine routes to Winograd (modeling.conv3x3_route on the 16-frame batch:
-    Cout % 64 == 0, Cin % 8 == 0, >= 2^12 batch output pixels, blocks >= 60 %
-    real output)."""
+    Cout % 64 == 0, Cin % 8 == 0, and >= 2^12 batch output pixels in blocks >= 60 %
+    real output, or below 2^18 pixels, where the alternative is MIOpen)."""
     import torch
     import torch.nn.functional as F
     x = torch.randn(1, 8, 64, 64)
@@ -77,7 +77,7 @@ def test_winograd_flop_classifier():
         F.conv2d(x[:, :, :8, :8], torch.randn(64, 8, 3, 3), padding=1)  # 16*64 px
         # 16 x 16 maps: 16 * 256 = 2^12 batch pixels in full 8 x 16 blocks -> Winograd
         F.conv2d(x[:, :, :16, :16], torch.randn(64, 8, 3, 3), padding=1)
-    assert wf.flops == 2 * 4096 * 64 * 8 * 9 + 2 * 256 * 64 * 8 * 9
+    assert wf.flops == 2 * 4096 * 64 * 8 * 9 + 2 * 256 * 64 * 8 * 9 + 2 * 64 * 64 * 8 * 9
 
 
 def test_roi_align_algorithmic_bytes_counts_union_once():

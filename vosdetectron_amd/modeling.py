@@ -118,12 +118,16 @@ def conv3x3_route(N: int, Cin: int, Cout: int, H: int, W: int, mosaic=True):
     One rule for the engine (_conv3x3_mfma) and the bench's executed-FLOP count."""
     npx = N * H * W
     mos, use = _pick_mosaic(N, H, W, mosaic)
-    if (os.environ.get("VOSDET_CONV3X3_ALGO", CONV3X3_ALGO) == "wino" and npx >= _WINO_MIN_PIXELS
-            and use >= _WINO_MIN_BLOCK_USE and Cout % 64 == 0 and Cin % 8 == 0 and Cout > 0
-            and Cin <= ops.WINO_MAX_CIN):
+    wino = (os.environ.get("VOSDET_CONV3X3_ALGO", CONV3X3_ALGO) == "wino" and Cout % 64 == 0
+            and Cin % 8 == 0 and Cout > 0 and Cin <= ops.WINO_MAX_CIN)
+    if wino and npx >= _WINO_MIN_PIXELS and use >= _WINO_MIN_BLOCK_USE:
         return "wino", mos
     if npx < _CONV3X3_MIN_PIXELS:
-        return None, None
+        # below the implicit GEMM's range the alternative is MIOpen, whose small-map
+        # solvers split K with atomics (igemm_fwd_gtcx35_..._gkgs): a 3-frame step's
+        # P6 RPN conv differed run to run.  Winograd is deterministic, and at these
+        # sizes its idle block share costs microseconds.
+        return ("wino", mos) if wino else (None, None)
     return "igemm", None
 
 
@@ -475,7 +479,15 @@ class TopdownLateral(nn.Module):
             if self.use_gn:
                 return _gn_epi(self.conv_lateral[0], self.conv_lateral[1], lateral, act=None,
                                res=top, up=True)
-            return _conv_epi(self.conv_lateral, lateral, relu=False, res=top, up=True)
+            c = self.conv_lateral
+            if _gemm_ok(lateral) and _is_1x1(c) and c.stride == (1, 1):
+                # the lateral 1x1 as a GEMM with its bias fused, then the nearest-2x
+                # top-down add (MIOpen / CK took it before; at small batches their
+                # solvers were not run-to-run deterministic)
+                y = _gemm_conv1x1(lateral, c.weight.reshape(c.out_channels, -1), c.bias,
+                                  relu=False)
+                return ops.bias_act_(y, None, top, relu=False, upsample_residual=True)
+            return _conv_epi(c, lateral, relu=False, res=top, up=True)
         return self.conv_lateral(lateral) + F.interpolate(top, scale_factor=2, mode="nearest")
 
 
