@@ -335,7 +335,9 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
             if (!(PR & 32)) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
-                    wino_dma_1k(psrc[i] + nxt * kKC, dbase + (uint32_t)((S ^ 1) * k2StageB + i * 4096));
+                    wino_dma_1k((PR & 64) ? X + ((int64_t)blockIdx.x * 512 + (wave + 4 * i) * 64 + lane) * 4 + nxt * 2048
+                                          : psrc[i] + nxt * kKC,
+                                dbase + (uint32_t)((S ^ 1) * k2StageB + i * 4096));
             }
             f2v d[4][4], b[16];
 #pragma unroll
@@ -483,7 +485,8 @@ int launch_wino(const float *X, int N, int H, int W, int C, const float *U, int 
                    : (relu ? conv3x3_wino2_kernel<true, 16> : conv3x3_wino2_kernel<false, 16>);
 #ifdef VD_RESEARCH_PROBES
     // speed-of-light probes (wrong results; tools/research/wino_sol_probe.py): 2 no
-    // patch reads, 4 no barrier, 8 no U loads, 32 no patch DMA.  Only in a research build
+    // patch reads, 4 no barrier, 8 no U loads, 32 no patch DMA, 64 patch DMA from
+    // lane-contiguous addresses (8 lines per wave instruction).  Only in a research build
     // (make VD_RESEARCH=1), never in the product library: a stray environment
     // variable must not be able to corrupt a product convolution.
     const char *pe = getenv("VOSDET_WINO_PROBE");
@@ -491,7 +494,7 @@ int launch_wino(const float *X, int N, int H, int W, int C, const float *U, int 
 #define VD_PROBE_CASE(B) \
         case B: kern = sq ? conv3x3_wino2_kernel<false, 8, B> : conv3x3_wino2_kernel<false, 16, B>; break;
         VD_PROBE_CASE(2) VD_PROBE_CASE(4) VD_PROBE_CASE(8) VD_PROBE_CASE(32) VD_PROBE_CASE(36)
-        VD_PROBE_CASE(12) VD_PROBE_CASE(46)
+        VD_PROBE_CASE(12) VD_PROBE_CASE(46) VD_PROBE_CASE(64)
 #undef VD_PROBE_CASE
         default: break;
     }
