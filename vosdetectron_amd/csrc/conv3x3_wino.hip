@@ -102,6 +102,20 @@ __device__ __forceinline__ void wino_dma_1k(const float *src, uint32_t lds) {
         : "memory");
 }
 
+// The same from a wave-uniform SGPR base + a per-lane 32-bit byte offset.
+__device__ __forceinline__ void wino_dma_1k_off(const float *base, uint32_t voff, uint32_t lds) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(base), "s"(lds)
+        : "memory");
+}
+
 // This wave's LDS-DMAs landed and LDS reads retired, then the workgroup barrier.
 __device__ __forceinline__ void wino_wait_barrier() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -160,7 +174,7 @@ __device__ __forceinline__ void wino_wait16_barrier() {
 }
 
 
-template <bool RELU, int TC, int PR = 0, bool SK = (TC == 16)>
+template <bool RELU, int TC, int PR = 0, bool SK = (TC == 16), bool RD = false>
 __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
@@ -197,6 +211,7 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     // patch DMA: blocks b = wave + 4 i (i < 2); slots outside the patch or the
     // image copy zeros
     const float *psrc[2];
+    uint32_t poff[2];  // RD: byte offsets from X (invalid lanes copy X[0..3], never read)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int s = 64 * (wave + 4 * i) + lane;
@@ -214,6 +229,7 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
             pix = ((int64_t)m * map_h + my) * map_w + mx;
         }
         psrc[i] = ok ? X + pix * C + 4 * h : reinterpret_cast<const float *>(g_wino_zero);
+        poff[i] = ok ? (uint32_t)((pix * C + 4 * h) * 4) : 0u;
     }
     // transform reads: lane (j, q) -> tile 16 tg + j, channels 2q, 2q + 1 (half
     // q >> 1, dwords 2 (q & 1) ..): byte offsets within a stage
@@ -328,16 +344,45 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
         for (int a = 0; a < 4; ++a)
 #pragma unroll
             for (int c = 0; c < 4; ++c) radr[a][c] = sbase + roff[a] + coff[c];
+        if constexpr (RD) {
+            // every tap outside the image (or a map's phantom row / column, or a
+            // mosaic neighbour -- the masks above) reads the zero row past the DMA'd
+            // slots, so the DMA never has to write zeros: its invalid lanes copy
+            // X[0..3] into slots no tap reads
+            const uint32_t zaddr = sbase + 16u * k2PDma + 8u * (q & 1);
+            // 2-D mosaic: the tile's rows / columns within its map (a tile never
+            // straddles maps; the taps past a map's side are the masks above)
+            const int ty = seg_w > 0 ? toy % seg_h : 0, tx = seg_w > 0 ? tox % seg_w : 0;
+            uint32_t badr = 0, badc = 0;
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const int y = toy - 1 + a, x = tox - 1 + a;
+                if ((unsigned)y >= (unsigned)H || (seg_w > 0 && ty - 1 + a >= map_h)) badr |= 1u << a;
+                if ((unsigned)x >= (unsigned)W || (seg_w > 0 && tx - 1 + a >= map_w)) badc |= 1u << a;
+            }
+            if (zero_top) badr |= 1u;
+            if (zero_bot) badr |= 8u;
+            if (zero_left) badc |= 1u;
+            if (zero_right) badc |= 8u;
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (((badr >> a) | (badc >> c)) & 1u) radr[a][c] = zaddr;
+        }
         const uint32_t dbase = sbase + (uint32_t)wave * 1024u;
         auto chunk = [&](int ch, auto stc) {
             constexpr int S = decltype(stc)::value;
             const int nxt = ch + 1 < nch ? ch + 1 : ch;
             if (!(PR & 32)) {
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
-                    wino_dma_1k((PR & 64) ? X + ((int64_t)blockIdx.x * 512 + (wave + 4 * i) * 64 + lane) * 4 + nxt * 2048
-                                          : psrc[i] + nxt * kKC,
-                                dbase + (uint32_t)((S ^ 1) * k2StageB + i * 4096));
+                for (int i = 0; i < 2; ++i) {
+                    if constexpr (RD)
+                        wino_dma_1k_off(X + nxt * kKC, poff[i],
+                                        dbase + (uint32_t)((S ^ 1) * k2StageB + i * 4096));
+                    else
+                        wino_dma_1k(psrc[i] + nxt * kKC, dbase + (uint32_t)((S ^ 1) * k2StageB + i * 4096));
+                }
             }
             f2v d[4][4], b[16];
 #pragma unroll
@@ -355,7 +400,12 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
             // and stage S read by every wave
             if (!(PR & 4)) wino_wait16_barrier();
         };
-        for (int l = 0; l < 2; ++l) wino_dma_1k(psrc[l], dbase + (uint32_t)(l * 4096));
+        for (int l = 0; l < 2; ++l) {
+            if constexpr (RD)
+                wino_dma_1k_off(X, poff[l], dbase + (uint32_t)(l * 4096));
+            else
+                wino_dma_1k(psrc[l], dbase + (uint32_t)(l * 4096));
+        }
 #pragma unroll
         for (int l = 0; l < 16; ++l) wino_load_u(ur[l], ursrc + l * 256, uvoff);
         wino_wait_barrier();
@@ -481,20 +531,28 @@ int launch_wino(const float *X, int N, int H, int W, int C, const float *U, int 
     const int64_t blocks = cbx ? (nsp + 8 / ncb - 1) / (8 / ncb) * 8
                                : (nsp + 7) / 8 * 8 * ncb;
     if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
-    auto kern = sq ? (relu ? conv3x3_wino2_kernel<true, 8> : conv3x3_wino2_kernel<false, 8>)
-                   : (relu ? conv3x3_wino2_kernel<true, 16> : conv3x3_wino2_kernel<false, 16>);
+    // the DMA reads X through 32-bit byte offsets (taps outside the image redirected to
+    // a zero row, so no zero source per lane: bit-identical, 0-3.5 % faster on the
+    // benched shapes, profiles/r04/wino_rd/); an X of 4 GiB or more takes the
+    // 64-bit-pointer form with the zero-buffer source
+    const int64_t xbytes = (seg_w > 0 ? (int64_t)nmaps * map_h * map_w : (int64_t)N * H * W) * C * 4;
+    auto kern = sq ? (relu ? conv3x3_wino2_kernel<true, 8, 0, false, true> : conv3x3_wino2_kernel<false, 8, 0, false, true>)
+                   : (relu ? conv3x3_wino2_kernel<true, 16, 0, true, true> : conv3x3_wino2_kernel<false, 16, 0, true, true>);
+    if (xbytes >= ((int64_t)1 << 32))
+        kern = sq ? (relu ? conv3x3_wino2_kernel<true, 8> : conv3x3_wino2_kernel<false, 8>)
+                  : (relu ? conv3x3_wino2_kernel<true, 16> : conv3x3_wino2_kernel<false, 16>);
 #ifdef VD_RESEARCH_PROBES
     // speed-of-light probes (wrong results; tools/research/wino_sol_probe.py): 2 no
-    // patch reads, 4 no barrier, 8 no U loads, 32 no patch DMA, 64 patch DMA from
-    // lane-contiguous addresses (8 lines per wave instruction).  Only in a research build
+    // patch reads, 4 no barrier, 8 no U loads, 32 no patch DMA (round-4 probe 64, the
+    // DMA from lane-contiguous addresses: profiles/r04/wino_sol_probe_dma.json).  Only in a research build
     // (make VD_RESEARCH=1), never in the product library: a stray environment
     // variable must not be able to corrupt a product convolution.
     const char *pe = getenv("VOSDET_WINO_PROBE");
     switch (pe && !relu ? atoi(pe) : 0) {
 #define VD_PROBE_CASE(B) \
-        case B: kern = sq ? conv3x3_wino2_kernel<false, 8, B> : conv3x3_wino2_kernel<false, 16, B>; break;
+        case B: kern = sq ? conv3x3_wino2_kernel<false, 8, B, false, true> : conv3x3_wino2_kernel<false, 16, B, true, true>; break;
         VD_PROBE_CASE(2) VD_PROBE_CASE(4) VD_PROBE_CASE(8) VD_PROBE_CASE(32) VD_PROBE_CASE(36)
-        VD_PROBE_CASE(12) VD_PROBE_CASE(46) VD_PROBE_CASE(64)
+        VD_PROBE_CASE(12) VD_PROBE_CASE(46)
 #undef VD_PROBE_CASE
         default: break;
     }
