@@ -736,6 +736,7 @@ class MaskHeadV1upXconvs(nn.Module):
         w = self.upconv.weight  # Cin x Cout x 2 x 2
         self.up_w = w.permute(0, 2, 3, 1).reshape(w.shape[0], -1).contiguous()  # Cin x (i,j,co)
         self.up_b = self.upconv.bias.repeat(4).contiguous()
+        self.up_wt = self.up_w.t().contiguous()  # (i,j,co) x Cin: ops.gemm_bias_act's W
         self.nhwc_ready = True
 
     def head_nhwc(self, x_nhwc):
@@ -744,9 +745,12 @@ class MaskHeadV1upXconvs(nn.Module):
         M, P, _, C = x_nhwc.shape
         x = self._convs_nhwc(x_nhwc.permute(0, 3, 1, 2))  # NCHW view, channels_last
         x = x.permute(0, 2, 3, 1).reshape(M * P * P, -1)
-        # bias + ReLU in the GEMM epilogue (hipBLASLt) instead of a separate pass
-        # over the (M*P*P x 4C) upconv output
-        y = torch._addmm_activation(self.up_b, x, self.up_w)
+        # bias + ReLU in the GEMM epilogue (hipBLASLt, the plan pinned per shape by
+        # ops.gemm_bias_act's timing search) instead of a separate pass over the
+        # (M*P*P x 4C) upconv output
+        y = ops.gemm_bias_act(x.contiguous(), self.up_wt, self.up_b, relu=True)
+        if y is None:
+            y = torch._addmm_activation(self.up_b, x, self.up_w)
         return y.view(M, P, P, 2, 2, -1)
 
     def _convs_nhwc(self, x):
