@@ -614,8 +614,15 @@ class Roi2MLPHead(nn.Module):
     def mlp_nhwc(self, x):
         """fc6/fc7 on R x P x P x C RoI features: fc6's weight columns are permuted
         once (prepare) from the reference's (c, ph, pw) flattening to (ph, pw, c)."""
-        x = F.relu(F.linear(x.reshape(x.size(0), -1), self.fc1_nhwc_weight, self.fc1.bias),
-                   inplace=True)
+        x = x.reshape(x.size(0), -1)
+        if x.is_cuda and x.dtype == torch.float32 and x.size(0) > 0:
+            # ReLU in the GEMM epilogue, the plan pinned per shape (ops.gemm_bias_act)
+            y = ops.gemm_bias_act(x.contiguous(), self.fc1_nhwc_weight, self.fc1.bias, relu=True)
+            if y is not None:
+                z = ops.gemm_bias_act(y, self.fc2.weight, self.fc2.bias, relu=True)
+                if z is not None:
+                    return z
+        x = F.relu(F.linear(x, self.fc1_nhwc_weight, self.fc1.bias), inplace=True)
         return F.relu(self.fc2(x), inplace=True)
 
     @torch.no_grad()
