@@ -13,7 +13,7 @@
 //
 // Workgroup = 4 waves, 32 tiles (2 x 16 tiles = 4 x 32 output pixels of one
 // image, or 4 x 8 tiles = 8 x 16 pixels for maps <= 16 wide: the 14 x 14 mask-head
-// RoIs) x 64 output channels, two waves per SIMD (240-246 VGPRs), so TWO workgroups share a CU and the
+// RoIs) x 64 output channels, two waves per SIMD (248-252 VGPRs), so TWO workgroups share a CU and the
 // barrier / transform gaps of one are filled by the MFMAs of the other (the
 // round-3 one-per-CU 8-wave form, 64 tiles and 150 KiB, ran 7-12 % slower on every
 // benched shape in one-process A/B: profiles/r03_wino_ab.json).  Wave w owns 16 tiles (w & 1) x
@@ -23,7 +23,7 @@
 //
 // K is walked in chunks of 8 input channels.  Per chunk the raw input patch is
 // copied HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR round trip),
-// double-buffered (16 KiB), one barrier per chunk; each wave's U operand (the 16
+// double-buffered (2 x 9 KiB), one barrier per chunk; each wave's U operand (the 16
 // positions x its 32 channels x 8 input channels, 64 VGPRs) comes straight from L2
 // into registers, each fragment reloaded for the next chunk right after its MFMAs
 // consumed it.  (U through LDS -- its 32 KiB slice LDS-DMA'd per chunk and read back
