@@ -174,7 +174,7 @@ __device__ __forceinline__ void wino_wait16_barrier() {
 }
 
 
-template <bool RELU, int TC, int PR = 0, bool SK = (TC == 16), bool RD = false>
+template <bool RELU, int TC, int PR = 0, bool SK = (TC == 16), bool RD = false, bool PRIO = true>
 __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
@@ -385,6 +385,11 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
                 }
             }
             f2v d[4][4], b[16];
+            // the reads + transform at wave priority 1: the partner wave on the SIMD
+            // keeps the matrix pipe while this one gets back to its MFMAs sooner
+            // (bit-identical, 0.3-2 % per benched shape, +0.4 % bench:
+            // profiles/r04/wino_prio/)
+            if constexpr (PRIO) asm volatile("s_setprio 1" ::: "memory");
 #pragma unroll
             for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -393,6 +398,10 @@ __global__ __launch_bounds__(k2Threads, 2) void conv3x3_wino2_kernel(
                                        : wino_ds_read<S * k2StageB>(radr[a][c]);
             wino_wait_lds(d);
             transform(d, b);
+            if constexpr (PRIO) {
+                // the transform's results pass through, so it cannot sink below
+                asm volatile("s_setprio 0" : "+v"(b[0]), "+v"(b[15]) : : "memory");
+            }
             const float *un = ursrc + (int64_t)nxt * kUChunk;
 #pragma unroll
             for (int pp = 0; pp < 8; ++pp) mfma_pair(pp, b, un);
