@@ -119,3 +119,30 @@ def test_conv3x3_wino_mosaic_bit_exact(N, C, H, W, Cout, relu, mode):
         ref = F.relu(ref)
     assert float((mos - ref).abs().max()) <= 2e-5 * max(1., float(ref.abs().max()))
 
+
+def test_conv3x3_wino_input_over_4gib():
+    """The Winograd kernel's patch DMA reads X through 32-bit byte offsets; an input
+    of 4 GiB or more takes the 64-bit-pointer form with the zero-buffer source
+    (csrc/conv3x3_wino.hip, launch_wino).  2 x 256 x 1536 x 1408 fp32 = 4.43 GB,
+    vs torch fp32 at 2e-5 of the output range, borders included."""
+    from vosdetectron_amd import ops
+    N, C, H, W = 2, 256, 1536, 1408
+    assert N * C * H * W * 4 >= 1 << 32
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(N, C, H, W, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    w = torch.randn(C, C, 3, 3, device="cuda", generator=g) / (3. * C ** .5)
+    b = torch.randn(C, device="cuda", generator=g)
+    got = ops.conv3x3_wino_bias_act(x, ops.conv3x3_wino_weight(w), b, relu=True)
+    ref = F.relu(F.conv2d(x, w, b, padding=1))
+    torch.cuda.synchronize()
+    err = float((got - ref).abs().max())
+    assert err <= 2e-5 * max(1., float(ref.abs().max())), err
+    # the image borders (first / last rows and columns) are where the zero taps live
+    for sl in ((slice(None), slice(None), 0), (slice(None), slice(None), H - 1),
+               (slice(None), slice(None), slice(None), 0), (slice(None), slice(None), slice(None), W - 1)):
+        e = float((got[sl] - ref[sl]).abs().max())
+        assert e <= 2e-5 * max(1., float(ref.abs().max())), (sl, e)
+    del x, got, ref
+    torch.cuda.empty_cache()
+
