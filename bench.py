@@ -621,7 +621,12 @@ def measure_segm(pipe, out, frames=16):
 
 def capture_graphs(pipe, slots, graphs, note):
     """Capture one hipGraph of the whole step per frame slot (sync=False: no host
-    read inside).  Eager execution stays in place if capture fails."""
+    read inside).  Each graph is captured on a stream of its own and into a
+    memory pool of its own, so nothing a launch keeps state in is shared between
+    the two graphs: torch's BLAS workspaces are per (handle, stream), and
+    ops.gemm_workspace allocates from the capturing graph's pool (a
+    shared GEMM workspace is what stalled two concurrently replayed steps in
+    round 4).  Eager execution stays in place if capture fails."""
     try:
         for x in slots[:2]:
             g = torch.cuda.CUDAGraph()
@@ -631,7 +636,7 @@ def capture_graphs(pipe, slots, graphs, note):
                 pipe.run(x, sync=False)  # warm on the capture stream
             torch.cuda.current_stream().wait_stream(s)
             torch.cuda.synchronize()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, stream=s):
                 gout = pipe.run(x, sync=False)
             torch.cuda.synchronize()
             graphs[x.data_ptr()] = (g, gout)
@@ -641,6 +646,123 @@ def capture_graphs(pipe, slots, graphs, note):
         note[0] = "capture failed: %s" % (str(e).splitlines()[0][:200],)
         print("bench: hipGraph %s; running eagerly" % note[0], file=sys.stderr, flush=True)
         torch.cuda.synchronize()
+
+
+class StepLoop:
+    """The step bench.py times, shared by main() and by the GPU test
+    that runs it as timed (tests/test_timed_loop_gpu.py).  One step: take the
+    next u8 batch (FrameUploader: its H2D was issued on a side stream during the
+    previous step; the next batch's copy is issued now), replay the step's
+    captured hipGraph for that upload slot (or run the pipeline eagerly), then
+    the previous step's one host read (pipe.complete) while this step runs, then
+    -- when a process group exists -- wait for the previous step's all_gather
+    (stream-ordered) and issue this step's, left in flight on RCCL's stream while
+    the next step computes.  At most one gather is in flight.
+
+    on_gathered(step, pending): called with each step's PendingGather just before
+    the loop waits on it (a test collects wait(clone=True) there)."""
+
+    def __init__(self, pipe, uploader, gatherer, vos=False, seq_len=50, resident=None,
+                 on_gathered=None):
+        self.pipe, self.uploader, self.gatherer = pipe, uploader, gatherer
+        self.vos, self.seq_len, self.resident = vos, seq_len, resident
+        self.on_gathered = on_gathered
+        self.asynchronous = getattr(pipe, "ASYNC", False)
+        self.graphs = {}  # upload slot data_ptr -> (CUDAGraph, static outputs)
+        self.graph_note = None
+        self.t = 0
+        self.pending = None  # (step, PendingGather)
+        self.prev_out = None
+        self.last_out = None
+
+    def frames(self, t, prefetch):
+        if self.resident is not None:
+            return self.resident[t % len(self.resident)]
+        return self.uploader.get(t, prefetch)
+
+    def drain(self):
+        """The previous step's gather has landed (stream-ordered)."""
+        if self.pending is not None:
+            t, p = self.pending
+            self.pending = None
+            if self.on_gathered is not None:
+                self.on_gathered(t, p)
+            p.wait(views=False)
+
+    def step(self, prefetch=True):
+        t = self.t
+        self.t += 1
+        pipe = self.pipe
+        if self.vos and t % self.seq_len == 0:
+            pipe.reset()
+        frames = self.frames(t, prefetch)
+        key = frames.data_ptr()
+        if key in self.graphs:  # replay the captured step (one launch, no host work)
+            g, gout = self.graphs[key]
+            g.replay()
+            out = dict(gout)
+        else:
+            out = pipe.run(frames, sync=not self.asynchronous)
+        if self.resident is None:
+            self.uploader.release(t)
+        if self.asynchronous:
+            # the previous step's one host read (counts, capacity, rare overflow
+            # masks) while this step runs on the GPU
+            if self.prev_out is not None:
+                pipe.complete(self.prev_out)
+            self.prev_out = out
+        if self.gatherer is not None and self.gatherer.collective:
+            # ONE packed all_gather per step over RCCL (runner.py)
+            self.drain()
+            self.pending = (t, self.gatherer.gather_async(out["dets"], out["classes"],
+                                                          out["counts"], out["masks"]))
+        self.last_out = out
+        return out
+
+    def capture(self):
+        """Capture the step once per upload slot (after warm-up) and restart the
+        upload cycle at slot 0."""
+        slots = self.resident if self.resident is not None else self.uploader.dev
+        note = [None]
+        capture_graphs(self.pipe, slots, self.graphs, note)
+        self.graph_note = note[0]
+        self.t = 0
+        return self.graph_note
+
+    def finish(self):
+        """The last step's gather and host read: its completed outputs."""
+        self.drain()
+        if self.asynchronous and self.prev_out is not None:
+            self.pipe.complete(self.prev_out)
+            return self.prev_out
+        return self.last_out
+
+
+def timed_region(loop, steps, sync, barrier=None, watchdog=None, clock=time.perf_counter):
+    """bench.py's timed region: barrier + device sync, `steps` loop steps, then
+    -- still inside -- the last step's gather and complete() (loop.finish: the
+    counts read and any overflow mask batch), device sync + barrier.  Returns
+    (seconds, the last step's completed outputs)."""
+    if barrier is not None:
+        barrier()
+    sync()
+    t0 = clock()
+    for i in range(steps):
+        if watchdog:
+            watchdog.start_step(i)
+        loop.step(prefetch=i < steps - 1)
+        if watchdog:
+            watchdog.end_step()
+    if watchdog:
+        watchdog.start_step(steps)
+    out = loop.finish()
+    sync()
+    if watchdog:
+        watchdog.end_step()
+    if barrier is not None:
+        barrier()
+    sync()
+    return clock() - t0, out
 
 
 def free_port() -> int:
@@ -814,6 +936,9 @@ def main():
     ap.add_argument("--rccl-gather", action="store_true",
                     help="issue the per-step all-gather even at world 1 (forms a 1-rank "
                          "RCCL group), so the collective is inside the timed step")
+    ap.add_argument("--no-watchdog", dest="watchdog", action="store_false",
+                    help="no per-rank step watchdog (default: a timed step running longer than "
+                         "10x the median step prints its index and exits the rank with status 3)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo rehearsal of the N-rank launch and gather (no GPU)")
     ap.add_argument("--share-gpu", action="store_true",
@@ -871,8 +996,9 @@ def main():
     uploader = FrameUploader(host, dev)
     if args.resident:
         resident = [torch.from_numpy(h).to(dev) for h in host]
+    else:
+        resident = None
     any_frames = resident[0] if args.resident else uploader.dev[0]  # post-run measurements
-    step_no = [0]
 
     # FPN engines queue a step without any host read (sync=False): the mask
     # batch has pipe.mask_rows(F) rows and the gather ships exactly those
@@ -881,46 +1007,9 @@ def main():
                  else F * max(100, int(cfg.TEST.DETECTIONS_PER_IM)) + 64)
     gatherer = ResultGatherer(F, pipe.det_cap, cfg.MRCNN.RESOLUTION, world, dev,
                               mask_rows=mask_rows)
-    graphs = {}  # uploader slot -> (CUDAGraph, static output dict)
-    graph_note = [None]
-    use_graph = args.graph and asynchronous and not vos
-
-    pending = [None]
-    prev_out = [None]
-
-    def drain():  # the previous step's gather has landed (stream-ordered)
-        if pending[0] is not None:
-            pending[0].wait(views=False)
-            pending[0] = None
-
-    def step(prefetch):
-        t = step_no[0]
-        step_no[0] += 1
-        if vos and t % args.seq_len == 0:
-            pipe.reset()
-        frames = resident[t % n_host] if args.resident else uploader.get(t, prefetch)
-        key = frames.data_ptr()
-        if key in graphs:  # replay the captured step (hipGraph: one launch, no host work)
-            g, gout = graphs[key]
-            g.replay()
-            out = dict(gout)
-        else:
-            out = pipe.run(frames, sync=not asynchronous)
-        if not args.resident:
-            uploader.release(t)
-        if asynchronous:
-            # the previous step's one host read (counts, capacity, rare overflow
-            # masks) while this step runs on the GPU
-            if prev_out[0] is not None:
-                pipe.complete(prev_out[0])
-            prev_out[0] = out
-        if gatherer.collective:
-            # ONE packed all_gather per step over RCCL (runner.py), left in flight
-            # on RCCL's stream while the next step computes; at most one in flight
-            drain()
-            pending[0] = gatherer.gather_async(out["dets"], out["classes"], out["counts"],
-                                               out["masks"])
-        return out
+    use_graph = args.graph and getattr(pipe, "ASYNC", False) and not vos
+    loop = StepLoop(pipe, uploader, gatherer, vos=vos, seq_len=args.seq_len,
+                    resident=resident if args.resident else None)
 
     # MIOpen's first-shape search (cudnn.benchmark) keeps the first warm-up step
     # silent for a minute or more: a heartbeat on stderr shows the run is alive.
@@ -936,29 +1025,21 @@ def main():
     if rank == 0:
         threading.Thread(target=heartbeat, daemon=True).start()
     for i in range(args.warmup):
-        out = step(prefetch=i < args.warmup - 1)
+        loop.step(prefetch=i < args.warmup - 1)
         if rank == 0:
             print("bench: warm-up step %d/%d issued" % (i + 1, args.warmup),
                   file=sys.stderr, flush=True)
-    drain()
+    loop.drain()
     torch.cuda.synchronize()
     if use_graph:
-        capture_graphs(pipe, uploader.dev if not args.resident else resident, graphs,
-                       graph_note)
-        step_no[0] = 0  # restart the upload cycle at slot 0 for the timed region
+        loop.capture()  # restarts the upload cycle at slot 0 for the timed region
     warm_done.set()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        out = step(prefetch=i < args.steps - 1)
-    drain()  # the last step's gather is inside the timed region
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    from vosdetectron_amd.runner import StepWatchdog
+    watchdog = StepWatchdog(rank=rank) if args.watchdog else None
+    dt, out = timed_region(loop, args.steps, torch.cuda.synchronize,
+                           dist.barrier if world > 1 else None, watchdog)
+    if watchdog:
+        watchdog.stop()
     rank_ms = None
     if world > 1:  # every rank's own step time; the line's value uses the slowest
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
@@ -992,9 +1073,6 @@ def main():
                         "how": "the step's packed all_gather alone, %d times after the timed "
                                "region (in the step it overlaps the next step's compute)"
                                % args.steps}
-    if asynchronous:
-        pipe.complete(prev_out[0])
-        out = prev_out[0]
     dets_per_frame = float(np.mean(out["counts_host"]))
 
     stages = None
@@ -1066,8 +1144,8 @@ def main():
                        "layout": args.layout, "dets_per_frame": dets_per_frame, "h2d": h2d,
                        "gather_bytes_per_rank": gatherer.bytes_per_rank
                        if gatherer.collective else 0,
-                       "launch": "hipGraph replay per step" if graphs else
-                       ("eager (%s)" % graph_note[0] if graph_note[0] else "eager")},
+                       "launch": "hipGraph replay per step" if loop.graphs else
+                       ("eager (%s)" % loop.graph_note if loop.graph_note else "eager")},
             "roofline": roof, "cpu_baseline": cpu,
         }
         if rank_ms:

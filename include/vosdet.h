@@ -144,6 +144,13 @@ size_t vd_gemm_workspace_size(void);
  * "<arch> hipblaslt-<version>-<git revision> cu<CUs>" of the current device; a
  * plans file's "# key ..." line must equal it for the pins below it to apply. */
 int vd_gemm_plans_key(char *buf, int n);
+/* The GEMM plans this process has made, one line per shape:
+ * "M N K relu has_res own|blas workspace_bytes".  A plan with workspace_bytes > 0
+ * keeps inter-workgroup state (split-K partials, stream-K fix-up flags) in the
+ * caller's workspace, so two launches that may run concurrently (two captured
+ * steps replayed on two streams) must be given different workspaces.
+ * VD_ERR_WORKSPACE when n bytes cannot hold the list. */
+int vd_gemm_plan_list(char *buf, int n);
 int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,
                      const float *residual, int relu, float *D, void *workspace,
                      size_t workspace_bytes, void *stream);

@@ -171,3 +171,104 @@ def test_winograd_input_channel_limit():
     assert ops.WINO_MAX_CIN == 4096
     assert modeling.conv3x3_route(16, 4096, 256, 200, 336)[0] == "wino"
     assert modeling.conv3x3_route(16, 4104, 256, 200, 336)[0] != "wino"
+
+
+class _FakePipe:
+    """An ASYNC engine stand-in: run() queues, complete() is the host read."""
+    ASYNC = True
+
+    def __init__(self, events):
+        self.events = events
+
+    def run(self, frames, sync=True):
+        self.events.append(("run", int(frames[0])))
+        return {"frame": int(frames[0])}
+
+    def complete(self, out):
+        if "counts_host" not in out:
+            self.events.append(("complete", out["frame"]))
+            out["counts_host"] = [1]
+        return out
+
+
+def test_timed_region_includes_last_complete():
+    """the last timed step's complete() (the counts read and
+    any overflow batch) runs inside the timed region, before the clock stops."""
+    import torch
+    events = []
+    pipe = _FakePipe(events)
+    frames = [torch.tensor([i]) for i in range(4)]
+    loop = bench.StepLoop(pipe, None, None, resident=frames)
+    clock_calls = []
+
+    def clock():
+        events.append(("clock",))
+        clock_calls.append(len(events))
+        return float(len(clock_calls))
+
+    dt, out = bench.timed_region(loop, 3, lambda: events.append(("sync",)), clock=clock)
+    t0, t1 = events.index(("clock",)), len(events) - 1 - events[::-1].index(("clock",))
+    inside = events[t0:t1]
+    assert [e for e in inside if e[0] == "run"] == [("run", 0), ("run", 1), ("run", 2)]
+    # every step's host read, the last one included, happens between the clocks
+    assert [e for e in inside if e[0] == "complete"] == [("complete", 0), ("complete", 1),
+                                                         ("complete", 2)]
+    assert inside.index(("complete", 2)) < len(inside) and out["frame"] == 2
+    assert ("sync",) in events[t0:t1] and dt == 1.0
+
+
+def test_step_loop_gathers_each_step_once():
+    """StepLoop with a collective: one gather per step, at most one in flight,
+    each drained (on_gathered) before the next is issued, the last by finish()."""
+    import torch
+    events = []
+
+    class G:
+        collective = True
+
+        def gather_async(self, *a):
+            events.append(("gather", len([e for e in events if e[0] == "gather"])))
+
+            class P:
+                def wait(self, views=True):
+                    events.append(("wait",))
+            return P()
+
+    class Pipe(_FakePipe):
+        def run(self, frames, sync=True):
+            super().run(frames, sync)
+            return {"frame": int(frames[0]), "dets": 0, "classes": 0, "counts": 0, "masks": 0}
+
+    seen = []
+    loop = bench.StepLoop(Pipe(events), None, G(), resident=[torch.tensor([i]) for i in range(2)],
+                          on_gathered=lambda t, p: seen.append(t))
+    for _ in range(3):
+        loop.step()
+    loop.finish()
+    assert seen == [0, 1, 2]
+    kinds = [e[0] for e in events if e[0] in ("gather", "wait")]
+    assert kinds == ["gather", "wait", "gather", "wait", "gather", "wait"]
+
+
+def test_step_watchdog_trips_on_a_stalled_iteration():
+    """runner.StepWatchdog: iterations within 10x the median pass; one that runs
+    past max(10 x median, floor) trips with its index (on_trip instead of the
+    process exit the bench uses)."""
+    import time
+    from vosdetectron_amd.runner import StepWatchdog
+    trips = []
+    wd = StepWatchdog(factor=10.0, floor_s=0.05, first_s=5.0, poll_s=0.005,
+                      on_trip=lambda i, ran, lim: trips.append((i, ran, lim)))
+    try:
+        for i in range(4):
+            wd.start_step(i)
+            time.sleep(0.004)
+            wd.end_step()
+        assert wd.limit() == 0.05 or wd.limit() >= 10 * 0.004
+        wd.start_step(4)
+        deadline = time.time() + 3.0
+        while not trips and time.time() < deadline:
+            time.sleep(0.01)
+        assert trips and trips[0][0] == 4 and trips[0][1] > trips[0][2]
+    finally:
+        wd.stop()

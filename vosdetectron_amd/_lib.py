@@ -57,6 +57,7 @@ SIGNATURES = {
                                             _I, _I, _P, _P, _S, _P]),
     "vd_gemm_workspace_size": (_S, []),
     "vd_gemm_plans_key": (_I, [_P, _I]),
+    "vd_gemm_plan_list": (_I, [_P, _I]),
     "vd_gemm_bias_act": (_I, [_P, _I, _I, _P, _I, _P, _P, _I, _P, _P, _S, _P]),
     "vd_gemm_dual_bias_act": (_I, [_P, _I, _P, _I, _I, _P, _I, _P, _I, _P, _P]),
     "vd_conv3x3_bias_act": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P]),

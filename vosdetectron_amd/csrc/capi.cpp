@@ -121,6 +121,8 @@ int vd_gemm_plans_key(char *buf, int n) {
     return gemm_plans_key(buf, n);
 }
 
+int vd_gemm_plan_list(char *buf, int n) { return gemm_plan_list(buf, n); }
+
 int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,
                      const float *residual, int relu, float *D, void *workspace,
                      size_t workspace_bytes, void *stream) {

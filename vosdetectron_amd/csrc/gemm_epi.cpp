@@ -301,6 +301,29 @@ int gemm_plans_key(char *buf, int n) {
     return VD_OK;
 }
 
+// One line per planned shape: "M N K relu has_res own|blas ws_bytes".  A
+// hipBLASLt algorithm with ws_bytes > 0 keeps split-K partials / stream-K
+// fix-up state in the caller's workspace between its workgroups, so two GEMMs
+// given the same workspace must never run at the same time.
+int gemm_plan_list(char *buf, int n) {
+    std::lock_guard<std::mutex> g(g_mu);
+    if (!buf || n < 1) return VD_ERR_ARG;
+    int used = 0;
+    buf[0] = 0;
+    for (const auto &kv : g_plans) {
+        const Plan &p = kv.second;
+        if (!p.ok) continue;
+        const int w = snprintf(buf + used, (size_t)(n - used), "%d %d %d %d %d %s %zu\n",
+                               std::get<0>(kv.first), std::get<1>(kv.first),
+                               std::get<2>(kv.first), std::get<3>(kv.first),
+                               std::get<4>(kv.first), p.own ? "own" : "blas",
+                               p.own ? (size_t)0 : p.ws);
+        if (w < 0 || w >= n - used) return VD_ERR_WORKSPACE;  // buffer too small
+        used += w;
+    }
+    return VD_OK;
+}
+
 int launch_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,
                          const float *R, int relu, float *D, void *ws, size_t ws_bytes,
                          hipStream_t s) {

@@ -8,13 +8,20 @@
 //   collect / distribute lib/modeling/collect_and_distribute_fpn_rpn_proposals.py:91-138
 //   map_rois_to_fpn_levels lib/utils/fpn.py:11-28
 //
-// One workgroup (1024 threads) per (level, image) does the whole chain in LDS:
-//   select  -- top pre_nms_topN of the H*W*A scores by the unique 64-bit key
-//              (score, ~index): a strided sample fixes a threshold whose
-//              candidate set is exact-superset-checked by a count pass (binary
-//              search over the sample on miss), candidates are compacted and
-//              bitonic-sorted.  Equals numpy's argpartition+argsort top-k with
-//              ties broken by lower index (the stable reading).
+// select  -- top pre_nms_topN of the H*W*A scores by the unique 64-bit key
+//            (score, ~index).  Multi-workgroup radix select (round 5): every
+//            (level, image) score map is split into 4096-score chunks, one
+//            256-thread workgroup each (~2200 workgroups for 32 frames);
+//            rpn_sel_hist_kernel passes build 11-bit digit histograms of the
+//            keys still inside the boundary prefix, until the keys above the
+//            boundary bin fit the candidate capacity; rpn_sel_compact_kernel
+//            writes them to a per-slot candidate list.  Then one workgroup
+//            (1024 threads) per (level, image) does the rest of the chain in
+//            LDS: candidates bitonic-sorted, first pre taken.  Equals numpy's
+//            argpartition+argsort top-k with ties broken by lower index (the
+//            stable reading).  VOSDET_RPN_PRESEL=0 keeps round 4's single-
+//            workgroup select (a strided sample fixes a threshold whose
+//            candidate set is exact-superset-checked by count passes).
 //   decode  -- anchors + shifts (float64, as numpy) -> float32 boxes; the
 //              delta decode reproduces numpy 2's float64 promotion of dw/dh by
 //              the float64 BBOX_XFORM_CLIP; clip; min-size/centre filter.
@@ -81,14 +88,32 @@ static inline size_t rpn_slot_bytes(int max_pre, bool large) {
     return large ? rpn_mask_bytes(p) + rpn_box_bytes(p) + rpn_key_bytes(p) : rpn_mask_bytes(p);
 }
 
+size_t sel_slot_bytes(int cap);
+
+// Multi-workgroup select (default; VOSDET_RPN_PRESEL=0: round 4's one-workgroup
+// sample-and-count select) and its candidate capacity per slot: twice the
+// power of two above pre (the boundary bin then usually closes after two
+// passes), at most the kernel's LDS key capacity.
+static bool rpn_presel() {
+    const char *e = getenv("VOSDET_RPN_PRESEL");
+    return !(e && e[0] == '0');
+}
+static int rpn_sel_cap(int max_pre, bool large) {
+    const int sel_cap = large ? kSelCapL : kSelCap;
+    const int c = 2 * next_pow2(max_pre < 64 ? 64 : max_pre);
+    return c < sel_cap ? c : sel_cap;
+}
+
 size_t rpn_workspace_bytes(const VdRpnLevel *levels, int num_levels, int num_images,
                            int pre_nms_topN) {
     int max_pre;
     bool large;
     if (num_levels < 1 || !rpn_plan(levels, num_levels, pre_nms_topN, &max_pre, &large))
         return 256;
-    return rpn_slot_bytes(max_pre, rpn_split(large)) * (size_t)num_levels * (size_t)num_images +
-           256;
+    const size_t slots = (size_t)num_levels * (size_t)num_images;
+    size_t b = rpn_slot_bytes(max_pre, rpn_split(large)) * slots + 256;
+    if (rpn_presel()) b += sel_slot_bytes(rpn_sel_cap(max_pre, large)) * slots;
+    return b;
 }
 
 // numpy-2 bbox_transform of one box with weights (wx, wy, ww, wh): returns
@@ -187,12 +212,232 @@ __device__ inline void sweep_probs(const float *__restrict__ probs, int n, F f) 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Multi-workgroup radix select of the top `pre` 64-bit keys of every
+// (level, image) slot.  Key of element e (score s):
+//   key = float_key(s) << 32 | ~e          (unique; larger = earlier in the order)
+// Pass q histograms the q-th digit (11 bits; the last pass 9) of the keys whose
+// higher digits equal the boundary prefix fixed by passes < q.  From the
+// histograms every workgroup derives the same state: walking the bins from the
+// top, the boundary bin b of pass q holds the pre-th largest key; if the keys
+// at or above it (above + cum(b)) fit the candidate capacity, the select is
+// done with threshold "top bits >= prefix.b", else b extends the prefix.  Keys
+// are unique, so the last pass always ends it (one key per bin).
+static constexpr int kSelChunk = 4096;    // scores per select workgroup
+static constexpr int kSelThreads = 256;
+static constexpr int kSelPer = kSelChunk / kSelThreads;
+static constexpr int kRadixBins = 2048;   // 11-bit digits
+static constexpr int kRadixPasses = 6;    // 11 x 5 + 9 = 64 bits
+
+__host__ __device__ constexpr int radix_width(int q) { return q < 5 ? 11 : 9; }
+__host__ __device__ constexpr int radix_shift(int q) { return q < 5 ? 53 - 11 * q : 0; }
+
+struct SelState {
+    uint64_t prefix;  // fixed top `pbits` bits of the boundary
+    int pbits;
+    int above;        // keys strictly above the prefix range
+    int done;         // 1: candidates = keys whose top `pbits` bits >= prefix
+    int ncand;
+};
+
+struct SelSlot {  // per (image, level) slot; the candidate keys follow
+    uint32_t hist[kRadixPasses][kRadixBins];
+    SelState state[kRadixPasses];  // state[q]: after passes [0, q), by pass q's chunk 0
+    int32_t count;
+};
+size_t sel_slot_bytes(int cap) {
+    return a256(sizeof(SelSlot)) + a256(sizeof(uint64_t) * (size_t)cap);
+}
+
+struct SelLevels {  // per-level chunk offsets of the flattened grid
+    int chunk0[VD_MAX_LEVELS + 1];
+};
+
+// Apply pass q's histogram to the state after passes [0, q): identical in every
+// workgroup of the slot.  lds: int[16].  kSelThreads threads.
+__device__ inline void sel_step(const SelSlot *__restrict__ st, int q, int pre, int cap, int *lds,
+                                SelState &S) {
+    const int t = threadIdx.x, lane = lane_id(), wave = wave_id();
+    // thread t owns bins top - 8t - 0 .. top - 8t - 7 (highest first)
+    uint32_t h[8];
+    int tot = 0;
+    const int top = kRadixBins - 1 - 8 * t;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        h[i] = st->hist[q][top - i];
+        tot += (int)h[i];
+    }
+    int incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) lds[wave] = incl;
+    __syncthreads();
+    int wbase = 0;
+    for (int w = 0; w < wave; ++w) wbase += lds[w];
+    const int excl = wbase + incl - tot;
+    const int need = pre - S.above;  // >= 1, <= this prefix's key count
+    if (excl < need && excl + tot >= need) {
+        int acc = excl, i = 0;
+        for (; i < 7; ++i) {
+            if (acc + (int)h[i] >= need) break;
+            acc += (int)h[i];
+        }
+        lds[8] = top - i;  // boundary bin
+        lds[9] = acc;      // keys above it (within the prefix)
+        lds[10] = (int)h[i];
+    }
+    __syncthreads();
+    const int b = lds[8], cum_excl = lds[9], hb = lds[10];
+    __syncthreads();
+    const int w = radix_width(q);
+    S.prefix = (S.prefix << w) | (uint64_t)b;
+    S.pbits += w;
+    if (S.above + cum_excl + hb <= cap) {
+        S.done = 1;
+        S.ncand = S.above + cum_excl + hb;
+    } else {
+        S.above += cum_excl;
+    }
+}
+
+// The state after passes [0, q): pass q - 1's saved state plus its histogram.
+__device__ inline SelState sel_state(const SelSlot *__restrict__ st, int q, int pre, int cap,
+                                     int *lds) {
+    if (q == 0) return SelState{0ull, 0, 0, 0, 0};
+    SelState S = st->state[q - 1];
+    if (!S.done) sel_step(st, q - 1, pre, cap, lds, S);
+    return S;
+}
+
+__device__ __forceinline__ void sel_locate(const SelLevels &lvls, int num_levels, int &l,
+                                           int &chunk) {
+    const int bx = blockIdx.x;
+    l = 0;
+    while (l + 1 < num_levels && bx >= lvls.chunk0[l + 1]) ++l;
+    chunk = bx - lvls.chunk0[l];
+}
+
+__device__ __forceinline__ uint64_t sel_key(const VdRpnLevel &lv, int m, float s) {
+    const int K = lv.H * lv.W;
+    const int a = m / K, hw = m - a * K;
+    const int e = hw * lv.A + a;
+    return ((uint64_t)float_key(s) << 32) | (uint32_t)(0xffffffffu - (uint32_t)e);
+}
+
+// top `bits` bits of key == / >= prefix, testing the float key first (the
+// index part, an integer division, only when the score bits alone tie)
+__device__ __forceinline__ int sel_cmp(const VdRpnLevel &lv, int m, float s, uint64_t prefix,
+                                       int bits) {  // -1 below, 0 equal, 1 above
+    if (bits == 0) return 0;
+    const uint32_t fk = float_key(s);
+    if (bits <= 32) {
+        const uint32_t v = fk >> (32 - bits), p = (uint32_t)prefix;
+        return v == p ? 0 : (v > p ? 1 : -1);
+    }
+    const uint32_t ph = (uint32_t)(prefix >> (bits - 32));
+    if (fk != ph) return fk > ph ? 1 : -1;
+    const uint64_t v = sel_key(lv, m, s) >> (64 - bits);
+    return v == prefix ? 0 : (v > prefix ? 1 : -1);
+}
+
+__device__ __forceinline__ int sel_pre(int pre_nms_topN, int n_all) {
+    return (pre_nms_topN <= 0 || pre_nms_topN >= n_all) ? n_all : pre_nms_topN;
+}
+
+__global__ __launch_bounds__(kSelThreads) void rpn_sel_hist_kernel(
+    RpnArgs args, SelLevels lvls, int num_levels, int pre_nms_topN, int cap, int pass,
+    char *__restrict__ sel_ws, size_t sel_slot_b) {
+    __shared__ uint32_t lh[kRadixBins];
+    __shared__ int lds[16];
+    int l, chunk;
+    sel_locate(lvls, num_levels, l, chunk);
+    const int img = blockIdx.y;
+    const VdRpnLevel lv = args.lv[l];
+    const int K = lv.H * lv.W, n_all = K * lv.A;
+    const int pre = sel_pre(pre_nms_topN, n_all);
+    SelSlot *st = reinterpret_cast<SelSlot *>(sel_ws + (size_t)(img * num_levels + l) * sel_slot_b);
+    const SelState S = sel_state(st, pass, pre, cap, lds);
+    if (chunk == 0 && threadIdx.x == 0) st->state[pass] = S;  // for pass + 1
+    if (S.done) return;
+    for (int b = threadIdx.x; b < kRadixBins; b += kSelThreads) lh[b] = 0;
+    __syncthreads();
+    const float *probs = lv.cls_prob + (int64_t)img * n_all;
+    const int m0 = chunk * kSelChunk + threadIdx.x;
+    float v[kSelPer];
+#pragma unroll
+    for (int i = 0; i < kSelPer; ++i) {
+        const int m = m0 + i * kSelThreads;
+        v[i] = m < n_all ? probs[m] : 0.f;
+    }
+    const int sh = radix_shift(pass);
+    const uint32_t dmask = (1u << radix_width(pass)) - 1u;
+#pragma unroll
+    for (int i = 0; i < kSelPer; ++i) {
+        const int m = m0 + i * kSelThreads;
+        if (m >= n_all) continue;
+        if (pass == 0) {
+            atomicAdd(&lh[float_key(v[i]) >> 21], 1u);
+        } else if (sel_cmp(lv, m, v[i], S.prefix, S.pbits) == 0) {
+            const uint64_t key = sel_key(lv, m, v[i]);
+            atomicAdd(&lh[(uint32_t)(key >> sh) & dmask], 1u);
+        }
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < kRadixBins; b += kSelThreads)
+        if (lh[b]) atomicAdd(&st->hist[pass][b], lh[b]);
+}
+
+__global__ __launch_bounds__(kSelThreads) void rpn_sel_compact_kernel(
+    RpnArgs args, SelLevels lvls, int num_levels, int pre_nms_topN, int cap,
+    char *__restrict__ sel_ws, size_t sel_slot_b) {
+    __shared__ int lds[16];
+    int l, chunk;
+    sel_locate(lvls, num_levels, l, chunk);
+    const int img = blockIdx.y;
+    const VdRpnLevel lv = args.lv[l];
+    const int K = lv.H * lv.W, n_all = K * lv.A;
+    const int pre = sel_pre(pre_nms_topN, n_all);
+    char *slot = sel_ws + (size_t)(img * num_levels + l) * sel_slot_b;
+    SelSlot *st = reinterpret_cast<SelSlot *>(slot);
+    uint64_t *cand = reinterpret_cast<uint64_t *>(slot + a256(sizeof(SelSlot)));
+    const SelState S = sel_state(st, kRadixPasses, pre, cap, lds);
+    if (!S.done) {  // unreachable for unique keys; the slot's kernel reports it
+        if (chunk == 0 && threadIdx.x == 0) st->count = -(1 << 30);
+        return;
+    }
+    const float *probs = lv.cls_prob + (int64_t)img * n_all;
+    const int m0 = chunk * kSelChunk + threadIdx.x;
+    float v[kSelPer];
+#pragma unroll
+    for (int i = 0; i < kSelPer; ++i) {
+        const int m = m0 + i * kSelThreads;
+        v[i] = m < n_all ? probs[m] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < kSelPer; ++i) {
+        const int m = m0 + i * kSelThreads;
+        const bool p = m < n_all && sel_cmp(lv, m, v[i], S.prefix, S.pbits) >= 0;
+        const uint64_t b = ballot(p);
+        if (!b) continue;
+        const int leader = __ffsll((unsigned long long)b) - 1;
+        int base = 0;
+        if (lane_id() == leader) base = atomicAdd(&st->count, __popcll(b));
+        base = __shfl(base, leader);
+        const int pos = base + lane_prefix(b);
+        if (p && pos < cap) cand[pos] = sel_key(lv, m, v[i]);
+    }
+}
+
 template <int SelCap, int PreMax, bool GB>
 __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
     RpnArgs args, int num_levels, const float *__restrict__ im_info, int pre_nms_topN,
     int post_nms_topN, float nms_thresh, float min_size, float *__restrict__ rois_out,
     float *__restrict__ probs_out, int32_t *__restrict__ counts_out, char *__restrict__ ws,
-    size_t slot_bytes, size_t mask_bytes, size_t box_bytes) {
+    size_t slot_bytes, size_t mask_bytes, size_t box_bytes, const char *__restrict__ sel_ws,
+    size_t sel_slot_b) {
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     auto &L = *reinterpret_cast<RpnLds<SelCap, PreMax, GB> *>(lds_raw);
     PROF_DECL
@@ -244,6 +489,20 @@ __global__ __launch_bounds__(1024) void rpn_proposals_kernel(
     if (take_all) {
         for (int e = threadIdx.x; e < n_all; e += blockDim.x) L.keys[e] = key_of(e);
         ncand = n_all;
+        __syncthreads();
+    } else if (sel_ws) {
+        // candidates from the multi-workgroup radix select
+        const char *sl = sel_ws + (size_t)slot * sel_slot_b;
+        const uint64_t *cand = reinterpret_cast<const uint64_t *>(sl + a256(sizeof(SelSlot)));
+        ncand = reinterpret_cast<const SelSlot *>(sl)->count;
+        if (ncand < pre || ncand > SelCap) {  // cannot happen for unique keys: report
+            if (threadIdx.x == 0) {
+                counts_out[slot] = -1;
+                if (GB) *gm = -1;
+            }
+            return;
+        }
+        for (int i = threadIdx.x; i < ncand; i += blockDim.x) L.keys[i] = cand[i];
         __syncthreads();
     } else {
         // ---- sample + threshold search
@@ -448,6 +707,60 @@ __global__ __launch_bounds__(1024) void rpn_nms_mask_kernel(char *__restrict__ w
                         gridDim.x * wpb);
 }
 
+// Split NMS, phase 2 (round 5): one 256-thread workgroup per (64-row block,
+// slot) with the slot's boxes from the block's first row on staged in LDS, so
+// the IoU tests read LDS instead of one global load per lane and box; each
+// wave builds 16 rows, a row's words stored by the lanes in one coalesced
+// write.  (The one-wave-per-row form above keeps the large variant, whose
+// boxes exceed the LDS budget.)
+static constexpr int kMaskLdsMaxBoxes = 3200;  // 5 x 4 B x 3200 = 62.5 KiB
+
+__global__ __launch_bounds__(256) void rpn_nms_mask_lds_kernel(char *__restrict__ ws,
+                                                               size_t slot_bytes,
+                                                               size_t mask_bytes,
+                                                               size_t box_bytes, float nms_thresh) {
+    extern __shared__ __attribute__((aligned(16))) float lbox[];
+    const int slot = blockIdx.y;
+    char *base = ws + (size_t)slot * slot_bytes;
+    const int bstride = (int)(box_bytes / (10 * sizeof(float)));
+    const float *boxes = reinterpret_cast<const float *>(base + mask_bytes);
+    const int32_t m = *reinterpret_cast<const int32_t *>(
+        reinterpret_cast<const uint64_t *>(base + mask_bytes + box_bytes) + bstride);
+    const int r0 = blockIdx.x * 64;
+    if (m < 1 || r0 >= m) return;
+    const int n = m - r0;  // boxes [r0, m): this block's rows and every later column
+    float *X1 = lbox, *Y1 = lbox + n, *X2 = lbox + 2 * n, *Y2 = lbox + 3 * n, *AR = lbox + 4 * n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        X1[i] = boxes[5 * bstride + r0 + i];
+        Y1[i] = boxes[6 * bstride + r0 + i];
+        X2[i] = boxes[7 * bstride + r0 + i];
+        Y2[i] = boxes[8 * bstride + r0 + i];
+        AR[i] = boxes[9 * bstride + r0 + i];
+    }
+    __syncthreads();
+    uint64_t *mask = reinterpret_cast<uint64_t *>(base);
+    const int words = (m + 63) >> 6;
+    const int lane = lane_id();
+    const int w0 = blockIdx.x;  // the diagonal word of every row of this block
+    for (int rr = wave_id(); rr < 64 && r0 + rr < m; rr += num_waves()) {
+        const int i = r0 + rr;
+        const float ix1 = X1[rr], iy1 = Y1[rr], ix2 = X2[rr], iy2 = Y2[rr], ia = AR[rr];
+        uint64_t mine = 0;
+        for (int w = w0; w < words; ++w) {
+            const int j = (w << 6) + lane;  // column; local index j - r0
+            bool sup = false;
+            if (j > i && j < m) {
+                const int q = j - r0;
+                sup = suppresses(ix1, iy1, ix2, iy2, ia, X1[q], Y1[q], X2[q], Y2[q], AR[q],
+                                 nms_thresh);
+            }
+            const uint64_t b = ballot(sup);
+            if (lane == w - w0) mine = b;
+        }
+        if (lane < words - w0) mask[(int64_t)i * words + w0 + lane] = mine;
+    }
+}
+
 // Split NMS, phase 3: greedy resolve (one wave) + ascending compaction.  The
 // slot's mask is first copied into LDS by the whole workgroup when it fits
 // (m <= ~1300 at 160 KiB): the resolve then waits on LDS, not on a global
@@ -540,25 +853,62 @@ int launch_rpn_proposals(const VdRpnLevel *levels, int num_levels, int num_image
     if (!workspace || ws_bytes < sb * (size_t)num_levels * (size_t)num_images)
         return VD_ERR_WORKSPACE;
     const dim3 grid(num_levels, num_images);
+    // multi-workgroup select of every slot that keeps fewer than all its anchors
+    const char *sel_ws = nullptr;
+    size_t selb = 0;
+    if (rpn_presel()) {
+        SelLevels sl;
+        int nch = 0;
+        for (int l = 0; l < num_levels; ++l) {
+            sl.chunk0[l] = nch;
+            const int n_all = levels[l].A * levels[l].H * levels[l].W;
+            const bool take_all = pre_nms_topN <= 0 || pre_nms_topN >= n_all;
+            nch += take_all ? 0 : (n_all + kSelChunk - 1) / kSelChunk;
+        }
+        sl.chunk0[num_levels] = nch;
+        const int cap = rpn_sel_cap(max_pre, large);
+        selb = sel_slot_bytes(cap);
+        const size_t slots = (size_t)num_levels * (size_t)num_images;
+        if (ws_bytes < sb * slots + selb * slots) return VD_ERR_WORKSPACE;
+        char *sw = (char *)workspace + sb * slots;
+        sel_ws = sw;
+        if (nch > 0) {
+            if (hipMemsetAsync(sw, 0, selb * slots, s) != hipSuccess) return VD_ERR_LAUNCH;
+            const dim3 sgrid(nch, num_images);
+            for (int pass = 0; pass < kRadixPasses; ++pass)
+                hipLaunchKernelGGL(rpn_sel_hist_kernel, sgrid, dim3(kSelThreads), 0, s, args, sl,
+                                   num_levels, pre_nms_topN, cap, pass, sw, selb);
+            hipLaunchKernelGGL(rpn_sel_compact_kernel, sgrid, dim3(kSelThreads), 0, s, args, sl,
+                               num_levels, pre_nms_topN, cap, sw, selb);
+        }
+    }
     if (split) {
         if (large) {
             using Lds = RpnLds<kSelCapL, kPreMaxL, true>;
             hipLaunchKernelGGL((rpn_proposals_kernel<kSelCapL, kPreMaxL, true>), grid,
                                dim3(1024), sizeof(Lds), s, args, num_levels, im_info,
                                pre_nms_topN, post_nms_topN, nms_thresh, min_size, rois_out,
-                               probs_out, counts_out, (char *)workspace, sb, mb, bb);
+                               probs_out, counts_out, (char *)workspace, sb, mb, bb, sel_ws, selb);
         } else {
             using Lds = RpnLds<kSelCap, kPreMax, true>;
             hipLaunchKernelGGL((rpn_proposals_kernel<kSelCap, kPreMax, true>), grid, dim3(1024),
                                sizeof(Lds), s, args, num_levels, im_info, pre_nms_topN,
                                post_nms_topN, nms_thresh, min_size, rois_out, probs_out,
-                               counts_out, (char *)workspace, sb, mb, bb);
+                               counts_out, (char *)workspace, sb, mb, bb, sel_ws, selb);
         }
         if (nms_thresh > 0.f) {
-            const int rows_per_block = 16;  // 16 waves, one row each per pass
-            const dim3 mgrid((p + rows_per_block - 1) / rows_per_block, num_levels * num_images);
-            hipLaunchKernelGGL(rpn_nms_mask_kernel, mgrid, dim3(64 * rows_per_block), 0, s,
-                               (char *)workspace, sb, mb, bb, nms_thresh);
+            if (p <= kMaskLdsMaxBoxes && (p + 63) / 64 <= 64) {
+                const dim3 mgrid((p + 63) / 64, num_levels * num_images);
+                hipLaunchKernelGGL(rpn_nms_mask_lds_kernel, mgrid, dim3(256),
+                                   5 * sizeof(float) * (size_t)p, s, (char *)workspace, sb, mb,
+                                   bb, nms_thresh);
+            } else {
+                const int rows_per_block = 16;  // 16 waves, one row each per pass
+                const dim3 mgrid((p + rows_per_block - 1) / rows_per_block,
+                                 num_levels * num_images);
+                hipLaunchKernelGGL(rpn_nms_mask_kernel, mgrid, dim3(64 * rows_per_block), 0, s,
+                                   (char *)workspace, sb, mb, bb, nms_thresh);
+            }
             // keys / keep arrays for p candidates, plus the mask when it fits
             const size_t lbase = finish_lds_base(p);
             const int words = (p + 63) / 64;
@@ -574,7 +924,7 @@ int launch_rpn_proposals(const VdRpnLevel *levels, int num_levels, int num_image
         hipLaunchKernelGGL((rpn_proposals_kernel<kSelCap, kPreMax, false>), grid, dim3(1024),
                            sizeof(Lds), s, args, num_levels, im_info, pre_nms_topN,
                            post_nms_topN, nms_thresh, min_size, rois_out, probs_out, counts_out,
-                           (char *)workspace, sb, mb, bb);
+                           (char *)workspace, sb, mb, bb, sel_ws, selb);
     }
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }

@@ -46,6 +46,7 @@ int launch_prev_box_filter(float *dets, int32_t *classes, int32_t *counts, int F
                            float score_thresh, hipStream_t s);
 size_t gemm_epi_workspace_bytes();
 int gemm_plans_key(char *buf, int n);
+int gemm_plan_list(char *buf, int n);
 int launch_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,
                          const float *R, int relu, float *D, void *ws, size_t ws_bytes,
                          hipStream_t s);

@@ -494,6 +494,47 @@ def bias_act_(x: torch.Tensor, bias: Optional[torch.Tensor], residual=None, resi
 _GEMM_WS = {}
 
 
+def gemm_workspace(device) -> torch.Tensor:
+    """The hipBLASLt workspace for one vd_gemm_bias_act launch.  Algorithms with
+    a workspace keep inter-workgroup state in it (split-K partials, stream-K
+    fix-up flags; vd_gemm_plan_list shows which plans use one), so two GEMMs
+    that can run at the same time must not share it.  A captured step bakes the
+    pointer into its graph: the two captured steps of bench.capture_graphs,
+    replayed concurrently on two streams, shared the one per-device workspace of
+    round 4 and stopped making progress.  So:
+      * while the current stream is capturing, every call takes its workspace
+        from the graph's private memory pool (freed after the call, the caching
+        allocator hands the same block to the next GEMM of the same capture:
+        one workspace per graph, stream-ordered inside it);
+      * eager launches use one workspace per (device, stream)."""
+    device = torch.device(device)
+    if torch.cuda.is_current_stream_capturing():
+        return _ws(lib().vd_gemm_workspace_size(), device)
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    ws = _GEMM_WS.get(key)
+    if ws is None:
+        ws = _GEMM_WS[key] = _ws(lib().vd_gemm_workspace_size(), device)
+    return ws
+
+
+def gemm_plan_list() -> list:
+    """(M, N, K, relu, has_res, 'own' | 'blas', workspace_bytes) for every GEMM
+    shape this process has planned (vd_gemm_plan_list)."""
+    n = 1 << 16
+    while True:
+        buf = ctypes.create_string_buffer(n)
+        st = lib().vd_gemm_plan_list(buf, n)
+        if st != _lib.VD_ERR_WORKSPACE:
+            break
+        n *= 4
+    check(st, "vd_gemm_plan_list")
+    rows = []
+    for line in buf.value.decode().splitlines():
+        M, N, K, relu, res, what, ws = line.split()
+        rows.append((int(M), int(N), int(K), int(relu), int(res), what, int(ws)))
+    return rows
+
+
 def gemm_bias_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
                   residual: Optional[torch.Tensor] = None, relu: bool = True,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -518,10 +559,7 @@ def gemm_bias_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
         out = torch.empty((M, N), dtype=torch.float32, device=a_.device)
     elif tuple(out.shape) != (M, N) or not out.is_contiguous():
         raise ValueError("out must be a contiguous %s tensor" % ((M, N),))
-    ws = _GEMM_WS.get(a_.device)
-    if ws is None:  # one stream-ordered workspace per device (single launch stream)
-        ws = _ws(lib().vd_gemm_workspace_size(), a_.device)
-        _GEMM_WS[a_.device] = ws
+    ws = gemm_workspace(a_.device)
     st = lib().vd_gemm_bias_act(a_.data_ptr(), M, K, w_.data_ptr(), N, b_.data_ptr(),
                                 r_.data_ptr() if r_ is not None else None, int(relu),
                                 out.data_ptr(), ws.data_ptr(), ws.numel(), _stream())

@@ -261,3 +261,79 @@ class FrameUploader:
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream())
         self.free[t % 2] = ev
+
+
+class StepWatchdog:
+    """Per-rank watchdog over a timed step loop (a stalled step must
+    end the run with its index, not at the launcher's time limit).  The loop
+    calls start_step(i) / end_step() around each iteration; a daemon thread
+    checks the running iteration against max(factor x the median of the
+    iterations done so far, floor_s) -- first_s until three have finished -- and
+    on a trip prints the rank, iteration and times and exits the process with
+    status 3 (os._exit: no re-exec, no cleanup that could block on the stalled
+    device).  With graph replay an iteration mostly waits in the previous step's
+    host read, so a stalled step t trips at iteration t or t + 1.  The reference
+    has no equivalent (its per-GPU subprocesses are joined without a timeout,
+    lib/utils/subprocess.py:84-101)."""
+
+    def __init__(self, rank: int = 0, factor: float = 10.0, floor_s: float = 2.0,
+                 first_s: float = 120.0, poll_s: float = 0.05, on_trip=None):
+        import threading
+        self.rank, self.factor, self.floor_s, self.first_s = rank, factor, floor_s, first_s
+        self.poll_s = poll_s
+        self.on_trip = on_trip
+        self.durations: List[float] = []
+        self.current = None  # (iteration, start time)
+        self.tripped = None
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._watch, daemon=True)
+        self._thread.start()
+
+    def limit(self) -> float:
+        with self._lock:
+            d = list(self.durations)
+        if len(d) < 3:
+            return self.first_s
+        return max(self.factor * float(np.median(d)), self.floor_s)
+
+    def start_step(self, i: int):
+        import time
+        with self._lock:
+            self.current = (i, time.perf_counter())
+
+    def end_step(self):
+        import time
+        with self._lock:
+            if self.current is not None:
+                self.durations.append(time.perf_counter() - self.current[1])
+            self.current = None
+
+    def stop(self):
+        self._stop.set()
+        self._thread.join(timeout=5.0)
+
+    def _watch(self):
+        import os
+        import sys
+        import time
+        while not self._stop.wait(self.poll_s):
+            lim = self.limit()
+            with self._lock:
+                cur = self.current
+                med = float(np.median(self.durations)) if self.durations else None
+            if cur is None:
+                continue
+            ran = time.perf_counter() - cur[1]
+            if ran <= lim:
+                continue
+            self.tripped = (cur[0], ran, lim)
+            print("watchdog: rank %d, timed iteration %d has run %.2f s > limit %.2f s "
+                  "(median iteration %s): stopping the rank"
+                  % (self.rank, cur[0], ran, lim,
+                     "%.1f ms" % (med * 1e3) if med is not None else "n/a"),
+                  file=sys.stderr, flush=True)
+            if self.on_trip is not None:
+                self.on_trip(*self.tripped)
+                return
+            os._exit(3)
