@@ -151,10 +151,14 @@ def test_generate_proposals_large_vs_oracle(seed, pre, A, H, W):
         assert np.array_equal(pr[img, 0, :k], ref_p[sel, 0]), img
 
 
+@pytest.mark.parametrize("presel", ["1", "0"])
 @pytest.mark.parametrize("seed,ties", [(0, False), (1, True), (2, True)])
-def test_generate_proposals_vs_oracle_batched(seed, ties):
-    """Two images, full-size P2..P6 of an 800x1344 blob, tied scores."""
+def test_generate_proposals_vs_oracle_batched(seed, ties, presel, monkeypatch):
+    """Two images, full-size P2..P6 of an 800x1344 blob, tied scores; through the
+    multi-workgroup radix select (default) and round 4's one-workgroup select
+    (VOSDET_RPN_PRESEL=0)."""
     from vosdetectron_amd import ops
+    monkeypatch.setenv("VOSDET_RPN_PRESEL", presel)
     rng = np.random.default_rng(seed)
     N = 2
     shapes = {2: (200, 336), 3: (100, 168), 4: (50, 84), 5: (25, 42), 6: (13, 21)}
@@ -191,6 +195,45 @@ def test_generate_proposals_vs_oracle_batched(seed, ties):
         assert np.array_equal(cr[img, :ccnt[img]], col)
         lvls = orc.map_rois_to_fpn_levels(col[:, 1:5], 2, 5).astype(np.int32) - 2
         assert np.array_equal(clv[img, :ccnt[img]], lvls)
+
+
+@pytest.mark.parametrize("case", ["all_equal", "two_values", "just_above_pre", "negative",
+                                  "pre_eq_cap"])
+def test_radix_select_edge_cases(case):
+    """The multi-workgroup radix select where its passes run deepest: every score
+    equal (the boundary is fixed by the index digits alone, all six passes),
+    two distinct values, n_all = pre + 1, negative and zero scores (sign-flipped
+    float keys), and pre = 2048 on a level of 3 x 200 x 336 (candidate capacity
+    = 2 x pre).  Bit-exact vs the oracle (lower index wins ties)."""
+    from vosdetectron_amd import ops
+    rng = np.random.default_rng(7)
+    A, H, W, pre = 3, 200, 336, 1000
+    if case == "just_above_pre":
+        H, W = 7, 48  # 1008 anchors, pre 1000 -> 1007 would be take-all
+        pre = 1000
+    p = rng.uniform(0, 1, (1, A, H, W)).astype(np.float32)
+    if case == "all_equal":
+        p[:] = np.float32(0.5)
+    elif case == "two_values":
+        p = np.where(p < 0.5, np.float32(0.25), np.float32(0.75)).astype(np.float32)
+    elif case == "negative":
+        p = -np.abs(rng.normal(0, 1, (1, A, H, W))).astype(np.float32)
+        p[0, 0, :5] = 0.0
+        p[0, 1, :5] = -0.0
+    elif case == "pre_eq_cap":
+        pre = 2048
+    d = rng.normal(0, 0.5, (1, 4 * A, H, W)).astype(np.float32)
+    info = np.array([[H * 4, W * 4, 1.0]], np.float32)
+    an = orc.fpn_level_anchors(2)
+    rois, pr, cnt = [t.cpu().numpy() for t in ops.generate_proposals(
+        [torch.from_numpy(p).to(DEV)], [torch.from_numpy(d).to(DEV)],
+        [torch.from_numpy(an).to(DEV)], [1. / 4], torch.from_numpy(info).to(DEV), pre, 1000,
+        0.7, 0)]
+    ref_r, ref_p = orc.generate_proposals(an, 1. / 4, p, d, info, pre, 1000, 0.7, 0)
+    k = cnt[0, 0]
+    assert k == len(ref_r), (k, len(ref_r))
+    assert np.array_equal(rois[0, 0, :k], ref_r)
+    assert np.array_equal(pr[0, 0, :k], ref_p[:, 0])
 
 
 @pytest.mark.parametrize("seed", [0, 1])

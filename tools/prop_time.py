@@ -1,10 +1,10 @@
 import sys, os, time
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 from oracle import oracle as orc
 from vosdetectron_amd import ops
 dev = "cuda"
-N = 16
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 shapes = {2: (200, 336), 3: (100, 168), 4: (50, 84), 5: (25, 42), 6: (13, 21)}
 rng = np.random.default_rng(0)
 probs = [torch.from_numpy(rng.uniform(0, 1, (N, 3, H, W)).astype(np.float32)).to(dev) for H, W in shapes.values()]
@@ -15,7 +15,10 @@ def run(thr, lv=None):
     idx = range(5) if lv is None else [lv]
     return ops.generate_proposals([probs[i] for i in idx], [deltas[i] for i in idx], [an[i] for i in idx],
                                   [1. / 2 ** (i + 2) for i in idx], info, 1000, 1000, thr, 0)
-for name, thr, lv in [("all nms", 0.7, None), ("all no-nms", 0.0, None), ("P2 nms", 0.7, 0), ("P2 no-nms", 0.0, 0), ("P3 nms", 0.7, 1)]:
+for presel in ("1", "0"):
+  os.environ["VOSDET_RPN_PRESEL"] = presel
+  print("VOSDET_RPN_PRESEL=%s, %d images" % (presel, N), flush=True)
+  for name, thr, lv in [("all nms", 0.7, None), ("all no-nms", 0.0, None), ("P2 nms", 0.7, 0), ("P2 no-nms", 0.0, 0), ("P3 nms", 0.7, 1)]:
     for _ in range(3): run(thr, lv)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
