@@ -33,6 +33,14 @@ enum {
 
 enum { VD_LAYOUT_NCHW = 0, VD_LAYOUT_NHWC = 1 };
 
+/* Per-frame failure codes written in place of a device count (never a valid
+ * count; downstream kernels treat a negative count as an empty frame and keep it):
+ *   VD_COUNT_SELECT_FAILED   the proposal top-k could not bracket pre_nms_topN
+ *   VD_COUNT_PREV_BOXES      NMS_SMALL_BOX_IOU: the previous frame kept more
+ *                            than one box of a class (vos_test.py:848 asserts) */
+#define VD_COUNT_SELECT_FAILED (-1)
+#define VD_COUNT_PREV_BOXES (-2)
+
 int vd_version(void);
 const char *vd_status_string(int status);
 
@@ -245,8 +253,9 @@ int vd_mask_iou_nms(const uint8_t *planes, int n, int im_h, int im_w, const floa
  * writes them): for each class whose previous-frame result (prev_* of the same
  * row, [F][prev_cap]) holds one box with score >= score_thresh, the class's
  * boxes with IoU (bb_intersection_over_union, float32) < iou_thresh are dropped;
- * order kept.  A class with several previous boxes (the reference asserts) sets
- * the frame's count to -1.  det_cap <= 1024. */
+ * order kept.  A previous result with several boxes of one class (the reference
+ * asserts for every class, vos_test.py:846-848) sets the frame's count to
+ * VD_COUNT_PREV_BOXES.  det_cap <= 1024. */
 int vd_detections_prev_box_filter(float *dets, int32_t *classes, int32_t *counts, int F,
                                   int det_cap, const float *prev_dets,
                                   const int32_t *prev_classes, const int32_t *prev_counts,

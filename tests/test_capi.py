@@ -74,6 +74,14 @@ def test_miopen_db_is_a_per_process_copy():
         assert names == repr(seed) or eval(names) == seed
         assert not os.path.exists(d)  # removed at exit
     assert outs[0][0] != outs[1][0]
+    # a child started by an importing parent inherits the parent's path
+    # but not its ownership -- it seeds a copy of its own
+    code = ("import os, subprocess, sys, vosdetectron_amd; print(os.environ['MIOPEN_USER_DB_PATH']); "
+            "sys.stdout.flush(); subprocess.run([sys.executable, '-c', 'import os, vosdetectron_amd; "
+            "print(os.environ[\\'MIOPEN_USER_DB_PATH\\'])'])")
+    parent, child = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                                   env=env, cwd=root, timeout=120).stdout.splitlines()
+    assert parent != child and not os.path.exists(child)
 
 
 @pytest.mark.gpu

@@ -71,10 +71,6 @@ def test_unsupported_overrides_raise():
     with pytest.raises(NotImplementedError, match="BBOX_VOTE"):
         vcfg.merge_cfg_from_list(["TEST.BBOX_VOTE.ENABLED", "True",
                                   "TEST.BBOX_VOTE.SCORING_METHOD", "TEMP_AVG"])
-    with pytest.raises(NotImplementedError, match="BBOX_VOTE"):
-        vcfg.load_cfg(overrides={"TEST.BBOX_VOTE.ENABLED": True,
-                                 "TEST.BBOX_VOTE.SCORING_METHOD": "GENERALIZED_AVG",
-                                 "TEST.BBOX_VOTE.SCORING_METHOD_BETA": 2.0})
     with pytest.raises(NotImplementedError, match="SOFT_NMS"):
         vcfg.load_cfg(overrides={"TEST.SOFT_NMS.ENABLED": True, "TEST.SOFT_NMS.METHOD": "cubic"})
     # disabled values are accepted
@@ -92,6 +88,13 @@ def test_soft_nms_and_box_voting_are_built():
         c = vcfg.load_cfg(overrides={"TEST.BBOX_VOTE.ENABLED": True,
                                      "TEST.BBOX_VOTE.SCORING_METHOD": sm})
         assert nms_options(c)["bbox_vote"] == sm
+    # SCORING_METHOD_BETA never reaches box_voting in the reference (test.py:770-775,
+    # vos_test.py:786-791): beta stays 1, GENERALIZED_AVG at any beta is AVG
+    for sm in ("QUASI_SUM", "GENERALIZED_AVG"):
+        c = vcfg.load_cfg(overrides={"TEST.BBOX_VOTE.ENABLED": True,
+                                     "TEST.BBOX_VOTE.SCORING_METHOD": sm,
+                                     "TEST.BBOX_VOTE.SCORING_METHOD_BETA": 2.0})
+        assert nms_options(c)["bbox_vote_beta"] == 1.0
     assert nms_options(vcfg.load_cfg()) == {}
     c = vcfg.load_cfg(os.path.join(REF, "lib_vos/tools/R-101-FPN_3x_gn_train_online.yaml")) \
         if os.path.isdir(REF) else None

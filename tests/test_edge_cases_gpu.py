@@ -136,14 +136,18 @@ def test_proposals_size_limits():
                                torch.tensor([[640., 960., 1.]], device=DEV), 8193, 1000, 0.7, 0)
 
 
-def test_proposals_unbracketable_topk_fails_loudly():
-    """a score map on which the top-k threshold search cannot bracket
-    pre_nms_topN within its candidate capacity (the sampled anchors score 0 but
-    four, every other anchor 0.5: 197k candidates tie between two adjacent
-    sample keys) must not drop the level silently -- its count is -1, which
-    collect_distribute and box_detections pass on and the engine raises on."""
+def test_proposals_unbracketable_topk_fails_loudly(monkeypatch):
+    """a score map on which the one-workgroup top-k threshold search
+    (VOSDET_RPN_PRESEL=0) cannot bracket pre_nms_topN within its candidate
+    capacity (the sampled anchors score 0 but four, every other anchor 0.5: 197k
+    candidates tie between two adjacent sample keys) must not drop the level
+    silently -- its count is -1, which collect_distribute and box_detections pass
+    on and the engine raises on.  The default multi-workgroup radix select
+    resolves the same map exactly (its index digits split the tie): checked
+    against the oracle."""
     from vosdetectron_amd import ops
     from vosdetectron_amd._lib import VosdetError
+    monkeypatch.setenv("VOSDET_RPN_PRESEL", "0")
     H, W, A = 200, 336, 3
     n_all, S = H * W * A, 2048  # kSampleMax
     flat = np.full(n_all, 0.5, np.float32)  # element order e = (h*W + w)*A + a
@@ -168,6 +172,16 @@ def test_proposals_unbracketable_topk_fails_loudly():
     assert dcnt.cpu().tolist() == [-1]
     with pytest.raises(VosdetError):
         ops.raise_on_failed_counts(dcnt.cpu().tolist())
+    monkeypatch.setenv("VOSDET_RPN_PRESEL", "1")
+    rois, pr, cnt = ops.generate_proposals(
+        [torch.from_numpy(p).to(DEV)], [torch.from_numpy(d).to(DEV)],
+        [torch.from_numpy(an).to(DEV)], [1. / 4], info, 1000, 1000, 0.7, 0)
+    ref_r, ref_p = orc.generate_proposals(an, 1. / 4, p, d, info.cpu().numpy(), 1000, 1000,
+                                          0.7, 0)
+    k = int(cnt[0, 0])
+    assert k == len(ref_r) and k > 0
+    assert np.array_equal(rois[0, 0, :k].cpu().numpy(), ref_r)
+    assert np.array_equal(pr[0, 0, :k].cpu().numpy(), ref_p[:, 0])
 
 
 def test_roi_align_fpn_malformed_indices_pool_to_zero():

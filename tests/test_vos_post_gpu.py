@@ -88,19 +88,24 @@ def test_prev_box_filter_vs_executed_reference(golden):
 
 def test_prev_box_filter_no_prev_and_assert():
     """A row without a previous result passes unchanged; two previous boxes of one
-    class (the reference asserts) fail the row with count -1."""
-    from vosdetectron_amd import ops
-    D = torch.rand((2, 8, 5), device=DEV) * 100
+    class (the reference asserts for every class, vos_test.py:846-848) fail the row
+    with VD_COUNT_PREV_BOXES -- also when the current frame has no box of that
+    class (row 2) -- and complete()'s check names the heuristic."""
+    from vosdetectron_amd import _lib, ops
+    D = torch.rand((3, 8, 5), device=DEV) * 100
     D[..., 2:4] += D[..., 0:2]
-    C = torch.tensor([[1, 1, 2, 3, 3, 3, 4, 5]] * 2, dtype=torch.int32, device=DEV)
-    N = torch.tensor([8, 8], dtype=torch.int32, device=DEV)
+    C = torch.tensor([[1, 1, 2, 3, 3, 3, 4, 5]] * 3, dtype=torch.int32, device=DEV)
+    N = torch.tensor([8, 8, 8], dtype=torch.int32, device=DEV)
     D0 = D.clone()
-    PD = torch.zeros((2, 4, 5), device=DEV)
-    PC = torch.tensor([[3, 0, 0, 0], [3, 3, 0, 0]], dtype=torch.int32, device=DEV)
-    PN = torch.tensor([0, 2], dtype=torch.int32, device=DEV)
+    PD = torch.zeros((3, 4, 5), device=DEV)
+    PC = torch.tensor([[3, 0, 0, 0], [3, 3, 0, 0], [1, 7, 7, 0]], dtype=torch.int32, device=DEV)
+    PN = torch.tensor([0, 2, 3], dtype=torch.int32, device=DEV)
     ops.detections_prev_box_filter(D, C, N, PD, PC, PN, 0.3, 0.0)
     assert int(N[0]) == 8 and torch.equal(D[0], D0[0])
-    assert int(N[1]) == -1
+    assert int(N[1]) == ops.COUNT_PREV_BOXES == -2
+    assert int(N[2]) == ops.COUNT_PREV_BOXES
+    with pytest.raises(_lib.VosdetError, match="NMS_SMALL_BOX_IOU"):
+        ops.raise_on_failed_counts(N.cpu().tolist())
 
 
 @pytest.fixture(scope="module")
@@ -182,3 +187,19 @@ def test_vos_pipeline_heuristics_stagewise(vos_seq):
                     fin[j] = cls_boxes[j]
             prev[f] = fin
     assert filtered_any, "the previous-frame filter never removed a detection"
+
+
+def test_vos_heuristics_refuse_unfinalized_steps(vos_seq):
+    """with NMS_WITH_MASK_IOU / NMS_SMALL_BOX_IOU on, a second run()
+    before frame_results(previous) would filter against the wrong frame, and
+    frame_segms would skip the mask-IoU NMS: both raise instead."""
+    from vosdetectron_amd.engine import frame_segms
+    cfg, pipe, frames = vos_seq
+    pipe.reset()
+    out = pipe.run(torch.from_numpy(frames[0]).to(DEV))
+    with pytest.raises(RuntimeError, match="frame_results"):
+        pipe.run(torch.from_numpy(frames[1]).to(DEV))
+    with pytest.raises(ValueError, match="frame_results"):
+        frame_segms(pipe, out, int(cfg.MODEL.NUM_CLASSES))
+    pipe.frame_results(out)
+    pipe.frame_results(pipe.run(torch.from_numpy(frames[1]).to(DEV)))  # now allowed

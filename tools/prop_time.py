@@ -15,9 +15,10 @@ def run(thr, lv=None):
     idx = range(5) if lv is None else [lv]
     return ops.generate_proposals([probs[i] for i in idx], [deltas[i] for i in idx], [an[i] for i in idx],
                                   [1. / 2 ** (i + 2) for i in idx], info, 1000, 1000, thr, 0)
-for presel in ("1", "0"):
+for presel, mlds in (("1", "1"), ("0", "1"), ("1", "0")):
   os.environ["VOSDET_RPN_PRESEL"] = presel
-  print("VOSDET_RPN_PRESEL=%s, %d images" % (presel, N), flush=True)
+  os.environ["VOSDET_RPN_MASK_LDS"] = mlds
+  print("VOSDET_RPN_PRESEL=%s VOSDET_RPN_MASK_LDS=%s, %d images" % (presel, mlds, N), flush=True)
   for name, thr, lv in [("all nms", 0.7, None), ("all no-nms", 0.0, None), ("P2 nms", 0.7, 0), ("P2 no-nms", 0.0, 0), ("P3 nms", 0.7, 1)]:
     for _ in range(3): run(thr, lv)
     torch.cuda.synchronize()

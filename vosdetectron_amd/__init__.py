@@ -15,12 +15,18 @@ os.environ.setdefault("MIOPEN_FIND_MODE", "1")
 # copies it to its own temporary directory and points MIOPEN_USER_DB_PATH there,
 # so problems not in it are found and appended to the copy -- eight ranks never
 # write one shared file and no run dirties the repository.
-# A caller's own MIOPEN_USER_DB_PATH wins (VOSDET_MIOPEN_DB_SEED=0: no seed).
+# A caller's own MIOPEN_USER_DB_PATH wins (VOSDET_MIOPEN_DB_SEED=0: no seed).  The
+# copy's owner PID travels with it (VOSDET_MIOPEN_DB_OWNER): a child process that
+# inherits the variable (a rank spawned by an importing parent) makes its own copy
+# instead of sharing the parent's, which the parent deletes at exit.
 
 
 def _seed_miopen_db():
-    if "MIOPEN_USER_DB_PATH" in os.environ or os.environ.get("VOSDET_MIOPEN_DB_SEED") == "0":
+    if os.environ.get("VOSDET_MIOPEN_DB_SEED") == "0":
         return
+    owner = os.environ.get("VOSDET_MIOPEN_DB_OWNER")
+    if "MIOPEN_USER_DB_PATH" in os.environ and (owner is None or owner == str(os.getpid())):
+        return  # the caller's own path, or this process's copy
     import atexit
     import shutil
     import tempfile
@@ -33,6 +39,7 @@ def _seed_miopen_db():
         return  # no writable temp dir: MIOpen uses its own default location
     atexit.register(shutil.rmtree, d, True)
     os.environ["MIOPEN_USER_DB_PATH"] = d
+    os.environ["VOSDET_MIOPEN_DB_OWNER"] = str(os.getpid())
 
 
 _seed_miopen_db()

@@ -116,11 +116,11 @@ def _merge(a, b):
 # Inference options of the reference that change detections and are not built
 # here: (dotted key, "enabled" predicate, where the reference implements it).
 UNSUPPORTED = (
-    ("TEST.BBOX_VOTE", lambda v: bool(v.get("ENABLED")) and not (
-        v.get("SCORING_METHOD") in ("ID", "AVG", "IOU_AVG", "QUASI_SUM") or (
-            v.get("SCORING_METHOD") == "GENERALIZED_AVG" and v.get("SCORING_METHOD_BETA") == 1.0)),
-     "box-voting scoring TEMP_AVG / GENERALIZED_AVG at beta != 1 (numpy float32 log / exp / "
-     "pow), lib/utils/boxes.py:300-331"),
+    # the reference's call sites never pass SCORING_METHOD_BETA (test.py:770-775),
+    # so GENERALIZED_AVG always runs at beta 1 = AVG; only TEMP_AVG is missing
+    ("TEST.BBOX_VOTE", lambda v: bool(v.get("ENABLED")) and v.get("SCORING_METHOD") not in (
+        "ID", "AVG", "IOU_AVG", "QUASI_SUM", "GENERALIZED_AVG"),
+     "box-voting scoring TEMP_AVG (numpy float32 log / exp), lib/utils/boxes.py:300-320"),
     ("TEST.SOFT_NMS", lambda v: bool(v.get("ENABLED")) and v.get("METHOD") not in (
         "hard", "linear", "gaussian"), "soft-NMS method (boxes.py:344 asserts)"),
     ("TEST.BBOX_AUG.ENABLED", bool, "box test-time augmentation, lib/core/test.py:193-727"),

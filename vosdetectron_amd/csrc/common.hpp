@@ -11,6 +11,14 @@
 
 #define VD_WAVE 64
 
+// gfx950 only: the launches size LDS for its 160 KiB per workgroup (NMS resolve
+// in LDS, det_limit's staged rows, soft-NMS at kSoftMax, the proposal select's
+// candidate keys) and the MFMA kernels use its instruction set.
+#define VD_LDS_BYTES (160 * 1024)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "vosdetectron_amd kernels target gfx950 (160 KiB LDS per workgroup) only"
+#endif
+
 namespace vd {
 
 // Orderable 32-bit key of a float: unsigned comparison of keys == numeric
@@ -280,6 +288,10 @@ __device__ __forceinline__ bool suppresses(float ix1, float iy1, float ix2, floa
     float w = cy_max(0.0f, xx2 - xx1 + 1.0f);
     float h = cy_max(0.0f, yy2 - yy1 + 1.0f);
     float inter = w * h;
+    // Disjoint boxes (most pairs of an NMS) have inter = 0, so ovr = +-0 or NaN:
+    // never >= a positive thresh.  A wave with no overlapping pair skips the
+    // IEEE division (~10 VALU with a quarter-rate rcp); the result is unchanged.
+    if (thresh > 0.f && ballot(inter > 0.f) == 0ull) return false;
     float ovr = inter / (iarea + jarea - inter);
     return ovr >= thresh;
 }

@@ -120,7 +120,7 @@ int launch_nms(const float *dets, int n, int stride, float thresh, int64_t *keep
     hipLaunchKernelGGL(nms_mask_kernel, dim3((n + rows_per_block - 1) / rows_per_block),
                        dim3(64 * rows_per_block), 0, s, n, thresh, ws);
     const size_t mask_bytes = sizeof(uint64_t) * (size_t)n * (size_t)((n + 63) / 64);
-    const int in_lds = mask_bytes + 2 * kNmsMaxN + 256 <= 160 * 1024;
+    const int in_lds = mask_bytes + 2 * kNmsMaxN + 256 <= VD_LDS_BYTES;
     hipLaunchKernelGGL(nms_resolve_kernel, dim3(1), dim3(1024), in_lds ? mask_bytes : 0, s, n, ws,
                        keep, nkeep, in_lds);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;

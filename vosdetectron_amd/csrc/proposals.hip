@@ -42,7 +42,7 @@ static constexpr int kSampleMax = 2048;
 // per-candidate box arrays in the global workspace.
 static constexpr int kSelCapL = 16384;
 static constexpr int kPreMaxL = 8192;
-static_assert(sizeof(uint64_t) * kSelCapL + 2 * kPreMaxL + 128 <= 160 * 1024, "LDS");
+static_assert(sizeof(uint64_t) * kSelCapL + 2 * kPreMaxL + 128 <= VD_LDS_BYTES, "LDS");
 static constexpr double kBboxXformClip = 4.135166556742356;  // np.log(1000. / 16.)
 
 struct RpnArgs {
@@ -96,6 +96,12 @@ size_t sel_slot_bytes(int cap);
 // passes), at most the kernel's LDS key capacity.
 static bool rpn_presel() {
     const char *e = getenv("VOSDET_RPN_PRESEL");
+    return !(e && e[0] == '0');
+}
+// Mask build of the split NMS: the LDS-staged row-block kernel (default) or the
+// one-wave-per-row kernel (VOSDET_RPN_MASK_LDS=0)
+static bool rpn_mask_lds() {
+    const char *e = getenv("VOSDET_RPN_MASK_LDS");
     return !(e && e[0] == '0');
 }
 static int rpn_sel_cap(int max_pre, bool large) {
@@ -897,7 +903,7 @@ int launch_rpn_proposals(const VdRpnLevel *levels, int num_levels, int num_image
                                counts_out, (char *)workspace, sb, mb, bb, sel_ws, selb);
         }
         if (nms_thresh > 0.f) {
-            if (p <= kMaskLdsMaxBoxes && (p + 63) / 64 <= 64) {
+            if (rpn_mask_lds() && p <= kMaskLdsMaxBoxes && (p + 63) / 64 <= 64) {
                 const dim3 mgrid((p + 63) / 64, num_levels * num_images);
                 hipLaunchKernelGGL(rpn_nms_mask_lds_kernel, mgrid, dim3(256),
                                    5 * sizeof(float) * (size_t)p, s, (char *)workspace, sb, mb,
@@ -913,7 +919,7 @@ int launch_rpn_proposals(const VdRpnLevel *levels, int num_levels, int num_image
             const size_t lbase = finish_lds_base(p);
             const int words = (p + 63) / 64;
             const size_t lmask = (size_t)p * words * 8;
-            const bool in_lds = lbase + lmask <= 160 * 1024;
+            const bool in_lds = lbase + lmask <= VD_LDS_BYTES;
             hipLaunchKernelGGL(rpn_nms_finish_kernel, grid, dim3(1024),
                                lbase + (in_lds ? lmask : 0), s, num_levels, post_nms_topN,
                                rois_out, probs_out, counts_out, (char *)workspace, sb, mb, bb,

@@ -577,7 +577,7 @@ static int launch_rows(const FpnLevels &fa, int C, const float *rois, const int 
     int rows = kTileBudget / row_bytes;
     if (rows < 1) rows = 1;
     if (rows > P || out_nhwc) rows = P;
-    if (!out_nhwc && (int64_t)rows * row_bytes > 160 * 1024) return VD_ERR_SHAPE;
+    if (!out_nhwc && (int64_t)rows * row_bytes > VD_LDS_BYTES) return VD_ERR_SHAPE;
     const int chunks = (C + 255) / 256;
     int waves = rows * chunks;
     if (waves > 8) waves = 8;  // __launch_bounds__(512): <= 256 VGPRs, acc[P] stays in registers
@@ -632,7 +632,7 @@ static int launch_sep_buf(const FpnLevels &fa, int C, const float *rois, const i
 static int launch_sep(const FpnLevels &fa, int C, const float *rois, const int *lvl,
                       const int *order, int R, int P, int out_nhwc, float *out, hipStream_t s) {
     const size_t lds = out_nhwc ? 0 : (size_t)C * P * P * 4;
-    if (lds > 160 * 1024) return VD_ERR_SHAPE;
+    if (lds > VD_LDS_BYTES) return VD_ERR_SHAPE;
     int waves = P * ((C + 255) / 256);
     if (waves > 8) waves = 8;
     // non-temporal output stores (297 us vs 306 us write-back on the 8-frame launch)
@@ -663,7 +663,7 @@ int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, con
                            : launch_rows<14, 0>(fa, C, rois, lvl, order, R, sr, out, s, 1);
         return VD_ERR_SHAPE;
     }
-    if (variant >= 8 && sr == 2 && PH == PW && (int64_t)C * PH * PW * 4 <= 160 * 1024)
+    if (variant >= 8 && sr == 2 && PH == PW && (int64_t)C * PH * PW * 4 <= VD_LDS_BYTES)
         return launch_sep(fa, C, rois, lvl, order, R, PH, 0, out, s);
     if (PH == PW && (PH == 7 || PH == 14)) {
         const bool unrolled = sr == 2 && variant >= 2;

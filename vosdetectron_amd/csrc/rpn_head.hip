@@ -174,7 +174,7 @@ int launch_rpn_head(const float *x, const float *conv_bias, const float *w, cons
     if (npix == 0) return VD_OK;
     if (C % 64 != 0 || A < 1 || 5 * A > 16) return VD_ERR_SHAPE;  // swizzle: 16 | C/4
     const size_t lds = ((size_t)kRpnTile * C + (size_t)C * 16) * 4;
-    if (lds > 160 * 1024) return VD_ERR_SHAPE;
+    if (lds > VD_LDS_BYTES) return VD_ERR_SHAPE;
     const char *e = getenv("VOSDET_RPN_HEAD_MFMA");
     if (C == 256 && !(e && e[0] == '0')) {
         const int64_t waves = (npix + 15) / 16;

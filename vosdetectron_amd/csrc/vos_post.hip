@@ -203,7 +203,9 @@ __device__ __forceinline__ float iou_vos(const float *a, const float *b) {
 
 // One workgroup per frame: filter the frame's detections against the previous
 // frame's result, stable compaction in place.  A class with more than one
-// previous box (the reference asserts < 2) fails the frame: count -1.
+// previous box (the reference asserts len(prev_cls_boxes[j]) < 2 for EVERY
+// class j, vos_test.py:846-848, whether or not the current frame has one) fails
+// the frame with its own code: count VD_COUNT_PREV_BOXES (-2).
 __global__ __launch_bounds__(1024) void prev_box_filter_kernel(
     float *__restrict__ dets, int32_t *__restrict__ classes, int32_t *__restrict__ counts,
     int det_cap, const float *__restrict__ prev_dets, const int32_t *__restrict__ prev_classes,
@@ -230,11 +232,13 @@ __global__ __launch_bounds__(1024) void prev_box_filter_kernel(
                 ++nprev;
                 found = k;
             }
-        if (nprev > 1) atomicOr(&bad, 1);
         keep = 1;
         if (nprev == 1 && !(pd[found * 5 + 4] < score_thresh))
             keep = !(iou_vos(pd + found * 5, row) < iou_thresh);
     }
+    for (int u = t; u < np_; u += blockDim.x)  // every previous class, present here or not
+        for (int k = 0; k < u; ++k)
+            if (pc[k] == pc[u]) atomicOr(&bad, 1);
     pref[t] = keep;
     __syncthreads();
     for (int s = 1; s < (int)blockDim.x; s <<= 1) {  // inclusive scan
@@ -249,7 +253,7 @@ __global__ __launch_bounds__(1024) void prev_box_filter_kernel(
         c[o] = cls;
     }
     __syncthreads();
-    if (t == 0) counts[f] = bad ? -1 : (n ? pref[n - 1] : 0);
+    if (t == 0) counts[f] = bad ? VD_COUNT_PREV_BOXES : (n ? pref[n - 1] : 0);
 }
 
 }  // namespace

@@ -47,7 +47,9 @@ class StageTimer:
 
 def nms_options(cfg) -> dict:
     """TEST.SOFT_NMS / TEST.BBOX_VOTE (lib/core/test.py:756-776) as box_detections
-    keywords (empty when both are off: the stock vd_box_detections)."""
+    keywords (empty when both are off: the stock vd_box_detections).  The
+    reference never passes TEST.BBOX_VOTE.SCORING_METHOD_BETA to box_voting
+    (test.py:770-775, vos_test.py:786-791), so beta stays 1.0 here too."""
     tst = cfg.TEST
     opts = {}
     if tst.SOFT_NMS.ENABLED:
@@ -55,7 +57,7 @@ def nms_options(cfg) -> dict:
     if tst.BBOX_VOTE.ENABLED:
         opts.update(bbox_vote=tst.BBOX_VOTE.SCORING_METHOD,
                     bbox_vote_thresh=tst.BBOX_VOTE.VOTE_TH,
-                    bbox_vote_beta=tst.BBOX_VOTE.SCORING_METHOD_BETA)
+                    bbox_vote_beta=1.0)
     return opts
 
 
@@ -294,6 +296,9 @@ def frame_segms(pipe: FramePipeline, out: dict, num_classes: int = 81):
     (vosdetectron_amd/segm.py), then the per-frame class grouping.  Returns a
     list over frames of cls_segms."""
     from . import segm
+    if isinstance(pipe, VOSPipeline) and pipe.heuristics_on():
+        raise ValueError("frame_segms skips TEST.NMS_WITH_MASK_IOU / NMS_SMALL_BOX_IOU: use "
+                         "VOSPipeline.frame_results for this config")
     ks = [int(k) for k in out["counts_host"]]
     total = sum(ks)
     if total == 0:
@@ -328,6 +333,16 @@ class VOSPipeline(FramePipeline):
         self.prev_dets = torch.zeros((F, det_cap, 5), dtype=torch.float32, device=self.device)
         self.prev_classes = torch.zeros((F, det_cap), dtype=torch.int32, device=self.device)
         self.prev_counts = torch.zeros((F,), dtype=torch.int32, device=self.device)
+        # a step whose result frame_results has not yet recorded as the previous
+        # frame (only tracked while a heuristic reads the previous result)
+        self._unfinalized = False
+
+    def heuristics_on(self) -> bool:
+        """TEST.NMS_WITH_MASK_IOU / NMS_SMALL_BOX_IOU (vos_test.py:113-118, 845-860):
+        both need frame_results, the step's mask-IoU NMS and the previous frame's
+        final result."""
+        tst = self.cfg.TEST
+        return float(tst.NMS_WITH_MASK_IOU) > 0 or float(tst.NMS_SMALL_BOX_IOU) > 0
 
     def reset(self, rows=None):
         """Zero the hidden states (and forget the previous-frame results) of batch
@@ -368,6 +383,7 @@ class VOSPipeline(FramePipeline):
         K = num_classes or int(self.cfg.MODEL.NUM_CLASSES)
         tst = self.cfg.TEST
         self.complete(out)
+        self._unfinalized = False
         ks = [int(k) for k in out["counts_host"]]
         thr = self.cfg.MRCNN.THRESH_BINARIZE
         res, start = [], 0
@@ -408,9 +424,19 @@ class VOSPipeline(FramePipeline):
             sync: bool = True):
         """frames: F x H x W x 3 u8 (frame t of each sequence); flow: optional
         F x 2 x Hp x Wp optical flow at blob resolution (flo_to_blob, data_flow);
-        sync as FramePipeline.run (False: complete() reads the counts later)."""
+        sync as FramePipeline.run (False: complete() reads the counts later).
+        With TEST.NMS_WITH_MASK_IOU / NMS_SMALL_BOX_IOU on, every step's result
+        must pass through frame_results before the next step runs (the filter
+        reads the previous frame's final result): raises otherwise."""
+        if self._unfinalized and self.heuristics_on():
+            raise RuntimeError(
+                "VOSPipeline.run: the previous step's result has not been through "
+                "frame_results(); TEST.NMS_WITH_MASK_IOU / NMS_SMALL_BOX_IOU need it as the "
+                "next frame's previous result (lib_vos/tools/vos_test.py:113-118, 845-860)")
         self._flow = flow
         try:
-            return super().run(frames, keep_intermediates, sync=sync)
+            out = super().run(frames, keep_intermediates, sync=sync)
         finally:
             self._flow = None
+        self._unfinalized = True
+        return out

@@ -788,11 +788,20 @@ def generate_proposals(cls_probs: Sequence[torch.Tensor], bbox_preds: Sequence[t
     return rois, probs, counts
 
 
+COUNT_SELECT_FAILED, COUNT_PREV_BOXES = -1, -2  # include/vosdet.h VD_COUNT_*
+
+
 def raise_on_failed_counts(counts, what: str = "frame"):
     """-1 in a per-image count means a device kernel could not complete that
     image (generate_proposals' top-k threshold search could not bracket
     pre_nms_topN within its candidate capacity; collect_distribute and
     box_detections pass the -1 on).  Raise instead of dropping proposals."""
+    prev = [i for i, c in enumerate(counts) if c == COUNT_PREV_BOXES]
+    if prev:
+        raise _lib.VosdetError(
+            "TEST.NMS_SMALL_BOX_IOU: the previous result of %s(s) %s holds more than one box "
+            "of a class (lib_vos/tools/vos_test.py:848 asserts < 2; set "
+            "TEST.NUM_DET_PER_CLASS_POST = 1 or TEST.NMS_WITH_MASK_IOU)" % (what, prev))
     bad = [i for i, c in enumerate(counts) if c < 0]
     if bad:
         raise _lib.VosdetError(
