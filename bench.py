@@ -1094,6 +1094,9 @@ def main():
     roof = None
     if not args.no_roofline and rank == 0:
         roof = measure_roialign_roofline(dev)
+        if "X-101" in args.config:
+            # SURVEY 8(d) config 5 stress: R = 1000 RoIs at P = 14 (282.1 MB per frame)
+            roof["stress_launch"] = measure_roialign_roofline(dev, P=14)
         if not vos and cfg.FPN.FPN_ON:
             roof["engine_launch"] = measure_pipeline_roialign(pipe, any_frames)
             extra["nms"] = measure_nms(dev)
