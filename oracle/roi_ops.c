@@ -13,13 +13,18 @@
  * contraction; the reference Cython NMS is built without FMA on x86-64, and the
  * CUDA kernels' own nvcc build would contract -- see DESIGN.md "Parity").
  *
- * Pinning status:
- *   - The reference CUDA kernels cannot be built in this image (they need the
- *     CUDA runtime headers/THC), and the Cython NMS does not compile unmodified
- *     against numpy 2, so these restatements are pinned by analytic known
- *     answers (bilinear exactness on affine ramps, hand-derived NMS cases, the
- *     survey-observed tie order) rather than by executing the reference.
- *     -> "parity unpinned" against an executed reference for these functions.
+ * Pinning status (see DESIGN.md §2 Parity):
+ *   - RoI operators (RoIAlign, RoIPool, RoICrop, jwyang RoIAlign, FlowAlign):
+ *     the reference CUDA kernels cannot be built in this image (they need the
+ *     CUDA runtime headers / THC) and the reference holds no vectors for them,
+ *     so these restatements are pinned by analytic known answers only
+ *     (bilinear exactness on affine ramps, tests/test_oracle_kat.py)
+ *     -> "parity unpinned" against an executed reference.
+ *   - Greedy NMS: PINNED since round 3 -- tools/ref_cython_nms.py compiles the
+ *     reference's own cython_nms.pyx (a scratch copy under /tmp, the only change
+ *     being numpy 2's dtype spelling) and tests/golden/nms.npz holds its
+ *     outputs (27 sets up to 5000 boxes), which this restatement reproduces
+ *     bit for bit (tests/test_oracle_golden.py).
  */
 #include <float.h>
 #include <math.h>

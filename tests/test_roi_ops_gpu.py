@@ -158,7 +158,7 @@ def test_roi_pool_backward_matches_scatter():
     assert np.array_equal(ft.grad.cpu().numpy().ravel(), ref)
 
 
-@pytest.mark.parametrize("variant", [None, "3"])
+@pytest.mark.parametrize("variant", [None, "3", "11"])
 @pytest.mark.parametrize("P,C", [(7, 256), (14, 256), (7, 64), (14, 520)])
 def test_roi_align_fpn_separable_within_tolerance(P, C, variant, monkeypatch):
     """Separable NHWC kernels (variants 8 / 10): same sampling, summation
@@ -219,10 +219,10 @@ def test_roi_align_fpn_schedules_and_edges(P):
         got = ops.roi_align_fpn(pyr, scales, rt, lt, P, 2, roi_order=order,
                                 out_layout="nhwc").cpu().numpy()
         assert np.array_equal(got, ref)
-    # variant 8 (global loads) and candidate kernels (VOSDET_TEST_RA_VARIANTS="..."):
-    # bit-identical to the product kernel (variant 10, buffer loads)
+    # variant 8 (global loads), variant 11 (the pipelined sweep) and candidate kernels
+    # (VOSDET_TEST_RA_VARIANTS="..."): bit-identical to variant 10 (buffer loads)
     import os
-    for variant in ["8"] + os.environ.get("VOSDET_TEST_RA_VARIANTS", "").split():
+    for variant in ["8", "11"] + os.environ.get("VOSDET_TEST_RA_VARIANTS", "").split():
         os.environ["VOSDET_ROIALIGN_VARIANT"] = variant
         try:
             got = ops.roi_align_fpn(pyr, scales, rt, lt, P, 2, out_layout="nhwc").cpu().numpy()

@@ -15,7 +15,7 @@ def run(thr, lv=None):
     idx = range(5) if lv is None else [lv]
     return ops.generate_proposals([probs[i] for i in idx], [deltas[i] for i in idx], [an[i] for i in idx],
                                   [1. / 2 ** (i + 2) for i in idx], info, 1000, 1000, thr, 0)
-for presel, mlds in (("1", "1"), ("0", "1"), ("1", "0")):
+for presel, mlds in (("1", "1"), ("0", "1"), ("1", "0")):  # profiles/r05: lds 1 slower
   os.environ["VOSDET_RPN_PRESEL"] = presel
   os.environ["VOSDET_RPN_MASK_LDS"] = mlds
   print("VOSDET_RPN_PRESEL=%s VOSDET_RPN_MASK_LDS=%s, %d images" % (presel, mlds, N), flush=True)

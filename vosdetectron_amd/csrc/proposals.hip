@@ -98,11 +98,14 @@ static bool rpn_presel() {
     const char *e = getenv("VOSDET_RPN_PRESEL");
     return !(e && e[0] == '0');
 }
-// Mask build of the split NMS: the LDS-staged row-block kernel (default) or the
-// one-wave-per-row kernel (VOSDET_RPN_MASK_LDS=0)
+// Mask build of the split NMS: the one-wave-per-row kernel (default) or the
+// LDS-staged row-block kernel (VOSDET_RPN_MASK_LDS=1), which measured slower:
+// 174 vs 132 us for P2-P6 x 32 images (profiles/r05/proposals_breakdown.txt) --
+// the build is VALU-bound on the IoU tests, and the LDS form's 4 waves per 64-row
+// block leave the long first blocks on few SIMDs
 static bool rpn_mask_lds() {
     const char *e = getenv("VOSDET_RPN_MASK_LDS");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }
 static int rpn_sel_cap(int max_pre, bool large) {
     const int sel_cap = large ? kSelCapL : kSelCap;
@@ -717,8 +720,8 @@ __global__ __launch_bounds__(1024) void rpn_nms_mask_kernel(char *__restrict__ w
 // slot) with the slot's boxes from the block's first row on staged in LDS, so
 // the IoU tests read LDS instead of one global load per lane and box; each
 // wave builds 16 rows, a row's words stored by the lanes in one coalesced
-// write.  (The one-wave-per-row form above keeps the large variant, whose
-// boxes exceed the LDS budget.)
+// write.  Opt-in (VOSDET_RPN_MASK_LDS=1): measured 1.3x slower than the
+// one-wave-per-row form above, which stays the default.
 static constexpr int kMaskLdsMaxBoxes = 3200;  // 5 x 4 B x 3200 = 62.5 KiB
 
 __global__ __launch_bounds__(256) void rpn_nms_mask_lds_kernel(char *__restrict__ ws,

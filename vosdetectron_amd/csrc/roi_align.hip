@@ -429,6 +429,210 @@ __global__ __launch_bounds__(1024) void roi_align_fpn_nhwc_sep_buf_kernel(
     }
 }
 
+// Pipelined separable sweep (variant 11, round 5): variant 10's sweep bin for bin
+// (bit-identical: the same V(x), the same per-bin sums in the same order), with
+// the row's distinct columns listed up front so that column k + 2's tap loads
+// are issued before column k is combined.  Variant 10 loads a column only when
+// the sweep reaches it, each tap behind a wave-uniform branch, and drains
+// (vmcnt 0) before combining it: <= 4 KiB in flight per wave, ~2.5 on average
+// (2-3 distinct tap rows per output row), about half of what an HBM miss needs
+// at 28 resident waves per CU (profiles/r05/roialign/README.md).  Here every
+// column issues exactly NR (= the row's distinct tap rows, 2..4) loads -- a
+// padding tap reads pixel (0, 0) and is skipped by the combine -- so the loop is
+// branch-free and two columns' loads stay outstanding while one is combined.
+//   Column list: lane 2 j + h holds sample j's column xl (h = 0) / xh (h = 1);
+//   the valid samples' columns are non-decreasing, so the distinct ones are the
+//   lanes that differ from the previous valid lane (ballot + prefix count), and
+//   sample j is finished when column index(xh_j) is combined (xl_j is the
+//   column before it, or the same one when clamped at the right edge).
+typedef int ra_v4i __attribute__((ext_vector_type(4)));
+typedef float ra_f4 __attribute__((ext_vector_type(4)));
+
+// One 16-B tap load per lane against the RoI image's buffer descriptor (SGPR quad):
+// vector offset = the lane's channel bytes, scalar offset = the tap's row + column.
+// Inline asm so the compiler neither waits on it nor reuses its destination
+// early; the caller counts vmcnt (ra_wait).
+__device__ __forceinline__ void ra_load(ra_f4 &r, ra_v4i desc, int voff, int soff) {
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(r) : "v"(voff), "s"(desc),
+                 "s"(soff) : "memory");
+}
+// All but the last N vector-memory ops retired; the slot's registers pass through
+// so nothing reads them above the wait.
+template <int N, int NR>
+__device__ __forceinline__ void ra_wait(ra_f4 (&a)[NR]) {
+    if constexpr (NR == 2)
+        asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a[0]), "+v"(a[1]) : "i"(N) : "memory");
+    else if constexpr (NR == 3)
+        asm volatile("s_waitcnt vmcnt(%3)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]) : "i"(N) : "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(%4)"
+                     : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3])
+                     : "i"(N)
+                     : "memory");
+}
+
+template <int NR, bool NT>
+__device__ __forceinline__ void pipe_row(const RoiGeom &g, ra_v4i desc, int voff,
+                                         const int (&roff)[4], const float (&rw)[4], int nr,
+                                         const int *cols, int nc, int ns, int colbytes, int xh_k,
+                                         int xinfo, float lxv, bool active, float *orow, int C) {
+    constexpr int SR = 2;
+    const float inv = 1.f / g.count;
+    // a padding tap (r >= nr, or a column past the list) loads pixel (0, 0) of the
+    // image -- in range, one cached line -- and is left out of the combine
+    auto issue = [&](int k, ra_f4 (&sl)[NR]) {
+        const bool live = k < nc;
+        const int xo = __builtin_amdgcn_readfirstlane(live ? cols[k] * colbytes : 0);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const bool real = live && r < nr;
+            ra_load(sl[r], desc, voff, __builtin_amdgcn_readfirstlane(real ? roff[r] + xo : 0));
+        }
+    };
+    ra_f4 s0[NR], s1[NR], s2[NR];
+    issue(0, s0);
+    issue(1, s1);
+    float4 vprev = make_float4(0.f, 0.f, 0.f, 0.f), vcur = vprev, acc = vprev;
+    int s = 0;  // the next sample to finish
+    auto finish = [&](int k) {  // every sample whose xh column is k (or invalid) in order
+        while (s < ns) {
+            const int fin = __builtin_amdgcn_readlane(xh_k, 2 * s + 1);
+            const int info = __builtin_amdgcn_readlane(xinfo, 2 * s + 1);  // 1 valid, 2 xl == xh
+            if ((info & 1) && fin > k) break;
+            if (info & 1) {
+                const float lx = __builtin_bit_cast(
+                    float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lxv), 2 * s + 1));
+                const float hx = 1.f - lx;
+                const float4 va = (info & 2) ? vcur : vprev;
+                acc.x += hx * va.x + lx * vcur.x;
+                acc.y += hx * va.y + lx * vcur.y;
+                acc.z += hx * va.z + lx * vcur.z;
+                acc.w += hx * va.w + lx * vcur.w;
+            }
+            if (s % SR == SR - 1) {
+                if (active)
+                    store_bin<NT>(orow + (int64_t)(s / SR) * C,
+                                  make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
+                acc = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            ++s;
+        }
+    };
+    // column k's loads were issued two columns ago; after them came column k + 1's
+    // and k + 2's (NR each) and the bin stores of one finish: vmcnt(2 NR) retires
+    // them (and at most those stores' worth of k + 1's loads early)
+    auto consume = [&](int k, ra_f4 (&sl)[NR]) {
+        ra_wait<2 * NR>(sl);
+        vprev = vcur;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {  // combine_column's sum, tap order
+            if (r < nr) {                // wave-uniform: padding taps are skipped
+                v.x += rw[r] * sl[r][0];
+                v.y += rw[r] * sl[r][1];
+                v.z += rw[r] * sl[r][2];
+                v.w += rw[r] * sl[r][3];
+            }
+        }
+        vcur = v;
+        finish(k);
+    };
+    for (int k = 0; k < nc; k += 3) {
+        issue(k + 2, s2);
+        consume(k, s0);
+        if (k + 1 >= nc) break;
+        issue(k + 3, s0);
+        consume(k + 1, s1);
+        if (k + 2 >= nc) break;
+        issue(k + 4, s1);
+        consume(k + 2, s2);
+    }
+    finish(0x7fffffff);  // samples past the last column: all invalid; their bins store 0
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the row's slots
+}
+
+template <bool NT>
+__global__ __launch_bounds__(1024) void roi_align_fpn_nhwc_sep_pipe_kernel(
+    FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
+    const int *__restrict__ roi_order, int P, float *__restrict__ out) {
+    constexpr int SR = 2;
+    __shared__ int s_cols[16][64];
+    const int b = blockIdx.x;
+    if (b >= fa.R) return;
+    const int r = roi_order ? roi_order[b] : b;
+    if (r < 0 || r >= fa.R) return;  // malformed schedule entry: write nothing
+    int li = roi_level ? roi_level[r] : 0;
+    li = __builtin_amdgcn_readfirstlane(li);
+    const RoiGeom g = roi_geom(fa, C, rois + (int64_t)r * 5, li, P, P, SR);
+    const int lane = lane_id(), wave = wave_id();
+    // raw buffer descriptor (stride 0, range = the RoI's image), as
+    // __builtin_amdgcn_make_buffer_rsrc builds it for variant 10
+    const uint64_t fb = (uint64_t)(uintptr_t)g.feat;
+    ra_v4i desc;
+    desc.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)fb);
+    desc.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(fb >> 32) & 0xffff);
+    desc.z = __builtin_amdgcn_readfirstlane(g.H * g.W * C * 4);
+    desc.w = 0x00020000;
+    const int rowbytes = g.W * C * 4, colbytes = C * 4;
+    const int c0 = lane * 4;
+    const bool active = c0 < C;
+    const int voff = (active ? c0 : 0) * 4;
+    const int ns = P * SR;  // samples per row (<= 32: two column candidates per lane pair)
+    // the row's x geometry does not depend on the row: sample j = lane >> 1
+    const int j = lane >> 1;
+    int xl = 0, xh = 0;
+    float lx = 0.f;
+    bool valid = false;
+    if (j < ns) {
+        const int pw = j / SR, ix = j % SR;
+        float x = g.sw + pw * g.bw + (ix + .5f) * g.bw / SR;
+        valid = !(x < -1.0f || x > (float)g.W);
+        if (x <= 0) x = 0;
+        xl = (int)x;
+        if (xl >= g.W - 1) { xh = xl = g.W - 1; x = (float)xl; } else xh = xl + 1;
+        lx = x - xl;
+    }
+    const int cand = (lane & 1) ? xh : xl;
+    const uint64_t lm = ballot(valid);
+    const uint64_t below = lm & ((1ull << lane) - 1ull);
+    const int pl = below ? 63 - __clzll((long long)below) : 0;
+    const int pc = __shfl(cand, pl);
+    const bool distinct = valid && (below == 0ull || cand != pc);
+    const uint64_t dm = ballot(distinct);
+    const int rank = __popcll(dm & ((1ull << lane) - 1ull));
+    const int nc = __popcll(dm);
+    const int xh_k = distinct ? rank : rank - 1;  // this lane's column index in the list
+    const int xinfo = (valid ? 1 : 0) | (xl == xh ? 2 : 0);
+    if (distinct) s_cols[wave][rank] = cand;
+    __builtin_amdgcn_wave_barrier();
+    for (int ph = wave; ph < P; ph += num_waves()) {
+        const RowTaps<SR> taps = row_taps<SR>(g, ph);
+        int roff[4] = {0, 0, 0, 0}, nr = 0;
+        float rw[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 2 * SR; ++k)
+            if (taps.alive[k]) {  // wave-uniform; the alive taps in tap order
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (q == nr) {
+                        roff[q] = __builtin_amdgcn_readfirstlane(taps.row[k] * rowbytes);
+                        rw[q] = taps.w[k];
+                    }
+                ++nr;
+            }
+        float *orow = out + (((int64_t)r * P + ph) * P) * C + c0;
+        if (nr <= 2)
+            pipe_row<2, NT>(g, desc, voff, roff, rw, nr, s_cols[wave], nc, ns, colbytes, xh_k,
+                            xinfo, lx, active, orow, C);
+        else if (nr == 3)
+            pipe_row<3, NT>(g, desc, voff, roff, rw, nr, s_cols[wave], nc, ns, colbytes, xh_k,
+                            xinfo, lx, active, orow, C);
+        else
+            pipe_row<4, NT>(g, desc, voff, roff, rw, nr, s_cols[wave], nc, ns, colbytes, xh_k,
+                            xinfo, lx, active, orow, C);
+    }
+}
+
 template <int P, int SR, int D>
 __global__ __launch_bounds__(512) void roi_align_fpn_nhwc_kernel(
     FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
@@ -629,6 +833,17 @@ static int launch_sep_buf(const FpnLevels &fa, int C, const float *rois, const i
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
+static int launch_sep_pipe(const FpnLevels &fa, int C, const float *rois, const int *lvl,
+                           const int *order, int R, int P, float *out, hipStream_t s) {
+    if (C > 256 || P > 16) return VD_ERR_SHAPE;
+    for (int l = 0; l < fa.L; ++l)  // 32-bit buffer offsets: every image of a level < 2 GiB
+        if ((int64_t)fa.H[l] * fa.W[l] * C * 4 >= (1ll << 31)) return VD_ERR_SHAPE;
+    const int waves = P < 8 ? P : 8;
+    hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_pipe_kernel<true>), dim3(R), dim3(64 * waves), 0,
+                       s, fa, C, rois, lvl, order, P, out);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
 static int launch_sep(const FpnLevels &fa, int C, const float *rois, const int *lvl,
                       const int *order, int R, int P, int out_nhwc, float *out, hipStream_t s) {
     const size_t lds = out_nhwc ? 0 : (size_t)C * P * P * 4;
@@ -649,7 +864,11 @@ int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, con
     if (C % 4 != 0) return VD_ERR_SHAPE;
     const int variant = roialign_variant();
     if (out_nhwc) {  // product path: [R][P][P][C] written straight from registers
-        if (variant == 10 && sr == 2 && PH == PW) {  // register gathers
+        if (variant == 11 && sr == 2 && PH == PW) {  // pipelined register gathers
+            const int st = launch_sep_pipe(fa, C, rois, lvl, order, R, PH, out, s);
+            if (st != VD_ERR_SHAPE) return st;
+        }
+        if (variant >= 10 && sr == 2 && PH == PW) {  // register gathers
             const int st = launch_sep_buf(fa, C, rois, lvl, order, R, PH, out, s);
             if (st != VD_ERR_SHAPE) return st;
         }
