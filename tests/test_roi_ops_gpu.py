@@ -219,10 +219,10 @@ def test_roi_align_fpn_schedules_and_edges(P):
         got = ops.roi_align_fpn(pyr, scales, rt, lt, P, 2, roi_order=order,
                                 out_layout="nhwc").cpu().numpy()
         assert np.array_equal(got, ref)
-    # variant 8 (global loads), variant 11 (the pipelined sweep) and candidate kernels
+    # variant 8 (global loads), variants 11 / 13 (the pipelined sweep) and candidate kernels
     # (VOSDET_TEST_RA_VARIANTS="..."): bit-identical to variant 10 (buffer loads)
     import os
-    for variant in ["8", "11"] + os.environ.get("VOSDET_TEST_RA_VARIANTS", "").split():
+    for variant in ["8", "11", "13"] + os.environ.get("VOSDET_TEST_RA_VARIANTS", "").split():
         os.environ["VOSDET_ROIALIGN_VARIANT"] = variant
         try:
             got = ops.roi_align_fpn(pyr, scales, rt, lt, P, 2, out_layout="nhwc").cpu().numpy()

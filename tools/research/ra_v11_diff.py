@@ -1,4 +1,4 @@
-"""Where variant 11 (pipelined sweep) differs from variant 10 on the schedule test's
+"""Where variants 11 / 13 (pipelined sweep) differ from variant 10 on the schedule test's
 frames: mismatch counts by (P, row ph, bin pw, lane, component) and a few RoIs."""
 import os
 import sys
@@ -19,10 +19,11 @@ rois = np.concatenate([synthetic_rois(f, 500, batch_idx=f) for f in range(F)])
 lv = fpn_levels_np(rois) - 2
 rt, lt = torch.from_numpy(rois).to(DEV), torch.from_numpy(lv).to(DEV)
 scales = [1. / 4, 1. / 8, 1. / 16, 1. / 32]
-for P in (7, 14):
+for P, v in ((7, "11"), (7, "13"), (14, "11"), (14, "13")):
+    print("variant", v)
     os.environ["VOSDET_ROIALIGN_VARIANT"] = "10"
     a = ops.roi_align_fpn(pyr, scales, rt, lt, P, 2, out_layout="nhwc").cpu().numpy()
-    os.environ["VOSDET_ROIALIGN_VARIANT"] = "11"
+    os.environ["VOSDET_ROIALIGN_VARIANT"] = v
     b = ops.roi_align_fpn(pyr, scales, rt, lt, P, 2, out_layout="nhwc").cpu().numpy()
     bad = a != b
     print("P", P, "mismatch", bad.sum(), "of", bad.size, flush=True)

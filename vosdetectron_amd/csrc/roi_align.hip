@@ -441,20 +441,30 @@ __global__ __launch_bounds__(1024) void roi_align_fpn_nhwc_sep_buf_kernel(
 // padding tap reads pixel (0, 0) and is skipped by the combine -- so the loop is
 // branch-free and two columns' loads stay outstanding while one is combined.
 //   Column list: lane 2 j + h holds sample j's column xl (h = 0) / xh (h = 1);
-//   the valid samples' columns are non-decreasing, so the distinct ones are the
-//   lanes that differ from the previous valid lane (ballot + prefix count), and
-//   sample j is finished when column index(xh_j) is combined (xl_j is the
-//   column before it, or the same one when clamped at the right edge).
+//   a valid lane's column is new iff it exceeds every earlier valid lane's
+//   (prefix max; ballot + prefix count give its index), the list is strictly
+//   increasing, and sample j is finished when column index(xh_j) is combined
+//   (xl_j = xh_j - 1 is the entry before it, or xh_j itself when clamped at the
+//   right edge).
 typedef int ra_v4i __attribute__((ext_vector_type(4)));
 typedef float ra_f4 __attribute__((ext_vector_type(4)));
 
 // One 16-B tap load per lane against the RoI image's buffer descriptor (SGPR quad):
 // vector offset = the lane's channel bytes, scalar offset = the tap's row + column.
 // Inline asm so the compiler neither waits on it nor reuses its destination
-// early; the caller counts vmcnt (ra_wait).
+// early; the tied operand keeps the slot in one register across the loop (an
+// untied output let the register allocator copy a loop-carried slot at the back
+// edge -- a read of the register before the load landed).  The caller counts
+// vmcnt (ra_wait).
+// The scalar offset usually comes straight from v_readfirstlane (a VALU write of
+// an SGPR), which a VMEM instruction may read only 5 wait states later; the
+// compiler's hazard recognizer does not look inside the asm, so the asm pads
+// them itself (without it the load read the previous column's offset).
 __device__ __forceinline__ void ra_load(ra_f4 &r, ra_v4i desc, int voff, int soff) {
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(r) : "v"(voff), "s"(desc),
-                 "s"(soff) : "memory");
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, %3 offen"
+                 : "+v"(r)
+                 : "v"(voff), "s"(desc), "s"(soff)
+                 : "memory");
 }
 // All but the last N vector-memory ops retired; the slot's registers pass through
 // so nothing reads them above the wait.
@@ -471,7 +481,7 @@ __device__ __forceinline__ void ra_wait(ra_f4 (&a)[NR]) {
                      : "memory");
 }
 
-template <int NR, bool NT>
+template <int NR, bool NT, int D>
 __device__ __forceinline__ void pipe_row(const RoiGeom &g, ra_v4i desc, int voff,
                                          const int (&roff)[4], const float (&rw)[4], int nr,
                                          const int *cols, int nc, int ns, int colbytes, int xh_k,
@@ -490,8 +500,10 @@ __device__ __forceinline__ void pipe_row(const RoiGeom &g, ra_v4i desc, int voff
         }
     };
     ra_f4 s0[NR], s1[NR], s2[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) s0[r] = s1[r] = s2[r] = ra_f4{0.f, 0.f, 0.f, 0.f};
     issue(0, s0);
-    issue(1, s1);
+    if (D == 2) issue(1, s1);
     float4 vprev = make_float4(0.f, 0.f, 0.f, 0.f), vcur = vprev, acc = vprev;
     int s = 0;  // the next sample to finish
     auto finish = [&](int k) {  // every sample whose xh column is k (or invalid) in order
@@ -522,7 +534,7 @@ __device__ __forceinline__ void pipe_row(const RoiGeom &g, ra_v4i desc, int voff
     // and k + 2's (NR each) and the bin stores of one finish: vmcnt(2 NR) retires
     // them (and at most those stores' worth of k + 1's loads early)
     auto consume = [&](int k, ra_f4 (&sl)[NR]) {
-        ra_wait<2 * NR>(sl);
+        ra_wait<D * NR>(sl);
         vprev = vcur;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -537,21 +549,31 @@ __device__ __forceinline__ void pipe_row(const RoiGeom &g, ra_v4i desc, int voff
         vcur = v;
         finish(k);
     };
-    for (int k = 0; k < nc; k += 3) {
-        issue(k + 2, s2);
-        consume(k, s0);
-        if (k + 1 >= nc) break;
-        issue(k + 3, s0);
-        consume(k + 1, s1);
-        if (k + 2 >= nc) break;
-        issue(k + 4, s1);
-        consume(k + 2, s2);
+    if constexpr (D == 2) {
+        for (int k = 0; k < nc; k += 3) {
+            issue(k + 2, s2);
+            consume(k, s0);
+            if (k + 1 >= nc) break;
+            issue(k + 3, s0);
+            consume(k + 1, s1);
+            if (k + 2 >= nc) break;
+            issue(k + 4, s1);
+            consume(k + 2, s2);
+        }
+    } else {  // one column ahead (fewer VGPRs, more resident waves)
+        for (int k = 0; k < nc; k += 2) {
+            issue(k + 1, s1);
+            consume(k, s0);
+            if (k + 1 >= nc) break;
+            issue(k + 2, s0);
+            consume(k + 1, s1);
+        }
     }
     finish(0x7fffffff);  // samples past the last column: all invalid; their bins store 0
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the row's slots
 }
 
-template <bool NT>
+template <bool NT, int D>
 __global__ __launch_bounds__(1024) void roi_align_fpn_nhwc_sep_pipe_kernel(
     FpnLevels fa, int C, const float *__restrict__ rois, const int *__restrict__ roi_level,
     const int *__restrict__ roi_order, int P, float *__restrict__ out) {
@@ -592,12 +614,19 @@ __global__ __launch_bounds__(1024) void roi_align_fpn_nhwc_sep_pipe_kernel(
         if (xl >= g.W - 1) { xh = xl = g.W - 1; x = (float)xl; } else xh = xl + 1;
         lx = x - xl;
     }
+    // the lanes' columns are NOT monotone (xl_1 < xh_0 when two samples share a
+    // pixel pair), but each valid lane's column is a new one iff it exceeds every
+    // earlier valid lane's: an exclusive prefix max over the wave
     const int cand = (lane & 1) ? xh : xl;
-    const uint64_t lm = ballot(valid);
-    const uint64_t below = lm & ((1ull << lane) - 1ull);
-    const int pl = below ? 63 - __clzll((long long)below) : 0;
-    const int pc = __shfl(cand, pl);
-    const bool distinct = valid && (below == 0ull || cand != pc);
+    int incl = valid ? cand : -1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl = incl > v ? incl : v;
+    }
+    int excl = __shfl_up(incl, 1);
+    if (lane == 0) excl = -1;
+    const bool distinct = valid && cand > excl;
     const uint64_t dm = ballot(distinct);
     const int rank = __popcll(dm & ((1ull << lane) - 1ull));
     const int nc = __popcll(dm);
@@ -622,14 +651,14 @@ __global__ __launch_bounds__(1024) void roi_align_fpn_nhwc_sep_pipe_kernel(
             }
         float *orow = out + (((int64_t)r * P + ph) * P) * C + c0;
         if (nr <= 2)
-            pipe_row<2, NT>(g, desc, voff, roff, rw, nr, s_cols[wave], nc, ns, colbytes, xh_k,
-                            xinfo, lx, active, orow, C);
+            pipe_row<2, NT, D>(g, desc, voff, roff, rw, nr, s_cols[wave], nc, ns, colbytes, xh_k,
+                                xinfo, lx, active, orow, C);
         else if (nr == 3)
-            pipe_row<3, NT>(g, desc, voff, roff, rw, nr, s_cols[wave], nc, ns, colbytes, xh_k,
-                            xinfo, lx, active, orow, C);
+            pipe_row<3, NT, D>(g, desc, voff, roff, rw, nr, s_cols[wave], nc, ns, colbytes, xh_k,
+                                xinfo, lx, active, orow, C);
         else
-            pipe_row<4, NT>(g, desc, voff, roff, rw, nr, s_cols[wave], nc, ns, colbytes, xh_k,
-                            xinfo, lx, active, orow, C);
+            pipe_row<4, NT, D>(g, desc, voff, roff, rw, nr, s_cols[wave], nc, ns, colbytes, xh_k,
+                                xinfo, lx, active, orow, C);
     }
 }
 
@@ -797,6 +826,8 @@ static int roialign_variant() {  // read per launch so tests can switch kernels
     // 10: separable kernel with buffer loads (product default, NHWC out; RoIAlign
     //    tolerance 1e-4 vs the reference's per-sample order); 8: the same sweep
     //    with global loads (bit-identical to 10; also the NCHW-out path);
+    //    11 / 13: variant 10's sweep pipelined two / one column(s) ahead (bit-
+    //    identical to 10, 8-9 % slower at half the occupancy: profiles/r05/roialign/);
     //    3: bit-exact row kernel (the reference's per-sample arithmetic order).  Round-2 alternatives (XCD channel slices,
     //    tile-binned LDS windows, a pipelined column ring) are in tools/research/
     //    with their measurements (profiles/r02_roialign/README.md).
@@ -834,13 +865,18 @@ static int launch_sep_buf(const FpnLevels &fa, int C, const float *rois, const i
 }
 
 static int launch_sep_pipe(const FpnLevels &fa, int C, const float *rois, const int *lvl,
-                           const int *order, int R, int P, float *out, hipStream_t s) {
+                           const int *order, int R, int P, float *out, hipStream_t s,
+                           bool depth1) {
     if (C > 256 || P > 16) return VD_ERR_SHAPE;
     for (int l = 0; l < fa.L; ++l)  // 32-bit buffer offsets: every image of a level < 2 GiB
         if ((int64_t)fa.H[l] * fa.W[l] * C * 4 >= (1ll << 31)) return VD_ERR_SHAPE;
     const int waves = P < 8 ? P : 8;
-    hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_pipe_kernel<true>), dim3(R), dim3(64 * waves), 0,
-                       s, fa, C, rois, lvl, order, P, out);
+    if (depth1)
+        hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_pipe_kernel<true, 1>), dim3(R),
+                           dim3(64 * waves), 0, s, fa, C, rois, lvl, order, P, out);
+    else
+        hipLaunchKernelGGL((roi_align_fpn_nhwc_sep_pipe_kernel<true, 2>), dim3(R),
+                           dim3(64 * waves), 0, s, fa, C, rois, lvl, order, P, out);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
@@ -864,8 +900,8 @@ int launch_roi_align_fpn_nhwc(const FpnLevels &fa, int C, const float *rois, con
     if (C % 4 != 0) return VD_ERR_SHAPE;
     const int variant = roialign_variant();
     if (out_nhwc) {  // product path: [R][P][P][C] written straight from registers
-        if (variant == 11 && sr == 2 && PH == PW) {  // pipelined register gathers
-            const int st = launch_sep_pipe(fa, C, rois, lvl, order, R, PH, out, s);
+        if ((variant == 11 || variant == 13) && sr == 2 && PH == PW) {  // pipelined gathers
+            const int st = launch_sep_pipe(fa, C, rois, lvl, order, R, PH, out, s, variant == 13);
             if (st != VD_ERR_SHAPE) return st;
         }
         if (variant >= 10 && sr == 2 && PH == PW) {  // register gathers
