@@ -184,6 +184,15 @@ int vd_conv3x3_wino_weight(const float *w, int Cout, int Cin, float *U, void *st
 int vd_conv3x3_wino_bias_act(const float *X, int N, int H, int W, int C, const float *U,
                              int Cout, const float *bias, int relu, float *Y, void *stream);
 
+/* The same convolution by Winograd F(4x4, 3x3) (round 5; 4x fewer multiplies than
+ * the direct form, 1.78x fewer than F(2x2); transforms scale by up to 8, so a few
+ * times F(2x2)'s rounding error): U from vd_conv3x3_wino4_weight (36 x Cout x Cin
+ * fp32, opaque fragment order).  Cin % 8 == 0, Cin <= 4096, Cout % 64 == 0
+ * (VD_ERR_SHAPE otherwise).  Replaces the same PyTorch convolutions as above. */
+int vd_conv3x3_wino4_weight(const float *w, int Cout, int Cin, float *U, void *stream);
+int vd_conv3x3_wino4_bias_act(const float *X, int N, int H, int W, int C, const float *U,
+                              int Cout, const float *bias, int relu, float *Y, void *stream);
+
 /* The Winograd convolution of R images of seg_h x W pixels stored back to back
  * (R x seg_h x W x C, i.e. one H = R * seg_h image), each padded by its own zeros:
  * the mask head's RoI maps run as one mosaic, so the 8 x 16-pixel blocks are not

@@ -146,3 +146,31 @@ def test_conv3x3_wino_input_over_4gib():
     del x, got, ref
     torch.cuda.empty_cache()
 
+
+
+@pytest.mark.parametrize("N,C,H,W,Cout", [(2, 64, 9, 13, 128), (1, 256, 14, 14, 256),
+                                          (3, 128, 1, 1, 128), (1, 256, 25, 42, 256),
+                                          (5, 256, 7, 7, 64), (2, 64, 30, 41, 64),
+                                          (1, 8, 5, 3, 64), (1, 256, 17, 70, 192),
+                                          (2, 256, 50, 84, 256), (1, 512, 33, 65, 128)])
+@pytest.mark.parametrize("relu", [False, True])
+def test_conv3x3_wino4_vs_torch(N, C, H, W, Cout, relu):
+    """Winograd F(4x4,3x3) MFMA kernel (csrc/conv3x3_wino4.hip) vs a plain torch fp32
+    conv2d(pad 1) + bias (+ ReLU): partial 4x4 tiles and 16 x 32 blocks, a 1x1
+    image, Cin 8..512, Cout 64..256.  Tolerance 5e-5 of max|y| (the F(4x4)
+    transforms scale by up to 8: ~2-4e-6 measured on these random data)."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(11 * N + C + H + W + Cout)
+    x = torch.randn(N, C, H, W, generator=g).cuda().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** .5).cuda()
+    b = torch.randn(Cout, generator=g).cuda()
+    u = ops.conv3x3_wino4_weight(w)
+    for bias in (b, None):
+        ref = F.conv2d(x, w, bias, padding=1)
+        if relu:
+            ref = F.relu(ref)
+        got = ops.conv3x3_wino4_bias_act(x, u, bias, relu=relu)
+        torch.cuda.synchronize()
+        assert got.is_contiguous(memory_format=torch.channels_last)
+        err = float((got - ref).abs().max())
+        assert err <= 5e-5 * max(1., float(ref.abs().max())), err

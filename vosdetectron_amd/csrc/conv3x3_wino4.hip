@@ -1,0 +1,365 @@
+// 3x3 stride-1 pad-1 convolution on NHWC fp32 by Winograd F(4x4, 3x3) on the MFMA
+// pipes, bias (+ ReLU) epilogue fused (round 5).
+//
+// Same operator as conv3x3_wino.hip's F(2x2, 3x3) kernel (FPN posthoc / RPN conv,
+// lib/modeling/FPN.py:227-258, 376-422; mask head convs, mask_rcnn_heads.py:178-188),
+// with every 4x4 output tile computed as
+//   Y = A^T [ sum_ci (G g G^T) (.) (B^T d B) ] A        (d: the tile's 6 x 6 patch)
+// -- 36 transform positions per 16 outputs instead of 16 per 4: 1.78x fewer MFMA
+// multiplies than F(2x2).  Interpolation points 0, +-1, +-2, inf (Lavin & Gray);
+// the transforms scale by up to 8 (A) and 5 (B), so the result carries a few times
+// F(2x2)'s rounding error (2-4e-6 of max|y| on random 64-256-channel data, vs 2e-6
+// for F(2x2) and 4e-7 for a direct fp32 conv).
+//
+// What keeps F(4x4) on the matrix pipe is the input transform: ~170 flops per (tile,
+// input channel), 4x F(2x2)'s.  Round 3's research kernel (tools/research/
+// conv3x3_wino4.hip) let every wave transform the patches of its own tiles, 4x
+// redundantly across the workgroup's channel groups, and ran at 0.40 of the fp32
+// matrix peak.  Here each (tile, channel) is transformed ONCE per workgroup, into
+// LDS, and read back by all the waves that need it:
+//
+//   workgroup = 8 waves (2 per SIMD), 32 tiles (4 x 8 = 16 x 32 output pixels) x 64
+//   output channels; wave (tg, cg) owns tiles 16 tg .. + 15 x channels 16 cg .. + 15 at
+//   all 36 positions (36 MFMA accumulators, 144 registers; the output transform is
+//   lane-local).  K walked in chunks of 8 input channels, three-stage pipeline:
+//     patch DMA (LDS-DMA, chunk ch + 2)  |  transform (waves 0-3, chunk ch + 1,
+//     patch -> V in LDS)  |  MFMAs (all waves, chunk ch, V from LDS, U from L2)
+//   one barrier per chunk.  Waves 0-3 and 4-7 share the SIMDs pairwise, so the
+//   partner wave's MFMAs fill a transforming wave's VALU time.
+// Per chunk and wave: 72 v_mfma_f32_16x16x4_f32, 36 ds_read_b64 (V), 18 U loads
+// (1 KiB each); per transforming lane: 36 ds_read_b32 (patch), ~170 VALU, 36
+// ds_write_b32 (V).
+//
+// LDS (120 KiB, one workgroup per CU):
+//   V [2][36 pos][32 tiles][8 ch] fp32 (36 KiB a stage): a wave's B fragment of a
+//     position is one conflict-free ds_read_b64 (lane (j, q) -> tile 16 tg + j,
+//     channels 2q, 2q + 1: the K permutation shared with U, as in F(2x2));
+//   patch [2][18 rows][84 16-B slots]: pixel column C's two 4-channel halves at slots
+//     2C + C/2 + half (a pad slot every other pixel), so the 64 lanes of a transform
+//     read (8 tiles of a tile row x 8 channels) fall in 64 distinct banks.
+#include <stdlib.h>
+
+#include "common.hpp"
+#include "vosdet_internal.hpp"
+
+namespace vd {
+
+namespace {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+constexpr int k4Co = 64;             // output channels per workgroup
+constexpr int k4KC = 8;              // input channels per chunk
+constexpr int k4Threads = 512;       // 8 waves
+constexpr int k4TR = 4, k4TC = 8;    // tiles per block: 16 x 32 output pixels
+constexpr int k4PR = 4 * k4TR + 2;   // 18 patch rows
+constexpr int k4PC = 4 * k4TC + 2;   // 34 patch columns
+constexpr int k4RP = 84;             // 16-B slots per patch row
+constexpr int k4PSlots = 1536;       // 24 DMA wave instructions (18 x 84 = 1512 used)
+constexpr int k4PStageB = k4PSlots * 16;        // 24 KiB
+constexpr int k4VStageB = 36 * 32 * k4KC * 4;   // 36 KiB
+constexpr int k4ZeroF4 = 1024;                  // zero source for C <= 4096
+
+__device__ float4 g_wino4_zero[k4ZeroF4];
+
+__device__ __forceinline__ void w4_dma_1k(const float *src, uint32_t lds) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(lds)
+        : "memory");
+}
+
+// y = B^T x, B^T = [4 0 -5 0 1 0; 0 -4 -4 1 1 0; 0 4 -4 -1 1 0; 0 -2 -1 2 1 0;
+//                   0 2 -1 -2 1 0; 0 4 0 -5 0 1]
+__device__ __forceinline__ void w4_bt6(const float (&x)[6], float (&y)[6]) {
+    const float t0 = __builtin_fmaf(-4.f, x[2], x[4]), t1 = __builtin_fmaf(-4.f, x[1], x[3]);
+    const float t2 = x[4] - x[2], t3 = 2.f * (x[3] - x[1]);
+    y[0] = __builtin_fmaf(4.f, x[0], __builtin_fmaf(-5.f, x[2], x[4]));
+    y[1] = t0 + t1;
+    y[2] = t0 - t1;
+    y[3] = t2 + t3;
+    y[4] = t2 - t3;
+    y[5] = __builtin_fmaf(4.f, x[1], __builtin_fmaf(-5.f, x[3], x[5]));
+}
+
+// y = A^T m, A^T = [1 1 1 1 1 0; 0 1 -1 2 -2 0; 0 1 1 4 4 0; 0 1 -1 8 -8 1]
+__device__ __forceinline__ void w4_at6(const float (&m)[6], float (&y)[4]) {
+    const float s12 = m[1] + m[2], d12 = m[1] - m[2], s34 = m[3] + m[4], d34 = m[3] - m[4];
+    y[0] = m[0] + s12 + s34;
+    y[1] = __builtin_fmaf(2.f, d34, d12);
+    y[2] = __builtin_fmaf(4.f, s34, s12);
+    y[3] = __builtin_fmaf(8.f, d34, d12) + m[5];
+}
+
+template <bool RELU>
+__global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
+    const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
+    int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
+    int cb_per_xcd) {
+    extern __shared__ __attribute__((aligned(16))) char w4_lds[];
+    float *const vst = reinterpret_cast<float *>(w4_lds);                  // [2][36][32][8]
+    char *const pst = w4_lds + 2 * k4VStageB;                              // [2][1536][16 B]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ncb = Cout / k4Co;
+    int cb, sp;
+    if (cb_per_xcd) {  // XCD x computes channel block x % ncb: its L2 holds one U block
+        const int xcd = blockIdx.x & 7;
+        cb = xcd % ncb;
+        sp = (blockIdx.x >> 3) * (8 / ncb) + xcd / ncb;
+    } else {
+        const int r8 = blockIdx.x % (8 * ncb);
+        cb = r8 / 8;
+        sp = (blockIdx.x / (8 * ncb)) * 8 + (r8 & 7);
+    }
+    if (sp >= N * tby * tbx) return;
+    const int n = sp / (tby * tbx);
+    const int rem = sp - n * tby * tbx;
+    const int tyb = rem / tbx, txb = rem - (rem / tbx) * tbx;
+    const int oy0 = 4 * k4TR * tyb, ox0 = 4 * k4TC * txb;
+    const int iy0 = oy0 - 1, ix0 = ox0 - 1;
+    const int nch = C / k4KC;
+    const uint32_t pbase = (uint32_t)(uintptr_t)pst;
+
+    // ---- patch DMA sources: instructions i = wave + 8 k (k < 3) of 24; slot s ->
+    // row R, column C = 2 m + (rem >> 1), half rem & 1 (rem = 4: the pad slot)
+    const float *psrc[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int s = 64 * (wave + 8 * k) + lane;
+        const int R = s / k4RP, u = s - R * k4RP;
+        const int m = u / 5, r5 = u - 5 * m;
+        const int Cc = 2 * m + (r5 >> 1), hf = r5 & 1;
+        const int y = iy0 + R, x = ix0 + Cc;
+        const bool ok = R < k4PR && r5 < 4 && Cc < k4PC && (unsigned)y < (unsigned)H &&
+                        (unsigned)x < (unsigned)W;
+        psrc[k] = ok ? X + (((int64_t)n * H + y) * W + x) * C + 4 * hf
+                     : reinterpret_cast<const float *>(g_wino4_zero) + 4 * hf;
+    }
+    auto dma = [&](int ch, int stage) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            w4_dma_1k(psrc[k] + ch * k4KC,
+                      pbase + (uint32_t)(stage * k4PStageB + (wave + 8 * k) * 1024));
+    };
+
+    // ---- transform (waves 0-3): lane -> tile (tile row = wave, column tc = lane >> 3),
+    // channel ci = lane & 7; reads pixel (4 tr + r, 4 tc + c), channel ci (slot
+    // (4 tr + r) * 84 + 10 tc + 2 c + c / 2 + ci / 4, word ci % 4), writes V[pos][tile][ci]
+    const int ttc = lane >> 3, tci = lane & 7;
+    const float *const tread =
+        reinterpret_cast<const float *>(pst) + ((4 * wave) * k4RP + 10 * ttc + (tci >> 2)) * 4 +
+        (tci & 3);
+    float *const twrite = vst + 64 * wave + lane;
+    auto transform = [&](int stage) {
+        const float *tp = tread + stage * (k4PStageB / 4);
+        float t[6][6];  // B^T d: column c's 6 values
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            float x[6], y[6];
+#pragma unroll
+            for (int r = 0; r < 6; ++r) x[r] = tp[(r * k4RP + 2 * c + (c >> 1)) * 4];
+            w4_bt6(x, y);
+#pragma unroll
+            for (int a = 0; a < 6; ++a) t[a][c] = y[a];
+        }
+        float *vp = twrite + stage * (k4VStageB / 4);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            float y[6];
+            w4_bt6(t[a], y);
+#pragma unroll
+            for (int b = 0; b < 6; ++b) vp[(6 * a + b) * 256] = y[b];
+        }
+    };
+
+    // ---- MFMAs: wave (tg = wave >> 2, cg = wave & 3), lane (j, q): V fragment of tile
+    // 16 tg + j, channels 2q, 2q + 1; U fragment of channel 16 cg + j (U's layout
+    // [Cout/64][C/8][cg][pp = pos / 2][lane][4], element 2 (pos & 1) + (ci & 1),
+    // conv3x3_wino4_weight_kernel)
+    const int tg = wave >> 2, cg = wave & 3;
+    const int j = lane & 15, q = lane >> 4;
+    const f2v *const vread = reinterpret_cast<const f2v *>(vst + (16 * tg + j) * 8 + 2 * q);
+    const f4v *const ubase =
+        reinterpret_cast<const f4v *>(U) + ((int64_t)cb * nch * 4 + cg) * (18 * 64) + lane;
+    f4v acc[36];
+#pragma unroll
+    for (int p = 0; p < 36; ++p) acc[p] = f4v{0.f, 0.f, 0.f, 0.f};
+    // U fragments: a ring of 9 (positions 2 pp, 2 pp + 1 each); after the MFMAs of pp
+    // its slot is reloaded with pp + 9 of this chunk, then with pp - 9 of the next
+    // chunk, so the next chunk's first half is in flight across the barrier
+    f4v u[9];
+    auto mfma_chunk = [&](int stage, const f4v *ub, const f4v *ubn) {
+        const f2v *vp = vread + stage * (k4VStageB / 8);
+#pragma unroll
+        for (int pp = 0; pp < 18; ++pp) {
+            const f2v b0 = vp[(2 * pp) * 128], b1 = vp[(2 * pp + 1) * 128];
+            const f4v uf = u[pp % 9];
+            acc[2 * pp] = __builtin_amdgcn_mfma_f32_16x16x4f32(uf.x, b0.x, acc[2 * pp], 0, 0, 0);
+            acc[2 * pp] = __builtin_amdgcn_mfma_f32_16x16x4f32(uf.y, b0.y, acc[2 * pp], 0, 0, 0);
+            acc[2 * pp + 1] =
+                __builtin_amdgcn_mfma_f32_16x16x4f32(uf.z, b1.x, acc[2 * pp + 1], 0, 0, 0);
+            acc[2 * pp + 1] =
+                __builtin_amdgcn_mfma_f32_16x16x4f32(uf.w, b1.y, acc[2 * pp + 1], 0, 0, 0);
+            if (pp < 9)
+                u[pp] = ub[(pp + 9) * 64];
+            else
+                u[pp - 9] = ubn[(pp - 9) * 64];
+        }
+    };
+
+    // ---- pipeline: prologue (chunk 0 transformed, chunk 1's patch landed)
+#pragma unroll
+    for (int i = 0; i < 9; ++i) u[i] = ubase[i * 64];
+    dma(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wave < 4) transform(0);
+    if (nch > 1) dma(1, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+        const int sv = ch & 1;
+        const f4v *ub = ubase + (int64_t)ch * (4 * 18 * 64);
+        const f4v *ubn = ubase + (int64_t)(ch + 1 < nch ? ch + 1 : ch) * (4 * 18 * 64);
+        if (ch + 2 < nch) dma(ch + 2, sv);  // stage sv held chunk ch, transformed already
+        if (wave < 4 && ch + 1 < nch) transform(sv ^ 1);
+        mfma_chunk(sv, ub, ubn);
+        // chunk ch + 2's patch (issued before the 18 U loads of this chunk's MFMA
+        // phase) landed; the next chunk's 9 U loads may stay in flight
+        asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        __syncthreads();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // ---- output transform (lane-local): accumulator slot r of lane (j, q) holds output
+    // channel 64 cb + 16 cg + 4 q + r of tile 16 tg + j
+    const int tile = 16 * tg + j, tr = tile >> 3, tc = tile & 7;
+    const int co = cb * k4Co + 16 * cg + 4 * q;
+    const float4 bv = bias ? *reinterpret_cast<const float4 *>(bias + co)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    float o[16][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float tt[4][6];
+#pragma unroll
+        for (int b = 0; b < 6; ++b) {
+            float m[6], y[4];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) m[a] = acc[6 * a + b][r];
+            w4_at6(m, y);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) tt[i][b] = y[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float y[4];
+            w4_at6(tt[i], y);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) o[4 * i + k][r] = y[k];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int yy = oy0 + 4 * tr + i;
+        if (yy >= H) continue;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int xx = ox0 + 4 * tc + k;
+            if (xx >= W) continue;
+            float4 v = make_float4(o[4 * i + k][0] + bv.x, o[4 * i + k][1] + bv.y,
+                                   o[4 * i + k][2] + bv.z, o[4 * i + k][3] + bv.w);
+            if (RELU) {
+                v.x = fmaxf(v.x, 0.f);
+                v.y = fmaxf(v.y, 0.f);
+                v.z = fmaxf(v.z, 0.f);
+                v.w = fmaxf(v.w, 0.f);
+            }
+            *reinterpret_cast<float4 *>(Y + (((int64_t)n * H + yy) * W + xx) * Cout + co) = v;
+        }
+    }
+}
+
+// U = G g G^T of the PyTorch weight w[co][ci][3][3], G = [1/4 0 0; -1/6 -1/6 -1/6;
+// -1/6 1/6 -1/6; 1/24 1/12 1/6; 1/24 -1/12 1/6; 0 0 1], float64, rounded once; stored
+// in the kernel's fragment order [co / 64][ci / 8][cg = co % 64 / 16][pp = pos / 2]
+// [lane = 16 (ci % 8 / 2) + co % 16][2 (pos & 1) + (ci & 1)], pos = 6 a + b.
+__global__ void wino4_weight_kernel(const float *__restrict__ w, int Cout, int C,
+                                    float *__restrict__ U) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)Cout * C) return;
+    const int co = (int)(i / C), ci = (int)(i - (int64_t)(i / C) * C);
+    const int cl = co % k4Co, nch = C / k4KC;
+    const int lane = 16 * ((ci & 7) >> 1) + (cl & 15);
+    float *dst = U + ((((int64_t)(co / k4Co) * nch + ci / k4KC) * 4 + (cl >> 4)) * 18) * 256 +
+                 lane * 4 + (ci & 1);
+    const float *g = w + i * 9;
+    const double Gm[6][3] = {{0.25, 0., 0.},
+                             {-1. / 6, -1. / 6, -1. / 6},
+                             {-1. / 6, 1. / 6, -1. / 6},
+                             {1. / 24, 1. / 12, 1. / 6},
+                             {1. / 24, -1. / 12, 1. / 6},
+                             {0., 0., 1.}};
+    double t[6][3];  // G g
+    for (int a = 0; a < 6; ++a)
+        for (int c = 0; c < 3; ++c)
+            t[a][c] = Gm[a][0] * g[c] + Gm[a][1] * g[3 + c] + Gm[a][2] * g[6 + c];
+    for (int a = 0; a < 6; ++a)
+        for (int b = 0; b < 6; ++b) {
+            const double u = t[a][0] * Gm[b][0] + t[a][1] * Gm[b][1] + t[a][2] * Gm[b][2];
+            const int pos = 6 * a + b;
+            dst[(pos >> 1) * 256 + (pos & 1) * 2] = (float)u;
+        }
+}
+
+}  // namespace
+
+bool conv3x3_wino4_supported(int C, int Cout) {
+    return C % k4KC == 0 && C >= k4KC && C <= 4 * k4ZeroF4 && Cout % k4Co == 0 && Cout >= k4Co;
+}
+
+size_t conv3x3_wino4_weight_floats(int Cout, int C) { return (size_t)Cout * C * 36; }
+
+int launch_conv3x3_wino4_weight(const float *w, int Cout, int C, float *U, hipStream_t s) {
+    const int64_t n = (int64_t)Cout * C;
+    if (n == 0) return VD_OK;
+    if (!conv3x3_wino4_supported(C, Cout)) return VD_ERR_SHAPE;
+    hipLaunchKernelGGL(wino4_weight_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w,
+                       Cout, C, U);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float *U, int Cout,
+                         const float *bias, int relu, float *Y, hipStream_t s) {
+    if ((int64_t)N * H * W == 0) return VD_OK;
+    if (!conv3x3_wino4_supported(C, Cout)) return VD_ERR_SHAPE;
+    if ((int64_t)N * H * W * C >= ((int64_t)1 << 40)) return VD_ERR_SHAPE;
+    const int tby = (H + 4 * k4TR - 1) / (4 * k4TR), tbx = (W + 4 * k4TC - 1) / (4 * k4TC);
+    const int64_t nsp = (int64_t)N * tby * tbx;
+    const int ncb = Cout / k4Co;
+    const int cbx = 8 % ncb == 0;
+    const int64_t blocks = cbx ? (nsp + 8 / ncb - 1) / (8 / ncb) * 8 : (nsp + 7) / 8 * 8 * ncb;
+    if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
+    constexpr size_t lds = 2 * (size_t)k4VStageB + 2 * (size_t)k4PStageB;
+    static_assert(lds <= VD_LDS_BYTES, "LDS");
+    auto kern = relu ? conv3x3_wino4_kernel<true> : conv3x3_wino4_kernel<false>;
+    static bool attr_t = hipFuncSetAttribute(reinterpret_cast<const void *>(conv3x3_wino4_kernel<true>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds) == hipSuccess;
+    static bool attr_f = hipFuncSetAttribute(reinterpret_cast<const void *>(conv3x3_wino4_kernel<false>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds) == hipSuccess;
+    if (!attr_t || !attr_f) return VD_ERR_LAUNCH;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(k4Threads), lds, s, X, N, H, W, C, U,
+                       Cout, bias, Y, tby, tbx, cbx);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
+}  // namespace vd

@@ -670,6 +670,51 @@ def conv3x3_wino_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch
     return out
 
 
+def conv3x3_wino4_weight(w: torch.Tensor) -> Optional[torch.Tensor]:
+    """PyTorch conv weight [Cout][Cin][3][3] -> the Winograd F(4x4,3x3) operand
+    U = G g G^T (6 x 6 positions) in the kernel's fragment order
+    [Cout/64][Cin/8][4][18][64][4] (vd_conv3x3_wino4_weight; once per model).  None
+    for a shape the kernel does not serve."""
+    w_ = _need(w, "w")
+    if w_.dim() != 4 or tuple(w_.shape[2:]) != (3, 3):
+        raise ValueError("conv3x3_wino4_weight: weight %s" % (tuple(w_.shape),))
+    Cout, C = w_.shape[:2]
+    if Cout % 64 or C % 8 or Cout == 0 or C == 0 or C > WINO_MAX_CIN:
+        return None
+    u = torch.empty((Cout // 64, C // 8, 4, 18, 64, 4), dtype=torch.float32, device=w_.device)
+    check(lib().vd_conv3x3_wino4_weight(w_.data_ptr(), Cout, C, u.data_ptr(), _stream()),
+          "vd_conv3x3_wino4_weight")
+    return u
+
+
+def conv3x3_wino4_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch.Tensor],
+                           relu: bool = False, out: Optional[torch.Tensor] = None):
+    """act(conv3x3(x, pad 1) + bias) on a channels_last fp32 tensor by Winograd
+    F(4x4,3x3) (vd_conv3x3_wino4_bias_act); u from conv3x3_wino4_weight.  None for a
+    shape the kernel does not serve."""
+    if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 4 \
+            or not x.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("x must be a channels_last fp32 device tensor")
+    if u is None:
+        return None
+    u_ = _need(u, "u")
+    N, C, H, W = x.shape
+    if u_.dim() != 6 or tuple(u_.shape[1:]) != (C // 8, 4, 18, 64, 4) or C % 8:
+        raise ValueError("u must be [Cout/64][%d][4][18][64][4], got %s" % (C // 8, tuple(u_.shape)))
+    Cout = u_.shape[0] * 64
+    b_ = _need(bias, "bias") if bias is not None else None
+    if out is None:
+        out = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device,
+                          memory_format=torch.channels_last)
+    st = lib().vd_conv3x3_wino4_bias_act(x.data_ptr(), N, H, W, C, u_.data_ptr(), Cout,
+                                         b_.data_ptr() if b_ is not None else None, int(relu),
+                                         out.data_ptr(), _stream())
+    if st == VD_ERR_SHAPE:
+        return None
+    check(st, "vd_conv3x3_wino4_bias_act")
+    return out
+
+
 def gemm_dual_bias_act(a1: torch.Tensor, a2: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
                        relu: bool = True, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """act(a1 @ w[:, :K1].T + a2 @ w[:, K1:].T + bias) in one MFMA kernel
