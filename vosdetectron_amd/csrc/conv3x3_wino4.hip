@@ -98,7 +98,9 @@ __device__ __forceinline__ void w4_at6(const float (&m)[6], float (&y)[4]) {
     y[3] = __builtin_fmaf(8.f, d34, d12) + m[5];
 }
 
-template <bool RELU>
+// PROBE (research timing only, VOSDET_WINO4_PROBE; results are wrong when set): bit 0
+// no transform, bit 1 no MFMA, bit 2 no patch DMA, bit 3 no U reloads
+template <bool RELU, int PROBE>
 __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
@@ -128,26 +130,36 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     const int nch = C / k4KC;
     const uint32_t pbase = (uint32_t)(uintptr_t)pst;
 
-    // ---- patch DMA sources: instructions i = wave + 8 k (k < 3) of 24; slot s ->
-    // row R, column C = 2 m + (rem >> 1), half rem & 1 (rem = 4: the pad slot)
-    const float *psrc[3];
+    // ---- patch DMA (waves 0-3 only, so the U loads of waves 4-7 never wait behind a
+    // patch piece): instructions i = wave + 4 k (k < 6) of 24; slot s -> row R, column
+    // C = 2 m + (rem >> 1), half rem & 1 (rem = 4: the pad slot).  Sources as 32-bit
+    // float offsets in frame n (bit 31: the zero page)
+    const float *const Xn = X + (int64_t)n * H * W * C;
+    // kept in LDS (after the patch stages), not in six registers the MFMA phase needs
+    uint32_t *const poff = reinterpret_cast<uint32_t *>(pst + 2 * k4PStageB) + tid;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const int s = 64 * (wave + 8 * k) + lane;
+    for (int k = 0; k < 6; ++k) {
+        if (wave >= 4) break;
+        const int s = 64 * (wave + 4 * k) + lane;
         const int R = s / k4RP, u = s - R * k4RP;
         const int m = u / 5, r5 = u - 5 * m;
         const int Cc = 2 * m + (r5 >> 1), hf = r5 & 1;
         const int y = iy0 + R, x = ix0 + Cc;
         const bool ok = R < k4PR && r5 < 4 && Cc < k4PC && (unsigned)y < (unsigned)H &&
                         (unsigned)x < (unsigned)W;
-        psrc[k] = ok ? X + (((int64_t)n * H + y) * W + x) * C + 4 * hf
-                     : reinterpret_cast<const float *>(g_wino4_zero) + 4 * hf;
+        poff[256 * k] = ok ? (uint32_t)((y * W + x) * C + 4 * hf) : 0x80000000u | (uint32_t)(4 * hf);
     }
+    const float *const zero = reinterpret_cast<const float *>(g_wino4_zero);
     auto dma = [&](int ch, int stage) {
+        uint32_t oo[6];  // all six offsets read before the first DMA (one LDS round trip)
 #pragma unroll
-        for (int k = 0; k < 3; ++k)
-            w4_dma_1k(psrc[k] + ch * k4KC,
-                      pbase + (uint32_t)(stage * k4PStageB + (wave + 8 * k) * 1024));
+        for (int k = 0; k < 6; ++k) oo[k] = poff[256 * k];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const uint32_t o = oo[k];
+            const float *src = (o & 0x80000000u) ? zero + (o & 7u) : Xn + o + ch * k4KC;
+            w4_dma_1k(src, pbase + (uint32_t)(stage * k4PStageB + (wave + 4 * k) * 1024));
+        }
     };
 
     // ---- transform (waves 0-3): lane -> tile (tile row = wave, column tc = lane >> 3),
@@ -187,51 +199,87 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     const int tg = wave >> 2, cg = wave & 3;
     const int j = lane & 15, q = lane >> 4;
     const f2v *const vread = reinterpret_cast<const f2v *>(vst + (16 * tg + j) * 8 + 2 * q);
-    const f4v *const ubase =
-        reinterpret_cast<const f4v *>(U) + ((int64_t)cb * nch * 4 + cg) * (18 * 64) + lane;
+    // U through a buffer resource: wave-uniform base and per-position offsets in scalar
+    // registers, one VGPR (the lane's 16 B) for all loads
+    const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(U) + (int64_t)__builtin_amdgcn_readfirstlane(
+                                     (cb * nch * 4 + cg) * (18 * 64)) * 4,
+        (short)0, nch * 4 * 18 * 64 * 16, 0x00020000);
+    const int uvoff = lane * 16;
+    auto uload = [&](int ch, int pos) {  // chunk ch, position pair pos
+        return __builtin_bit_cast(
+            f4v, __builtin_amdgcn_raw_buffer_load_b128(urs, uvoff,
+                                                       (ch * 4 * 18 + pos) * 1024, 0));
+    };
     f4v acc[36];
 #pragma unroll
     for (int p = 0; p < 36; ++p) acc[p] = f4v{0.f, 0.f, 0.f, 0.f};
     // U fragments: a ring of 9 (positions 2 pp, 2 pp + 1 each); after the MFMAs of pp
     // its slot is reloaded with pp + 9 of this chunk, then with pp - 9 of the next
     // chunk, so the next chunk's first half is in flight across the barrier
-    f4v u[9];
-    auto mfma_chunk = [&](int stage, const f4v *ub, const f4v *ubn) {
+    constexpr int kUR = 9;  // divides 18: position q of every chunk in slot q % kUR
+    f4v u[kUR];
+    // V fragments are read one position ahead; a scheduling barrier after every
+    // position keeps the U reloads where they are written (left to itself the compiler
+    // sinks them next to their use, and each of the second half's positions then waits
+    // a full L2 round trip) and the V read of position pp + 1 ahead of pp's MFMAs.
+    // xon (waves 0-3): the next chunk's transform rides along -- column c of B^T d at
+    // position c (its patch reads one position ahead), row a of (B^T d) B and its V
+    // writes at position 6 + a -- so its VALU issues between this wave's own MFMAs and
+    // the four SIMDs' two waves reach the barrier together.
+    auto mfma_chunk = [&](bool xon, int stage, int ch, int chn, int tstage) {
         const f2v *vp = vread + stage * (k4VStageB / 8);
+        if (xon) transform(tstage);
+        f2v b0 = vp[0], b1 = vp[128];
 #pragma unroll
         for (int pp = 0; pp < 18; ++pp) {
-            const f2v b0 = vp[(2 * pp) * 128], b1 = vp[(2 * pp + 1) * 128];
-            const f4v uf = u[pp % 9];
+            f2v n0, n1;
+            if (pp < 17) {
+                n0 = vp[(2 * pp + 2) * 128];
+                n1 = vp[(2 * pp + 3) * 128];
+            }
+            const f4v uf = u[pp % kUR];
+            if constexpr (!(PROBE & 2)) {
             acc[2 * pp] = __builtin_amdgcn_mfma_f32_16x16x4f32(uf.x, b0.x, acc[2 * pp], 0, 0, 0);
             acc[2 * pp] = __builtin_amdgcn_mfma_f32_16x16x4f32(uf.y, b0.y, acc[2 * pp], 0, 0, 0);
             acc[2 * pp + 1] =
                 __builtin_amdgcn_mfma_f32_16x16x4f32(uf.z, b1.x, acc[2 * pp + 1], 0, 0, 0);
             acc[2 * pp + 1] =
                 __builtin_amdgcn_mfma_f32_16x16x4f32(uf.w, b1.y, acc[2 * pp + 1], 0, 0, 0);
-            if (pp < 9)
-                u[pp] = ub[(pp + 9) * 64];
-            else
-                u[pp - 9] = ubn[(pp - 9) * 64];
+            } else {
+                acc[2 * pp][0] += b0.x + b1.y;
+            }
+            if constexpr (!(PROBE & 8)) {
+                if (pp + kUR < 18)
+                    u[pp % kUR] = uload(ch, pp + kUR);
+                else
+                    u[pp % kUR] = uload(chn, pp + kUR - 18);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (pp < 17) {
+                b0 = n0;
+                b1 = n1;
+            }
         }
     };
 
     // ---- pipeline: prologue (chunk 0 transformed, chunk 1's patch landed)
 #pragma unroll
-    for (int i = 0; i < 9; ++i) u[i] = ubase[i * 64];
-    dma(0, 0);
+    for (int i = 0; i < kUR; ++i) u[i] = uload(0, i);
+    if (wave < 4) dma(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (wave < 4) transform(0);
-    if (nch > 1) dma(1, 1);
+    if (wave < 4 && nch > 1) dma(1, 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int ch = 0; ch < nch; ++ch) {
         const int sv = ch & 1;
-        const f4v *ub = ubase + (int64_t)ch * (4 * 18 * 64);
-        const f4v *ubn = ubase + (int64_t)(ch + 1 < nch ? ch + 1 : ch) * (4 * 18 * 64);
-        if (ch + 2 < nch) dma(ch + 2, sv);  // stage sv held chunk ch, transformed already
-        if (wave < 4 && ch + 1 < nch) transform(sv ^ 1);
-        mfma_chunk(sv, ub, ubn);
+        const int chn = ch + 1 < nch ? ch + 1 : ch;
+        if (!(PROBE & 4) && wave < 4 && ch + 2 < nch) dma(ch + 2, sv);  // stage sv: chunk ch, transformed
+        // one code path for all waves (a separate transform-free copy of the loop
+        // doubles the live ranges the register allocator sees across the branch)
+        mfma_chunk(!(PROBE & 1) && wave < 4 && ch + 1 < nch, sv, ch, chn, sv ^ 1);
         // chunk ch + 2's patch (issued before the 18 U loads of this chunk's MFMA
         // phase) landed; the next chunk's 9 U loads may stay in flight
         asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
@@ -340,23 +388,50 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
                          const float *bias, int relu, float *Y, hipStream_t s) {
     if ((int64_t)N * H * W == 0) return VD_OK;
     if (!conv3x3_wino4_supported(C, Cout)) return VD_ERR_SHAPE;
-    if ((int64_t)N * H * W * C >= ((int64_t)1 << 40)) return VD_ERR_SHAPE;
+    if ((int64_t)N * H * W * C >= ((int64_t)1 << 40) || (int64_t)H * W * C >= ((int64_t)1 << 31))
+        return VD_ERR_SHAPE;
     const int tby = (H + 4 * k4TR - 1) / (4 * k4TR), tbx = (W + 4 * k4TC - 1) / (4 * k4TC);
     const int64_t nsp = (int64_t)N * tby * tbx;
     const int ncb = Cout / k4Co;
     const int cbx = 8 % ncb == 0;
     const int64_t blocks = cbx ? (nsp + 8 / ncb - 1) / (8 / ncb) * 8 : (nsp + 7) / 8 * 8 * ncb;
     if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
-    constexpr size_t lds = 2 * (size_t)k4VStageB + 2 * (size_t)k4PStageB;
+    constexpr size_t lds = 2 * (size_t)k4VStageB + 2 * (size_t)k4PStageB + 6 * 256 * 4;
     static_assert(lds <= VD_LDS_BYTES, "LDS");
-    auto kern = relu ? conv3x3_wino4_kernel<true> : conv3x3_wino4_kernel<false>;
-    static bool attr_t = hipFuncSetAttribute(reinterpret_cast<const void *>(conv3x3_wino4_kernel<true>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)lds) == hipSuccess;
-    static bool attr_f = hipFuncSetAttribute(reinterpret_cast<const void *>(conv3x3_wino4_kernel<false>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)lds) == hipSuccess;
-    if (!attr_t || !attr_f) return VD_ERR_LAUNCH;
+    static const int probe = [] {
+        const char *e = getenv("VOSDET_WINO4_PROBE");
+        return e ? atoi(e) & 15 : 0;
+    }();
+    typedef void (*kern_t)(const float *, int, int, int, int, const float *, int, const float *,
+                           float *, int, int, int);
+    static const kern_t table[2][16] = {
+        {conv3x3_wino4_kernel<false, 0>, conv3x3_wino4_kernel<false, 1>,
+         conv3x3_wino4_kernel<false, 2>, conv3x3_wino4_kernel<false, 3>,
+         conv3x3_wino4_kernel<false, 4>, conv3x3_wino4_kernel<false, 5>,
+         conv3x3_wino4_kernel<false, 6>, conv3x3_wino4_kernel<false, 7>,
+         conv3x3_wino4_kernel<false, 8>, conv3x3_wino4_kernel<false, 9>,
+         conv3x3_wino4_kernel<false, 10>, conv3x3_wino4_kernel<false, 11>,
+         conv3x3_wino4_kernel<false, 12>, conv3x3_wino4_kernel<false, 13>,
+         conv3x3_wino4_kernel<false, 14>, conv3x3_wino4_kernel<false, 15>},
+        {conv3x3_wino4_kernel<true, 0>, conv3x3_wino4_kernel<true, 1>,
+         conv3x3_wino4_kernel<true, 2>, conv3x3_wino4_kernel<true, 3>,
+         conv3x3_wino4_kernel<true, 4>, conv3x3_wino4_kernel<true, 5>,
+         conv3x3_wino4_kernel<true, 6>, conv3x3_wino4_kernel<true, 7>,
+         conv3x3_wino4_kernel<true, 8>, conv3x3_wino4_kernel<true, 9>,
+         conv3x3_wino4_kernel<true, 10>, conv3x3_wino4_kernel<true, 11>,
+         conv3x3_wino4_kernel<true, 12>, conv3x3_wino4_kernel<true, 13>,
+         conv3x3_wino4_kernel<true, 14>, conv3x3_wino4_kernel<true, 15>}};
+    static const bool attr = [] {
+        bool ok = true;
+        for (int r = 0; r < 2; ++r)
+            for (int p = 0; p < 16; ++p)
+                ok = ok && hipFuncSetAttribute(reinterpret_cast<const void *>(table[r][p]),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)lds) == hipSuccess;
+        return ok;
+    }();
+    if (!attr) return VD_ERR_LAUNCH;
+    const kern_t kern = table[relu ? 1 : 0][probe];
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(k4Threads), lds, s, X, N, H, W, C, U,
                        Cout, bias, Y, tby, tbx, cbx);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
