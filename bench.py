@@ -268,29 +268,32 @@ def ref_cpu_pipeline(sd, n_frames, cfg):
     return ref, fr, what
 
 
-def frame_flops(sd, cfg):
+def frame_flops(sd, cfg, frames=16):
     """Algorithmic FLOPs of one frame (torch.utils.flop_counter,
     2 per MAC, convs + linears incl. the mask head at that frame's detections),
     counted on the reference's CPU path -- independent of how the GPU path
-    fuses or lays out the contractions.  Returns (flops, detections)."""
+    fuses or lays out the contractions.  Returns (flops, detections, direct-form
+    FLOPs the `frames`-frame engine runs as Winograd F(2x2), as F(4x4))."""
     from torch.utils.flop_counter import FlopCounterMode
     ref, fr, _ = ref_cpu_pipeline(sd, 0, cfg)
-    with FlopCounterMode(display=False) as fc, _WinoFlops() as wf:
+    with FlopCounterMode(display=False) as fc, _WinoFlops(frames) as wf:
         res = ref(fr[0])
-    return int(fc.get_total_flops()), int(len(res[1])), wf.flops
+    return int(fc.get_total_flops()), int(len(res[1])), wf.flops, wf.flops4
 
 
 class _WinoFlops(torch.overrides.TorchFunctionMode):
     """Direct-form FLOPs of the frame's 3x3 convolutions the engine runs as
-    Winograd F(2x2,3x3): the engine's own routing rule (modeling.conv3x3_route,
-    incl. the mosaic choice and the block-occupancy gate) applied to the
-    `frames`-frame batch of each conv the reference path runs.  Their MFMA work
-    is 1/2.25 of the direct form's.  Only stride-1 / pad-1 / ungrouped 3x3s with
-    a frame-level batch qualify (the mask head's RoI maps: N = frames x dets)."""
+    Winograd F(2x2,3x3) (`flops`) and F(4x4,3x3) (`flops4`): the engine's own
+    routing rule (modeling.conv3x3_route, incl. the mosaic choice and the
+    block-occupancy gates) applied to the `frames`-frame batch of each conv the
+    reference path runs.  Their MFMA work is 1/2.25 (16 positions per 2x2 tile) and
+    1/4 (36 per 4x4 tile) of the direct form's.  Only stride-1 / pad-1 / ungrouped
+    3x3s with a frame-level batch qualify (the mask head's RoI maps: N = frames x
+    dets)."""
 
     def __init__(self, frames=16):
         super().__init__()
-        self.flops, self.frames = 0, frames
+        self.flops, self.flops4, self.frames = 0, 0, frames
 
     def __torch_function__(self, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
@@ -308,8 +311,11 @@ class _WinoFlops(torch.overrides.TorchFunctionMode):
             N, H, W = out.shape[0], out.shape[2], out.shape[3]
             if tuple(w.shape[2:]) == (3, 3) and st == (1, 1) and pd == (1, 1) and groups == 1:
                 # one reference frame's conv -> the engine's batch of `frames` frames
-                if conv3x3_route(N * self.frames, Cin, Cout, H, W)[0] == "wino":
+                algo = conv3x3_route(N * self.frames, Cin, Cout, H, W)[0]
+                if algo == "wino":
                     self.flops += 2 * N * H * W * Cout * Cin * 9
+                elif algo == "wino4":
+                    self.flops4 += 2 * N * H * W * Cout * Cin * 9
         return out
 
 
@@ -340,61 +346,75 @@ MFMA_FP32_PEAK_TFS = 157.3  # MI355X dense fp32 matrix peak
 
 def measure_dominant_conv(dev, F, H, W, C=256, iters=None):
     """The step's dominant kernel by time: the P2 3x3 256 -> 256 convolution (FPN
-    posthoc and RPN conv, Winograd F(2x2,3x3) on the MFMA pipes), timed alone at
-    the benched shape with HIP events on its stream.  Algorithmic FLOPs are the
-    direct convolution's 2*9*C*Cout per output pixel (what the reference computes;
-    Winograd can take the rate past the peak), executed FLOPs the 16 MFMA
-    positions per 2x2 tile actually run (4/9 of them)."""
-    from vosdetectron_amd import ops
+    posthoc and RPN conv) on the kernel the engine routes it to
+    (modeling.conv3x3_route: Winograd F(4x4,3x3) at the benched 32 frames, F(2x2)
+    below its workgroup gate), timed alone at the benched shape with HIP events on
+    its stream.  Algorithmic FLOPs are the direct convolution's 2*9*C*Cout per
+    output pixel (what the reference computes; Winograd takes the rate past the
+    peak), executed FLOPs the MFMA positions actually run: 16 per 2x2 tile (4/9 of
+    the direct form) or 36 per 4x4 tile (1/4)."""
+    from vosdetectron_amd import modeling, ops
     iters = iters or int(os.environ.get("CONV_ITERS", "10"))
     g = torch.Generator(device=dev).manual_seed(3)
     x = torch.randn((F, C, H, W), generator=g, device=dev).contiguous(
         memory_format=torch.channels_last)
     w = torch.randn((C, C, 3, 3), generator=g, device=dev) / (9 * C) ** .5
     b = torch.randn((C,), generator=g, device=dev)
-    u = ops.conv3x3_wino_weight(w)
-    y = ops.conv3x3_wino_bias_act(x, u, b)
+    algo, mos = modeling.conv3x3_route(F, C, C, H, W)
+    if algo == "wino4":
+        u = ops.conv3x3_wino4_weight(w)
+        run = lambda out=None: ops.conv3x3_wino4_bias_act(x, u, b, out=out)  # noqa: E731
+        name = "vd::conv3x3_wino4_kernel (Winograd F(4x4,3x3), v_mfma_f32_16x16x4_f32)"
+        share, positions = 1 / 4, "36 positions per 4x4 tile, 1/4"
+    else:
+        u = ops.conv3x3_wino_weight(w)
+        run = lambda out=None: ops.conv3x3_wino_bias_act(x, u, b, out=out,  # noqa: E731
+                                                         mosaic=mos or False)
+        name = "vd::conv3x3_wino2_kernel (Winograd F(2x2,3x3), v_mfma_f32_16x16x4_f32)"
+        share, positions = 4 / 9, "16 positions per 2x2 tile, 4/9"
+    y = run()
     if y is None:
         return None
     for _ in range(2):
-        ops.conv3x3_wino_bias_act(x, u, b, out=y)
+        run(y)
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(iters):
-        ops.conv3x3_wino_bias_act(x, u, b, out=y)
+        run(y)
     e1.record(s)
     e1.synchronize()
     t = e0.elapsed_time(e1) / 1e3 / iters
     alg = 2.0 * F * H * W * C * C * 9
-    exe = alg * 4 / 9
+    exe = alg * share
     del x, y, u
-    return {"kernel": "vd::conv3x3_wino2_kernel (Winograd F(2x2,3x3), v_mfma_f32_16x16x4_f32)",
+    return {"kernel": name, "route": algo,
             "bound": "mfma", "shape": [F, C, H, W, C], "avg_launch_us": round(t * 1e6, 1),
             "unit": "TFLOP/s", "peak": MFMA_FP32_PEAK_TFS,
             "achieved": round(exe / t / 1e12, 1),
             "frac": round(exe / t / 1e12 / MFMA_FP32_PEAK_TFS, 4),
             "direct_conv_equivalent_TFs": round(alg / t / 1e12, 1),
             "how": "HIP events over %d launches; achieved / frac = the MFMA work Winograd "
-                   "executes (16 positions per 2x2 tile, 4/9 of the direct FLOPs); "
-                   "direct_conv_equivalent_TFs = direct-conv FLOPs / time, a rate that "
-                   "exceeds the peak by design, not a fraction" % iters}
+                   "executes (%s of the direct FLOPs); direct_conv_equivalent_TFs = "
+                   "direct-conv FLOPs / time, a rate that exceeds the peak by design, "
+                   "not a fraction" % (iters, positions)}
 
 
 def step_roofline(flops_frame, dets_cpu, frames, ms_per_step, engine_launch, frame_hw, blob_hw,
-                  wino_flops_frame=0):
+                  wino_flops_frame=0, wino4_flops_frame=0):
     """the FPS as a fraction of the roofline = sum of per-stage
     bound times / measured step time.  MFMA-bound stages: the FLOPs the engine's
     MFMAs execute for one frame at the fp32 matrix peak -- the reference's
     algorithmic FLOPs (torch.utils.flop_counter on its CPU path) with the
-    convolutions the engine runs as Winograd F(2x2,3x3) priced at the 1/2.25 of
-    their direct form that Winograd multiplies; HBM-bound stages: the box
+    convolutions the engine runs as Winograd F(2x2,3x3) / F(4x4,3x3) priced at the
+    1/2.25 / 1/4 of their direct form that Winograd multiplies; HBM-bound stages: the box
     RoIAlign's algorithmic bytes (the engine's own launch) and frame prep (u8 read
     + fp32 blob write) at 8 TB/s; latency-bound stages (proposals, NMS) carry no
     bound.  `frac` is that executed-work fraction (<= 1 by construction).  Pricing
     every conv in its direct form instead gives a rate, not a fraction (Winograd
     takes it past 1): reported as `direct_conv_equivalent`, never as a frac."""
-    exec_flops = flops_frame - wino_flops_frame * (1 - 1 / 2.25)
+    exec_flops = (flops_frame - wino_flops_frame * (1 - 1 / 2.25)
+                  - wino4_flops_frame * (1 - 1 / 4.0))
     exec_ms = exec_flops * frames / (MFMA_FP32_PEAK_TFS * 1e12) * 1e3
     direct_ms = flops_frame * frames / (MFMA_FP32_PEAK_TFS * 1e12) * 1e3
     h, w = frame_hw
@@ -406,6 +426,7 @@ def step_roofline(flops_frame, dets_cpu, frames, ms_per_step, engine_launch, fra
             "hbm_bound_ms": round(hbm_ms, 3), "frac": round(bound / ms_per_step, 4),
             "executed_gflop_per_frame": round(exec_flops / 1e9, 2),
             "winograd_direct_gflop_per_frame": round(wino_flops_frame / 1e9, 2),
+            "winograd4_direct_gflop_per_frame": round(wino4_flops_frame / 1e9, 2),
             "mfma_util_step": round(exec_ms / ms_per_step, 4),
             "direct_conv_equivalent": {
                 "gflop_per_frame": round(flops_frame / 1e9, 2),
@@ -1108,13 +1129,14 @@ def main():
                 dev, F, getattr(pipe, "Hp", fh) // 4, getattr(pipe, "Wp", fw) // 4)
         nthr = torch.get_num_threads()
         torch.set_num_threads(cpu_share()[0])
-        flops, dets_cpu, wino_flops = frame_flops(sd, cfg)
+        flops, dets_cpu, wino_flops, wino4_flops = frame_flops(sd, cfg, F)
         torch.set_num_threads(nthr)
         extra["step_roofline"] = step_roofline(
             flops, dets_cpu, F, dt / args.steps * 1e3, roof.get("engine_launch") if roof else None,
             (fh, fw),
             (getattr(pipe, "Hp", fh), getattr(pipe, "Wp", fw)),
-            wino_flops if getattr(pipe, "ASYNC", False) and not vos else 0)
+            wino_flops if getattr(pipe, "ASYNC", False) and not vos else 0,
+            wino4_flops if getattr(pipe, "ASYNC", False) and not vos else 0)
     cpu = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:
         cpu = cpu_baseline(args.config, sd, args.cpu_frames, cfg=cfg)

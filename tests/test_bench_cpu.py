@@ -25,6 +25,12 @@ def test_step_roofline_sums_stage_bounds():
     ex = (528e9 - 300e9 * (1 - 1 / 2.25)) * 16 / 157.3e12 * 1e3
     assert abs(r2["mfma_bound_ms"] - round(ex, 3)) < 1e-6
     assert r2["frac"] < r["frac"]
+    # F(4x4) convolutions at 1/4 of theirs
+    r3 = bench.step_roofline(528e9, 100, 16, 72.0, {"algorithmic_bytes_per_launch": 2.0e9},
+                             (800, 1333), (800, 1344), wino_flops_frame=100e9,
+                             wino4_flops_frame=200e9)
+    ex = (528e9 - 100e9 * (1 - 1 / 2.25) - 200e9 * 0.75) * 16 / 157.3e12 * 1e3
+    assert abs(r3["mfma_bound_ms"] - round(ex, 3)) < 1e-6
 
 
 def _fracs(d, path=""):
@@ -89,6 +95,41 @@ def test_roi_align_algorithmic_bytes_counts_union_once():
     # scale 1/4: [2, 10] x [2, 10] -> rows/cols floor(2)..floor(10)+1 = 2..11 inclusive
     touched = 10 * 10
     assert got == 4 * C * touched + 2 * 4 * C * P * P + 2 * 20
+
+
+def test_winograd4_route_gate():
+    """modeling.conv3x3_route sends a 3x3 to Winograd F(4x4) where the launch has
+    >= 1024 16 x 32 x 64 workgroups (4 per CU) and its blocks are >= 50 % real
+    output: at the benched 32 frames P2-P4 and res2-res5 conv2; not P5 / P6, the
+    mask head's 14 x 14 RoI maps (38 %) or a 1-frame P2 (572 workgroups);
+    VOSDET_WINO4=0 turns it off.  Counted by bench._WinoFlops at 1/4 of the
+    direct form."""
+    import torch
+    import torch.nn.functional as F
+    from vosdetectron_amd import modeling
+    r = modeling.conv3x3_route
+    for args in [(32, 256, 256, 200, 336), (32, 256, 256, 100, 168), (32, 256, 256, 50, 84),
+                 (32, 64, 64, 200, 336), (32, 128, 128, 100, 168), (32, 512, 512, 25, 42)]:
+        assert r(*args) == ("wino4", None), args
+    for args in [(32, 256, 256, 25, 42), (32, 256, 256, 13, 21), (3200, 256, 256, 14, 14),
+                 (1, 256, 256, 200, 336), (32, 256, 96, 200, 336)]:
+        assert r(*args)[0] != "wino4", args
+    assert abs(modeling._wino4_block_use(25, 42) - 1050 / 2048) < 1e-12
+    old = os.environ.get("VOSDET_WINO4")
+    try:
+        os.environ["VOSDET_WINO4"] = "0"
+        assert r(32, 256, 256, 200, 336) == ("wino", False)
+    finally:
+        if old is None:
+            os.environ.pop("VOSDET_WINO4", None)
+        else:
+            os.environ["VOSDET_WINO4"] = old
+    x = torch.randn(1, 64, 50, 84)
+    with bench._WinoFlops(frames=32) as wf:
+        F.conv2d(x, torch.randn(256, 64, 3, 3), None, 1, 1)  # 32 x 4 x 3 x 4 WGs: F(4x4)
+        F.conv2d(x[:, :, :25, :42], torch.randn(256, 64, 3, 3), None, 1, 1)  # 512: F(2x2)
+    assert wf.flops4 == 2 * 50 * 84 * 256 * 64 * 9
+    assert wf.flops == 2 * 25 * 42 * 256 * 64 * 9
 
 
 def test_cpu_share_is_positive():
@@ -169,8 +210,10 @@ def test_winograd_input_channel_limit():
     input channels off it (the implicit GEMM or MIOpen / CK take it)."""
     from vosdetectron_amd import modeling, ops
     assert ops.WINO_MAX_CIN == 4096
-    assert modeling.conv3x3_route(16, 4096, 256, 200, 336)[0] == "wino"
-    assert modeling.conv3x3_route(16, 4104, 256, 200, 336)[0] != "wino"
+    assert modeling.conv3x3_route(16, 4096, 256, 200, 336)[0] == "wino4"
+    assert modeling.conv3x3_route(1, 4096, 256, 200, 336)[0] == "wino"
+    for n in (1, 16):
+        assert modeling.conv3x3_route(n, 4104, 256, 200, 336)[0] not in ("wino", "wino4")
 
 
 class _FakePipe:

@@ -174,3 +174,37 @@ def test_conv3x3_wino4_vs_torch(N, C, H, W, Cout, relu):
         assert got.is_contiguous(memory_format=torch.channels_last)
         err = float((got - ref).abs().max())
         assert err <= 5e-5 * max(1., float(ref.abs().max())), err
+
+
+def test_conv3x3_wino4_graph_replay_bit_exact():
+    """The F(4x4) launch captured into a hipGraph (as bench.py replays the step)
+    writes exactly what the direct launch writes: its 126 KiB of LDS is a static
+    allocation (a > 64 KiB dynamic one, set by hipFuncSetAttribute, left a
+    replayed launch's output unwritten), and nothing else is baked in at capture.
+    Replayed twice, with new input copied into the captured buffer in between."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randn(2, 64, 40, 70, generator=g).cuda().contiguous(
+        memory_format=torch.channels_last)
+    x2 = torch.randn(2, 64, 40, 70, generator=g).cuda().contiguous(
+        memory_format=torch.channels_last)
+    w = (torch.randn(128, 64, 3, 3, generator=g) / 24.).cuda()
+    b = torch.randn(128, generator=g).cuda()
+    u = ops.conv3x3_wino4_weight(w)
+    eager = [ops.conv3x3_wino4_bias_act(xx, u, b, relu=True) for xx in (x, x2)]
+    xs = x.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.conv3x3_wino4_bias_act(xs, u, b, relu=True)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        out = ops.conv3x3_wino4_bias_act(xs, u, b, relu=True)
+    for xx, ref in ((x, eager[0]), (x2, eager[1])):
+        xs.copy_(xx)
+        out.fill_(float("nan"))
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)

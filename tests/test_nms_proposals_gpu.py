@@ -380,3 +380,47 @@ def test_proposals_tie_fixture(golden):
         if c["same_rows_as_a_set"]:
             key = lambda a: a[np.lexsort(a.T[::-1])]  # noqa: E731
             assert np.array_equal(key(got), key(g[tag + "_ref_rois"])), tag
+
+
+def test_generate_proposals_graph_replays_like_eager():
+    """vd_generate_proposals (multi-workgroup radix select) captured into a hipGraph
+    and replayed three times, then with new scores: every replay equals an eager
+    call.  Its selection counters are re-zeroed by a kernel inside the step (a
+    captured hipMemsetAsync did not run again at replay on this ROCm: every replay
+    after the first returned count -1, round 5)."""
+    import torch
+    from vosdetectron_amd import ops
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cuda").manual_seed(0)
+    F, A = 4, 3
+    shapes = [(200, 336), (100, 168), (50, 84), (25, 42), (13, 21)]
+    scales = [1 / 4., 1 / 8., 1 / 16., 1 / 32., 1 / 64.]
+    cls = [torch.rand(F, A, h, w, device=dev, generator=g) for h, w in shapes]
+    box = [torch.randn(F, 4 * A, h, w, device=dev, generator=g) * .1 for h, w in shapes]
+    anc = [torch.rand(h * w * A, 4, device=dev, generator=g, dtype=torch.float64) * 500
+           for h, w in shapes]
+    for a in anc:
+        a[:, 2:] += a[:, :2] + 16
+    info = torch.tensor([[800., 1344., 1.]] * F, device=dev)
+    args = (cls, box, anc, scales, info, 1000, 1000, 0.7, 0.)
+    eager = ops.generate_proposals(*args)
+    assert int(eager[2].min()) > 0
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.generate_proposals(*args)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        out = ops.generate_proposals(*args)
+    for _ in range(3):
+        graph.replay()
+        torch.cuda.synchronize()
+        assert all(torch.equal(a, b) for a, b in zip(out, eager))
+    for c in cls:
+        c.uniform_(generator=g)
+    eager2 = ops.generate_proposals(*args)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(out, eager2))

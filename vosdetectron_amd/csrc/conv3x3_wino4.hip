@@ -60,6 +60,7 @@ constexpr int k4PSlots = 1536;       // 24 DMA wave instructions (18 x 84 = 1512
 constexpr int k4PStageB = k4PSlots * 16;        // 24 KiB
 constexpr int k4VStageB = 36 * 32 * k4KC * 4;   // 36 KiB
 constexpr int k4ZeroF4 = 1024;                  // zero source for C <= 4096
+constexpr int k4LdsB = 2 * k4VStageB + 2 * k4PStageB + 6 * 256 * 4;  // + DMA offsets
 
 __device__ float4 g_wino4_zero[k4ZeroF4];
 
@@ -105,7 +106,10 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
     int cb_per_xcd) {
-    extern __shared__ __attribute__((aligned(16))) char w4_lds[];
+    // static, not dynamic: a > 64 KiB dynamic allocation is honoured by a direct launch
+    // after hipFuncSetAttribute but not by the same launch captured into a hipGraph
+    // (every replayed P2 conv came out unwritten, round 5)
+    __shared__ __attribute__((aligned(16))) char w4_lds[k4LdsB];
     float *const vst = reinterpret_cast<float *>(w4_lds);                  // [2][36][32][8]
     char *const pst = w4_lds + 2 * k4VStageB;                              // [2][1536][16 B]
     const int tid = threadIdx.x, lane = tid & 63;
@@ -396,8 +400,7 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
     const int cbx = 8 % ncb == 0;
     const int64_t blocks = cbx ? (nsp + 8 / ncb - 1) / (8 / ncb) * 8 : (nsp + 7) / 8 * 8 * ncb;
     if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
-    constexpr size_t lds = 2 * (size_t)k4VStageB + 2 * (size_t)k4PStageB + 6 * 256 * 4;
-    static_assert(lds <= VD_LDS_BYTES, "LDS");
+    static_assert(k4LdsB <= VD_LDS_BYTES, "LDS");
     static const int probe = [] {
         const char *e = getenv("VOSDET_WINO4_PROBE");
         return e ? atoi(e) & 15 : 0;
@@ -421,18 +424,8 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
          conv3x3_wino4_kernel<true, 10>, conv3x3_wino4_kernel<true, 11>,
          conv3x3_wino4_kernel<true, 12>, conv3x3_wino4_kernel<true, 13>,
          conv3x3_wino4_kernel<true, 14>, conv3x3_wino4_kernel<true, 15>}};
-    static const bool attr = [] {
-        bool ok = true;
-        for (int r = 0; r < 2; ++r)
-            for (int p = 0; p < 16; ++p)
-                ok = ok && hipFuncSetAttribute(reinterpret_cast<const void *>(table[r][p]),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)lds) == hipSuccess;
-        return ok;
-    }();
-    if (!attr) return VD_ERR_LAUNCH;
     const kern_t kern = table[relu ? 1 : 0][probe];
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(k4Threads), lds, s, X, N, H, W, C, U,
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(k4Threads), 0, s, X, N, H, W, C, U,
                        Cout, bias, Y, tby, tbx, cbx);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }

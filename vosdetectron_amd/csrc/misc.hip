@@ -516,4 +516,33 @@ int launch_bias_relu_maxpool(const float *x, const float *bias, int N, int C, in
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
+// [p, p + bytes): the 16-B aligned middle as uint4 stores, the < 16-B head and tail
+// bytes by workgroup 0
+__global__ void zero_kernel(uint8_t *head, int nhead, uint4 *mid, size_t n16, uint8_t *tail,
+                            int ntail) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+        mid[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (blockIdx.x == 0) {
+        if ((int)threadIdx.x < nhead) head[threadIdx.x] = 0;
+        if ((int)threadIdx.x < ntail) tail[threadIdx.x] = 0;
+    }
+}
+
+int zero_async(void *p, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return VD_OK;
+    uint8_t *b = reinterpret_cast<uint8_t *>(p);
+    size_t nhead = (16 - ((uintptr_t)b & 15)) & 15;
+    if (nhead > bytes) nhead = bytes;
+    const size_t n16 = (bytes - nhead) / 16;
+    const size_t ntail = bytes - nhead - n16 * 16;
+    size_t blocks = (n16 + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(zero_kernel, dim3((unsigned)blocks), dim3(256), 0, s, b, (int)nhead,
+                       reinterpret_cast<uint4 *>(b + nhead), n16, b + nhead + n16 * 16,
+                       (int)ntail);
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
+
 }  // namespace vd

@@ -882,7 +882,7 @@ int launch_rpn_proposals(const VdRpnLevel *levels, int num_levels, int num_image
         char *sw = (char *)workspace + sb * slots;
         sel_ws = sw;
         if (nch > 0) {
-            if (hipMemsetAsync(sw, 0, selb * slots, s) != hipSuccess) return VD_ERR_LAUNCH;
+            if (zero_async(sw, selb * slots, s) != VD_OK) return VD_ERR_LAUNCH;
             const dim3 sgrid(nch, num_images);
             for (int pass = 0; pass < kRadixPasses; ++pass)
                 hipLaunchKernelGGL(rpn_sel_hist_kernel, sgrid, dim3(kSelThreads), 0, s, args, sl,

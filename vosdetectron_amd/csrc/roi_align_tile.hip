@@ -732,7 +732,7 @@ int launch_roi_align_fpn_tiled(const FpnLevels &fa, int C, const float *rois, co
     const TileGrid tg = tile_grid(fa);
     const int64_t nb = (int64_t)R * P * P;
     const int S = C / kG;
-    if (hipMemsetAsync(w.ext, 0, w.zero_bytes, s) != hipSuccess) return VD_ERR_LAUNCH;
+    if (zero_async(w.ext, w.zero_bytes, s) != VD_OK) return VD_ERR_LAUNCH;
     const unsigned blk = (unsigned)((nb + 255) / 256);
     const int chunk = chunk_bins();
     const int T = tg.base[fa.L];

@@ -506,7 +506,7 @@ int launch_gn_stats(const GnSets &sets, int nsets, int B, int C, int HW, int G, 
                     hipStream_t s) {
     if (B == 0 || HW == 0) return VD_OK;
     for (int k = 0; k < nsets; ++k)
-        if (hipMemsetAsync(sets.s[k].ws, 0, (size_t)B * G * 2 * sizeof(double), s) != hipSuccess)
+        if (zero_async(sets.s[k].ws, (size_t)B * G * 2 * sizeof(double), s) != VD_OK)
             return VD_ERR_LAUNCH;
     if (nhwc && C % 4 == 0 && G <= 64) {
         const int C4 = C / 4;

@@ -19,6 +19,12 @@ struct FpnLevels {
     int R;  // RoIs of the launch (bounds roi_order entries)
 };
 
+// Zero `bytes` at p with a kernel on stream s.  Used instead of
+// hipMemsetAsync for workspaces a captured step re-zeroes: on this ROCm a captured
+// hipMemsetAsync did not run again at hipGraph replay (the radix select's counters
+// kept the previous replay's values; tools/research/graph_prop_dbg.py, round 5).
+int zero_async(void *p, size_t bytes, hipStream_t s);
+
 int launch_roi_align_fwd_nchw(const float *feat, int B, int C, int H, int W, const float *rois,
                               int R, int PH, int PW, float scale, int sr, float *out,
                               hipStream_t s);

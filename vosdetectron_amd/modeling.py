@@ -109,9 +109,37 @@ def _pick_mosaic(N: int, H: int, W: int, allow=True):
     return best
 
 
+# Winograd F(4x4,3x3) (csrc/conv3x3_wino4.hip): 16 x 32-pixel x 64-channel workgroups,
+# one per CU (120 KiB of LDS), 1.78x fewer MFMA multiplies than F(2x2).  Faster than
+# F(2x2) on every 32-frame step shape with >= 4 workgroups per CU and blocks >= 50 %
+# real output (profiles/r05/wino4/ab_v3.jsonl: P2 7.41 vs 9.31 ms, P3 2.13 vs 2.61,
+# P4 0.65 vs 0.81, res2 0.63 vs 0.85, res5 0.79 vs 0.91); below that its coarse blocks
+# leave CUs idle.  No mosaic: the mask head's 14 x 14 RoI maps stay on F(2x2).
+_WINO4_MIN_WGS = 1024
+_WINO4_MIN_BLOCK_USE = 0.5
+
+
+def _wino4_block_use(H: int, W: int) -> float:
+    """Fraction of the F(4x4) kernel's 16 x 32 output-pixel blocks that is real output."""
+    return H * W / float(-(-H // 16) * 16 * -(-W // 32) * 32)
+
+
+def _wino4_ok(N: int, Cin: int, Cout: int, H: int, W: int) -> bool:
+    """conv3x3_route's F(4x4) gate (VOSDET_WINO4=0 turns it off)."""
+    if os.environ.get("VOSDET_WINO4", "1") == "0":
+        return False
+    if Cout % 64 or Cin % 8 or Cout == 0 or Cin == 0 or Cin > ops.WINO_MAX_CIN:
+        return False
+    if H * W * Cin >= (1 << 31):
+        return False
+    wgs = N * -(-H // 16) * -(-W // 32) * (Cout // 64)
+    return wgs >= _WINO4_MIN_WGS and _wino4_block_use(H, W) >= _WINO4_MIN_BLOCK_USE
+
+
 def conv3x3_route(N: int, Cin: int, Cout: int, H: int, W: int, mosaic=True):
     """(algorithm, mosaic) the engine runs a 3x3 / stride-1 / pad-1 fp32 conv of an
-    N x Cin x H x W channels_last batch with: ('wino', layout) -- Winograd
+    N x Cin x H x W channels_last batch with: ('wino4', None) -- Winograd F(4x4,3x3),
+    csrc/conv3x3_wino4.hip, where _wino4_ok holds -- else ('wino', layout) -- Winograd
     F(2x2,3x3), csrc/conv3x3_wino.hip, from 2^12 output pixels where its blocks are
     >= 60 % real output (Cout % 64, Cin % 8) -- else ('igemm', None), the implicit
     GEMM (csrc/conv3x3.hip), from 2^18 pixels, else (None, None): MIOpen / CK.
@@ -120,6 +148,8 @@ def conv3x3_route(N: int, Cin: int, Cout: int, H: int, W: int, mosaic=True):
     mos, use = _pick_mosaic(N, H, W, mosaic)
     wino = (os.environ.get("VOSDET_CONV3X3_ALGO", CONV3X3_ALGO) == "wino" and Cout % 64 == 0
             and Cin % 8 == 0 and Cout > 0 and Cin <= ops.WINO_MAX_CIN)
+    if wino and _wino4_ok(N, Cin, Cout, H, W):
+        return "wino4", None
     if wino and npx >= _WINO_MIN_PIXELS and use >= _WINO_MIN_BLOCK_USE:
         return "wino", mos
     if npx < _CONV3X3_MIN_PIXELS:
@@ -132,7 +162,7 @@ def conv3x3_route(N: int, Cin: int, Cout: int, H: int, W: int, mosaic=True):
 
 
 # conv3x3 launches per route since the last reset (host-side, also counted while a
-# hipGraph is captured): 'wino', 'wino_rows', 'wino_2d', 'igemm', 'miopen'
+# hipGraph is captured): 'wino4', 'wino', 'wino_rows', 'wino_2d', 'igemm', 'miopen'
 ROUTE_COUNTS = {}
 
 
@@ -162,6 +192,15 @@ def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=True):
     b = conv.bias.detach() if (bias and conv.bias is not None) else None
     algo, mos = conv3x3_route(x.shape[0], x.shape[1], w.shape[0], x.shape[2], x.shape[3],
                               mosaic)
+    if algo == "wino4":
+        if getattr(conv, "_vd_u4_key", None) != key:
+            conv._vd_u4 = ops.conv3x3_wino4_weight(w.detach())
+            conv._vd_u4_key = key
+        y = ops.conv3x3_wino4_bias_act(x, conv._vd_u4, b, relu=relu)
+        if y is not None:
+            _count_route("wino4")
+            return y
+        algo, mos = "wino", _pick_mosaic(x.shape[0], x.shape[2], x.shape[3], mosaic)[0]
     if algo == "wino":
         if getattr(conv, "_vd_u_key", None) != key:
             conv._vd_u = ops.conv3x3_wino_weight(w.detach())
