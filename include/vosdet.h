@@ -223,6 +223,20 @@ int vd_conv3x3_wino_mosaic_bias_act(const float *X, int R, int H, int W, int C, 
 int vd_gemm_dual_bias_act(const float *A1, int K1, const float *A2, int K2, int M, const float *W,
                           int N, const float *bias, int relu, float *D, void *stream);
 
+/* The FPN top-down lateral step in one MFMA GEMM with the nearest-2x add fused
+ * (replaces lib/modeling/FPN.py:292-300 topdown_lateral_module.forward, which runs
+ * in PyTorch in the reference: lat = conv_lateral(lateral); td = F.upsample(top,
+ * scale_factor=2, mode='nearest'); return lat + td):
+ *   D[p][co] = (A[p] . W[co] + bias[co]) + top[up(p)][co]
+ * A: M x K NHWC rows of the lateral (M = images x H x W), top: images x H/2 x W/2 x N
+ * (NULL: no top-down term), D: M x N.  H, W even.  Wf from vd_fpn_lateral_weight
+ * (W [N][K] row-major -> an opaque fragment order, K x N fp32, once per model).
+ * N == 256 and K in {256, 512, 1024}; VD_ERR_SHAPE otherwise. */
+int vd_fpn_lateral_weight(const float *W, int N, int K, float *Wf, void *stream);
+int vd_fpn_lateral_topdown(const float *A, int64_t M, int K, const float *Wf, int N,
+                           const float *bias, const float *top, int H, int W, float *D,
+                           void *stream);
+
 /* ---------------------------------------------------------------------------
  * NMS with the semantics of the NMS the reference executes,
  * utils.boxes.nms -> cython_nms.nms (lib/utils/boxes.py:329-333,

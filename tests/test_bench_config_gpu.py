@@ -71,6 +71,8 @@ def test_bench_batch_routes(bench_setup):
     # F(2x2): posthoc P5 + RPN P5 / P6 + the mask head's four convs at least
     assert routes.get("wino4", 0) >= 6 + 3 + 3 + 5 + 2, routes
     assert n_wino >= 7 and routes.get("wino_2d", 0) >= 7, routes
+    # the P2 top-down lateral step as one fused MFMA launch (modeling._fpn_lateral_fused_k)
+    assert routes.get("fpn_lateral", 0) == 1, routes
 
 
 @pytest.mark.parametrize("f", [0, 7, BATCH - 1])

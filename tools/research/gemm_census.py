@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Every GEMM of one eager 16-frame FPN step (ops.gemm_bias_act / gemm_dual_bias_act,
+"""Every GEMM of one eager F-frame FPN step (F = argv[1], default 32) (ops.gemm_bias_act / gemm_dual_bias_act,
 F.linear, torch._addmm_activation): shape, calls, and its time alone with HIP events
 (pinned plans), as TF/s against the 157.3 TF/s fp32 matrix peak.  One process."""
 import collections
@@ -40,12 +40,21 @@ def timed(fn, iters=10):
 dev = torch.device("cuda", 0)
 cfg = vcfg.get("e2e_mask_rcnn_R-50-FPN_1x")
 model, sd = build_model(cfg, seed=0, device=dev, channels_last=True)
-pipe, fh, fw = bench.make_pipeline(cfg, model, 16, "nhwc", dev)
-frames = torch.from_numpy(bench.synthetic_frames(16, 1, fh, fw)).to(dev)
+NF = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+pipe, fh, fw = bench.make_pipeline(cfg, model, NF, "nhwc", dev)
+frames = torch.from_numpy(bench.synthetic_frames(NF, 1, fh, fw)).to(dev)
 pipe.run(frames)
 torch.cuda.synchronize()
 
 g0, gd0, lin0, addmm0 = ops.gemm_bias_act, ops.gemm_dual_bias_act, Fn.linear, torch._addmm_activation
+fl0 = ops.fpn_lateral_topdown
+
+
+def fl(lat, wf, bias, top):
+    c = (lat.clone(), wf.clone(), bias.clone(), None if top is None else top.clone())
+    N, K, H, W = lat.shape
+    log("fpn_lateral" + ("+top" if top is not None else ""), N * H * W, 256, K, lambda: fl0(*c))
+    return fl0(lat, wf, bias, top)
 
 
 def g(a, w, bias, residual=None, relu=True, out=None):
@@ -75,9 +84,11 @@ def addmm(b, x, w, **kw):
 
 
 ops.gemm_bias_act, ops.gemm_dual_bias_act, Fn.linear, torch._addmm_activation = g, gd, lin, addmm
+ops.fpn_lateral_topdown = fl
 pipe.run(frames)
 torch.cuda.synchronize()
 ops.gemm_bias_act, ops.gemm_dual_bias_act, Fn.linear, torch._addmm_activation = g0, gd0, lin0, addmm0
+ops.fpn_lateral_topdown = fl0
 tot_ms = tot_gf = 0.0
 for (kind, M, N, K), (n, fn) in seen.items():
     ms = timed(fn)

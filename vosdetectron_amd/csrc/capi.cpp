@@ -173,6 +173,18 @@ int vd_conv3x3_wino_mosaic_bias_act(const float *X, int R, int H, int W, int C, 
     return launch_conv3x3_wino_mosaic(X, R, H, W, C, U, Cout, bias, relu, Y, VD_STREAM(stream));
 }
 
+int vd_fpn_lateral_weight(const float *W, int N, int K, float *Wf, void *stream) {
+    if (!W || !Wf) return VD_ERR_ARG;
+    return launch_fpn_lateral_weight(W, N, K, Wf, VD_STREAM(stream));
+}
+
+int vd_fpn_lateral_topdown(const float *A, int64_t M, int K, const float *Wf, int N,
+                           const float *bias, const float *top, int H, int W, float *D,
+                           void *stream) {
+    if (M < 0 || !Wf || !bias || !D || (M > 0 && !A)) return VD_ERR_ARG;
+    return launch_fpn_lateral(A, M, K, Wf, N, bias, top, H, W, D, VD_STREAM(stream));
+}
+
 int vd_gemm_dual_bias_act(const float *A1, int K1, const float *A2, int K2, int M, const float *W,
                           int N, const float *bias, int relu, float *D, void *stream) {
     if (M < 0 || K1 < 1 || K2 < 1 || N < 1 || !W || !bias || !D || (M > 0 && (!A1 || !A2)))

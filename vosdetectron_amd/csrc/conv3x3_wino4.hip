@@ -105,7 +105,7 @@ template <bool RELU, int PROBE>
 __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
-    int cb_per_xcd) {
+    int cb_per_xcd, int probe_hi) {
     // static, not dynamic: a > 64 KiB dynamic allocation is honoured by a direct launch
     // after hipFuncSetAttribute but not by the same launch captured into a hipGraph
     // (every replayed P2 conv came out unwritten, round 5)
@@ -334,7 +334,10 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
                 v.z = fmaxf(v.z, 0.f);
                 v.w = fmaxf(v.w, 0.f);
             }
-            *reinterpret_cast<float4 *>(Y + (((int64_t)n * H + yy) * W + xx) * Cout + co) = v;
+            // probe_hi bit 0 (research, VOSDET_WINO4_PROBE bit 4): no output stores (a
+            // store the data never takes keeps the values live)
+            if (!(probe_hi & 1) || v.x == 1234.5678f)
+                *reinterpret_cast<float4 *>(Y + (((int64_t)n * H + yy) * W + xx) * Cout + co) = v;
         }
     }
 }
@@ -405,8 +408,12 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
         const char *e = getenv("VOSDET_WINO4_PROBE");
         return e ? atoi(e) & 15 : 0;
     }();
+    static const int probe_hi = [] {
+        const char *e = getenv("VOSDET_WINO4_PROBE");
+        return e ? (atoi(e) >> 4) & 1 : 0;
+    }();
     typedef void (*kern_t)(const float *, int, int, int, int, const float *, int, const float *,
-                           float *, int, int, int);
+                           float *, int, int, int, int);
     static const kern_t table[2][16] = {
         {conv3x3_wino4_kernel<false, 0>, conv3x3_wino4_kernel<false, 1>,
          conv3x3_wino4_kernel<false, 2>, conv3x3_wino4_kernel<false, 3>,
@@ -426,7 +433,7 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
          conv3x3_wino4_kernel<true, 14>, conv3x3_wino4_kernel<true, 15>}};
     const kern_t kern = table[relu ? 1 : 0][probe];
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(k4Threads), 0, s, X, N, H, W, C, U,
-                       Cout, bias, Y, tby, tbx, cbx);
+                       Cout, bias, Y, tby, tbx, cbx, probe_hi);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 

@@ -75,6 +75,10 @@ int launch_gemm1x1_dual(const float *A1, int K1, const float *A2, int K2, int M,
                         int N, const float *bias, int relu, float *D, hipStream_t s);
 int launch_gemm1x1_mfma(const float *A, int M, int K, const float *W, int N, const float *bias,
                         const float *R, int relu, float *D, hipStream_t s);
+bool fpn_lateral_supported(int K, int N);
+int launch_fpn_lateral_weight(const float *W, int N, int K, float *Wf, hipStream_t s);
+int launch_fpn_lateral(const float *A, int64_t M, int K, const float *Wf, int N, const float *bias,
+                       const float *T, int H, int Wd, float *D, hipStream_t s);
 
 int launch_roi_align_legacy_fwd(const float *feat, int B, int C, int H, int W, const float *rois,
                                 int R, int PH, int PW, float scale, float *out, hipStream_t s);

@@ -519,6 +519,13 @@ class TopdownLateral(nn.Module):
                 return _gn_epi(self.conv_lateral[0], self.conv_lateral[1], lateral, act=None,
                                res=top, up=True)
             c = self.conv_lateral
+            wf = getattr(self, "_vd_wf", None)
+            if wf is not None and _gemm_ok(lateral) and top.shape[2] * 2 == lateral.shape[2] \
+                    and top.shape[3] * 2 == lateral.shape[3]:
+                # the lateral 1x1, its bias and the nearest-2x top-down add in one
+                # MFMA launch (csrc/gemm_lateral.hip): no separate pass over the sum
+                _count_route("fpn_lateral")
+                return ops.fpn_lateral_topdown(lateral, wf, c.bias, top)
             if _gemm_ok(lateral) and _is_1x1(c) and c.stride == (1, 1):
                 # the lateral 1x1 as a GEMM with its bias fused, then the nearest-2x
                 # top-down add (MIOpen / CK took it before; at small batches their
@@ -1007,11 +1014,30 @@ def prepare_resnet_body(body: ResNetBody, epilogue: bool = True):
 
 
 @torch.no_grad()
+def _fpn_lateral_fused_k():
+    """Lateral input widths whose top-down step runs as ONE fused MFMA launch
+    (ops.fpn_lateral_topdown).  Measured at the benched 32-frame shapes
+    (profiles/r05/fpn_lateral/ab.jsonl): P2 (K = 256) 2.64 ms fused vs 3.13 ms for
+    hipBLASLt + the add pass; P3 (512) even; P4 (1024) 0.68 vs 0.55 -- so P2 only by
+    default.  VOSDET_FPN_LATERAL = 0 (none) | all | comma-separated K list."""
+    v = os.environ.get("VOSDET_FPN_LATERAL", "256").strip().lower()
+    if v in ("0", "", "none"):
+        return ()
+    if v == "all":
+        return ops.FPN_LATERAL_K
+    return tuple(int(k) for k in v.split(","))
+
+
 def prepare_fpn_body(fpn: FPNBody, epilogue: bool = True):
     """Inference-time rewrite of an FPNBody: AffineChannel2d folded into the
     convs (BN bodies) and the fused HIP epilogues switched on."""
     prepare_resnet_body(fpn.conv_body, epilogue)
     for m in fpn.topdown_lateral_modules:
+        m._vd_wf = None
+        c = m.conv_lateral
+        if epilogue and not m.use_gn and c.weight.is_cuda and _is_1x1(c) and c.stride == (1, 1) \
+                and c.bias is not None and c.in_channels in _fpn_lateral_fused_k():
+            m._vd_wf = ops.fpn_lateral_weight(c.weight.detach())
         m.epilogue = epilogue
     fpn.epilogue = epilogue
     return fpn

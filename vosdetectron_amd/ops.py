@@ -740,6 +740,58 @@ def gemm_dual_bias_act(a1: torch.Tensor, a2: torch.Tensor, w: torch.Tensor, bias
     return out
 
 
+FPN_LATERAL_K = (256, 512, 1024)  # csrc/gemm_lateral.hip (N = 256)
+
+
+def fpn_lateral_weight(w: torch.Tensor) -> Optional[torch.Tensor]:
+    """The lateral 1x1 conv weight [256][K] (or [256][K][1][1]) -> the fragment order
+    vd_fpn_lateral_topdown reads (vd_fpn_lateral_weight; once per model).  None for a
+    shape the kernel does not serve (N != 256 or K not in FPN_LATERAL_K)."""
+    w_ = _need(w, "w").reshape(w.shape[0], -1).contiguous()
+    N, K = w_.shape
+    if N != 256 or K not in FPN_LATERAL_K:
+        return None
+    wf = torch.empty((K // 32, 16, 2, 64, 4), dtype=torch.float32, device=w_.device)
+    check(lib().vd_fpn_lateral_weight(w_.data_ptr(), N, K, wf.data_ptr(), _stream()),
+          "vd_fpn_lateral_weight")
+    return wf
+
+
+def fpn_lateral_topdown(lateral: torch.Tensor, wf: torch.Tensor, bias: torch.Tensor,
+                        top: Optional[torch.Tensor]) -> torch.Tensor:
+    """FPN.py topdown_lateral_module.forward (:292-300) in one MFMA launch
+    (vd_fpn_lateral_topdown): conv_lateral(lateral) + nearest-2x(top), the sum in the
+    reference's order ((conv + bias) + top).  lateral: channels_last N x K x H x W fp32;
+    top: channels_last N x 256 x H/2 x W/2 (None: the lateral conv alone); wf from
+    fpn_lateral_weight.  Returns a channels_last N x 256 x H x W tensor."""
+    if not lateral.is_cuda or lateral.dtype != torch.float32 or lateral.dim() != 4 \
+            or not lateral.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("lateral must be a channels_last fp32 device tensor")
+    N, K, H, W = lateral.shape
+    wf_ = _need(wf, "wf")
+    b_ = _need(bias, "bias")
+    if tuple(wf_.shape) != (K // 32, 16, 2, 64, 4) or b_.numel() != 256:
+        raise ValueError("fpn_lateral_topdown: wf %s / bias %s for K = %d"
+                         % (tuple(wf_.shape), tuple(b_.shape), K))
+    t_ = None
+    if top is not None:
+        if tuple(top.shape) != (N, 256, H // 2, W // 2) or H % 2 or W % 2:
+            raise ValueError("top must be %s, got %s" % ((N, 256, H // 2, W // 2),
+                                                         tuple(top.shape)))
+        if not top.is_cuda or top.dtype != torch.float32:
+            raise ValueError("top must be a float32 device tensor")
+        # (not _need: its .contiguous() would copy a channels_last tensor to NCHW)
+        t_ = top if top.is_contiguous(memory_format=torch.channels_last) else \
+            top.contiguous(memory_format=torch.channels_last)
+    out = torch.empty((N, 256, H, W), dtype=torch.float32, device=lateral.device,
+                      memory_format=torch.channels_last)
+    check(lib().vd_fpn_lateral_topdown(lateral.data_ptr(), N * H * W, K, wf_.data_ptr(), 256,
+                                       b_.data_ptr(), t_.data_ptr() if t_ is not None else None,
+                                       H, W, out.data_ptr(), _stream()),
+          "vd_fpn_lateral_topdown")
+    return out
+
+
 def pixel_lut(pixel_means=(102.9801, 115.9465, 122.7717)) -> np.ndarray:
     """float32(u - mean_c) for u in 0..255 exactly as numpy computes
     ``im.astype(float32); im -= PIXEL_MEANS`` (float64 subtraction, float32 store,
