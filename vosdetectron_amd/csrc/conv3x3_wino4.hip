@@ -342,6 +342,307 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Position-split form (round 5, VOSDET_WINO4_PS): the same block (32 tiles x 64 output
+// channels, 8-channel chunks, patch DMA -> transform -> MFMA pipeline), but a wave owns
+// a set of transform POSITIONS for all 64 channels x 32 tiles instead of all 36
+// positions for 16 channels x 16 tiles:
+//   waves 0-3: positions 5 w .. 5 w + 4 (MFMAs only), waves 4-7: positions 20 + 4 v ..
+//   + 3 (and the patch DMA + transform); each SIMD pairs a 5- and a 4-position wave:
+//   144 MFMAs per SIMD per chunk, as before.
+//   per position and chunk: 2 V fragments (ds_read_b64) and 4 U fragments (b64 buffer
+//   loads) feed 16 MFMAs (was 2 + 1 b128 for 4): a quarter of the V reads and half the
+//   U bytes per workgroup, and 16 independent MFMAs between dependences instead of 4.
+// The output transform needs all 36 positions of a (tile, channel): after the K loop
+// the accumulators go through LDS in four 16-channel rounds (positions 0-15 in the V
+// stage 0 array, 16-31 in V stage 1, 32-35 in patch stage 0), one (tile, channel) per
+// thread.  The MFMA operands, their order and the output transform are the first
+// form's, so the results are bit-identical to it.
+// Patch fill through registers (three LDS stages: loaded at the end of one chunk,
+// written at the end of the next), not LDS-DMA: the asm DMA is invisible to the
+// compiler's vmcnt bookkeeping, so a wait for a U load issued before a DMA also waited
+// for the DMA; the builtin is counted but makes every barrier wait for all loads.
+constexpr int k4VStageF = 36 * 32 * k4KC;  // floats per V stage
+constexpr int k4XS = 32 * 16;              // exchange floats per position (16 ch x 32 tiles)
+
+template <bool RELU, int NP, bool XW, int PP>
+__device__ __forceinline__ void wino4ps_body(
+    const float *__restrict__ Xn, int H, int W, int C, const float *__restrict__ U, int Cout,
+    const float *__restrict__ bias, float *__restrict__ Y, int n, int cb, int oy0, int ox0,
+    float4 *pst, float *vs, uint32_t *poff, int wave, int lane) {
+    const int nch = C / k4KC;
+    const int p0 = XW ? 20 + 4 * (wave - 4) : 5 * wave;
+    const int tw = wave & 3;  // XW: transform tile row / DMA instruction group
+    const int j = lane & 15, q = lane >> 4;
+    const int tid = wave * 64 + lane;
+
+    // ---- patch fill (XW waves): slot group i = tw + 4 k (k < 6) of 24, sources from the
+    // offsets in poff (bit 31: the zero page), loaded into registers at the start of a
+    // chunk and written to the stage at its end: ordinary compiler-counted loads, so no
+    // wait ever covers more than it needs (an LDS-DMA either hid from the compiler's
+    // vmcnt counts -- asm -- or, as the builtin, made it wait for everything at each
+    // barrier)
+    const float *const zero = reinterpret_cast<const float *>(g_wino4_zero);
+    // (inline in the chunk body, not lambdas over a captured array: a captured
+    // register array is kept in scratch memory)
+#define VD_W4PS_PLOAD(CH, PR)                                                              \
+    {                                                                                      \
+        uint32_t oo_[6];                                                                   \
+        _Pragma("unroll") for (int k = 0; k < 6; ++k) oo_[k] = poff[256 * k + (tid - 256)]; \
+        _Pragma("unroll") for (int k = 0; k < 6; ++k) {                                    \
+            const uint32_t o = oo_[k];                                                     \
+            const float *src = (o & 0x80000000u) ? zero + (o & 7u) : Xn + o + (CH) * k4KC; \
+            PR[k] = *reinterpret_cast<const f4v *>(src);                                   \
+        }                                                                                  \
+    }
+#define VD_W4PS_PSTORE(STAGE, PR)                                                          \
+    _Pragma("unroll") for (int k = 0; k < 6; ++k)                                          \
+        *reinterpret_cast<f4v *>((STAGE) + (tw + 4 * k) * 64 + lane) = PR[k];
+    // ---- transform (XW waves): as the first form's, tile row tw
+    const int ttc = lane >> 3, tci = lane & 7;
+    const int tro = ((4 * tw) * k4RP + 10 * ttc + (tci >> 2)) * 4 + (tci & 3);
+    auto transform = [&](const float4 *pstage, float *vstage) {
+        const float *tp = reinterpret_cast<const float *>(pstage) + tro;
+        float t[6][6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            float x[6], y[6];
+#pragma unroll
+            for (int r = 0; r < 6; ++r) x[r] = tp[(r * k4RP + 2 * c + (c >> 1)) * 4];
+            w4_bt6(x, y);
+#pragma unroll
+            for (int a = 0; a < 6; ++a) t[a][c] = y[a];
+        }
+        float *vp = vstage + 64 * tw + lane;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            float y[6];
+            w4_bt6(t[a], y);
+#pragma unroll
+            for (int b = 0; b < 6; ++b) vp[(6 * a + b) * 256] = y[b];
+        }
+    };
+
+    // ---- U: the first form's layout [Cout/64][C/8][cg][pp][lane][4], element
+    // 2 (pos & 1) + (ci & 1): co-tile i of position p is the float2 at
+    // (((ch * 4 + i) * 18 + p / 2) * 64 + lane) * 4 + 2 (p & 1)
+    const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(U) + (int64_t)__builtin_amdgcn_readfirstlane(cb * nch * 4 * 18 * 256),
+        (short)0, nch * 4 * 18 * 64 * 16, 0x00020000);
+    const int uvoff = lane * 16;
+    auto uload = [&](int ch, int p, int i) {
+        return __builtin_bit_cast(
+            f2v, __builtin_amdgcn_raw_buffer_load_b64(
+                     urs, uvoff + 8 * (p & 1), ((ch * 4 + i) * 18 + (p >> 1)) * 1024, 0));
+    };
+    // U: a whole chunk's positions in registers.  MFMA-only waves reload position k's
+    // slot for the next chunk right after its MFMAs; the transforming waves load the
+    // next chunk's batch at the end of the chunk, BEFORE their patch loads: vmcnt
+    // retires loads in issue order, so a U load issued after a patch load (HBM, the
+    // longest latency here) could not be waited for without waiting for the patch
+    constexpr int UR = NP;
+    f2v ub[UR][4];
+#pragma unroll
+    for (int k = 0; k < UR; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ub[k][i] = uload(0, p0 + k, i);
+
+    f4v acc[NP][4][2];
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int g = 0; g < 2; ++g) acc[k][i][g] = f4v{0.f, 0.f, 0.f, 0.f};
+
+    // V fragment of position p, tile group g: lane (j, q) -> tile 16 g + j, channels 2q, 2q+1
+    const int vro = (16 * 0 + j) * 8 + 2 * q;
+    // Patch pipeline, three stages: the registers loaded at the END of chunk ch (patch
+    // of chunk ch + 3, the last memory loads the chunk issues, so no U wait ever sits
+    // behind them) are written to their stage at the end of chunk ch + 1 and
+    // transformed during chunk ch + 2.
+    f4v pr[6];  // f4v, not float4: an array of the struct type stays in scratch
+    auto chunk = [&](int ch) {
+        if (XW) {
+            // no scheduling barrier: the compiler interleaves the transform's VALU and
+            // LDS traffic with this wave's first MFMAs (serialised it cost 1.8 ms at P2)
+            if (!(PP & 1) && ch + 1 < nch)
+                transform(pst + ((ch + 1) % 3) * k4PSlots, vs + ((ch + 1) & 1) * k4VStageF);
+        }
+        const int chn = ch + 1 < nch ? ch + 1 : ch;
+        const f2v *vp = reinterpret_cast<const f2v *>(vs + (ch & 1) * k4VStageF + vro);
+        f2v v0 = vp[(p0 * 256) / 2], v1 = vp[(p0 * 256 + 128) / 2];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            const int p = p0 + k;
+            f2v n0, n1;
+            if (k + 1 < NP) {
+                n0 = vp[((p + 1) * 256) / 2];
+                n1 = vp[((p + 1) * 256 + 128) / 2];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const f2v u = ub[k][i];
+                if constexpr (PP & 2) {  // research probe: no MFMAs
+                    acc[k][i][0][0] += u.x + v0.x + v1.y;
+                } else {
+                acc[k][i][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u.x, v0.x, acc[k][i][0], 0, 0, 0);
+                acc[k][i][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(u.y, v0.y, acc[k][i][0], 0, 0, 0);
+                acc[k][i][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(u.x, v1.x, acc[k][i][1], 0, 0, 0);
+                acc[k][i][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(u.y, v1.y, acc[k][i][1], 0, 0, 0);
+                }
+            }
+            if (!XW) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (!(PP & 8)) ub[k][i] = uload(chn, p, i);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (k + 1 < NP) {
+                v0 = n0;
+                v1 = n1;
+            }
+        }
+        if (XW) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (!(PP & 8)) ub[k][i] = uload(chn, p0 + k, i);
+            __builtin_amdgcn_sched_barrier(0);
+            // unconditional (past the last chunk: the last chunk's patch again, into a
+            // stage nothing reads)
+            if constexpr (!(PP & 4)) {
+                VD_W4PS_PSTORE(pst + ((ch + 2) % 3) * k4PSlots, pr)
+                VD_W4PS_PLOAD(ch + 3 < nch ? ch + 3 : nch - 1, pr)
+            }
+        }
+        __syncthreads();
+    };
+
+    // ---- prologue: patches 0 and 1 in their stages, chunk 0 transformed, patch 2 in
+    // the registers
+    if (XW) {
+        VD_W4PS_PLOAD(0, pr)
+        VD_W4PS_PSTORE(pst, pr)
+        VD_W4PS_PLOAD(nch > 1 ? 1 : 0, pr)
+        VD_W4PS_PSTORE(pst + k4PSlots, pr)
+    }
+    __syncthreads();
+    if (XW) {
+        VD_W4PS_PLOAD(nch > 2 ? 2 : nch - 1, pr)
+        transform(pst, vs);
+    }
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) chunk(ch);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#undef VD_W4PS_PLOAD
+#undef VD_W4PS_PSTORE
+
+    // ---- output: four rounds of 16 channels (co-tile rr) through LDS, then one
+    // (tile, channel) per thread: tile = tid >> 4, channel 16 rr + (tid & 15)
+    float *const xs0 = vs, *const xs1 = vs + k4VStageF, *const xs2 = reinterpret_cast<float *>(pst);
+    auto xpos = [&](int p) {  // exchange base of position p
+        return p < 16 ? xs0 + p * k4XS : (p < 32 ? xs1 + (p - 16) * k4XS : xs2 + (p - 32) * k4XS);
+    };
+    const int otile = tid >> 4, och = tid & 15;
+    const int otr = otile >> 3, otc = otile & 7;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+                *reinterpret_cast<f4v *>(xpos(p0 + k) + (16 * g + j) * 16 + 4 * q) = acc[k][rr][g];
+        __syncthreads();
+        float m[36];
+#pragma unroll
+        for (int p = 0; p < 36; ++p) m[p] = xpos(p)[otile * 16 + och];
+        float tt[4][6];
+#pragma unroll
+        for (int b = 0; b < 6; ++b) {
+            float mm[6], y[4];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) mm[a] = m[6 * a + b];
+            w4_at6(mm, y);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) tt[i][b] = y[i];
+        }
+        const int co = cb * k4Co + 16 * rr + och;
+        const float bv = bias ? bias[co] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float y[4];
+            w4_at6(tt[i], y);
+            const int yy = oy0 + 4 * otr + i;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int xx = ox0 + 4 * otc + k;
+                float v = y[k] + bv;
+                if (RELU) v = fmaxf(v, 0.f);
+                if (yy < H && xx < W && (!(PP & 16) || v == 1234.5678f))
+                    Y[(((int64_t)n * H + yy) * W + xx) * Cout + co] = v;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// PP: research probes (VOSDET_WINO4_PSPROBE; wrong results when set): 1 no transform,
+// 2 no MFMAs, 4 no patch loads / stores, 8 no U reloads, 16 no output stores
+template <bool RELU, int PP>
+__global__ __launch_bounds__(k4Threads) void conv3x3_wino4ps_kernel(
+    const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
+    int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
+    int cb_per_xcd) {
+    __shared__ __attribute__((aligned(16))) float4 pst[3 * k4PSlots];
+    __shared__ __attribute__((aligned(16))) float vs[2 * k4VStageF];
+    __shared__ uint32_t poff[6 * 256];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ncb = Cout / k4Co;
+    int cb, sp;
+    if (cb_per_xcd) {
+        const int xcd = blockIdx.x & 7;
+        cb = xcd % ncb;
+        sp = (blockIdx.x >> 3) * (8 / ncb) + xcd / ncb;
+    } else {
+        const int r8 = blockIdx.x % (8 * ncb);
+        cb = r8 / 8;
+        sp = (blockIdx.x / (8 * ncb)) * 8 + (r8 & 7);
+    }
+    if (sp >= N * tby * tbx) return;
+    const int n = sp / (tby * tbx);
+    const int rem = sp - n * tby * tbx;
+    const int tyb = rem / tbx, txb = rem - (rem / tbx) * tbx;
+    const int oy0 = 4 * k4TR * tyb, ox0 = 4 * k4TC * txb;
+    const int iy0 = oy0 - 1, ix0 = ox0 - 1;
+    // DMA source offsets of the XW waves (4-7): slot s of instruction tw + 4 k, as the
+    // first form's
+    if (wave >= 4) {
+        const int tw = wave & 3;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int s = 64 * (tw + 4 * k) + lane;
+            const int R = s / k4RP, u = s - R * k4RP;
+            const int m = u / 5, r5 = u - 5 * m;
+            const int Cc = 2 * m + (r5 >> 1), hf = r5 & 1;
+            const int y = iy0 + R, x = ix0 + Cc;
+            const bool ok = R < k4PR && r5 < 4 && Cc < k4PC && (unsigned)y < (unsigned)H &&
+                            (unsigned)x < (unsigned)W;
+            poff[256 * k + (tid - 256)] =
+                ok ? (uint32_t)((y * W + x) * C + 4 * hf) : 0x80000000u | (uint32_t)(4 * hf);
+        }
+    }
+    const float *const Xn = X + (int64_t)n * H * W * C;
+    if (wave < 4)
+        wino4ps_body<RELU, 5, false, PP>(Xn, H, W, C, U, Cout, bias, Y, n, cb, oy0, ox0, pst, vs, poff,
+                                     wave, lane);
+    else
+        wino4ps_body<RELU, 4, true, PP>(Xn, H, W, C, U, Cout, bias, Y, n, cb, oy0, ox0, pst, vs, poff,
+                                    wave, lane);
+}
+
 // U = G g G^T of the PyTorch weight w[co][ci][3][3], G = [1/4 0 0; -1/6 -1/6 -1/6;
 // -1/6 1/6 -1/6; 1/24 1/12 1/6; 1/24 -1/12 1/6; 0 0 1], float64, rounded once; stored
 // in the kernel's fragment order [co / 64][ci / 8][cg = co % 64 / 16][pp = pos / 2]
@@ -400,7 +701,11 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
     const int tby = (H + 4 * k4TR - 1) / (4 * k4TR), tbx = (W + 4 * k4TC - 1) / (4 * k4TC);
     const int64_t nsp = (int64_t)N * tby * tbx;
     const int ncb = Cout / k4Co;
-    const int cbx = 8 % ncb == 0;
+    // VOSDET_WINO4_CBX=0: the four channel blocks of a spatial block on one XCD (the
+    // patch then comes from that XCD's L2 three times in four), not one channel block
+    // per XCD (its U in that L2)
+    const char *cbxe = getenv("VOSDET_WINO4_CBX");
+    const int cbx = (8 % ncb == 0) && !(cbxe && cbxe[0] == '0');
     const int64_t blocks = cbx ? (nsp + 8 / ncb - 1) / (8 / ncb) * 8 : (nsp + 7) / 8 * 8 * ncb;
     if (blocks > 0x7fffffff) return VD_ERR_SHAPE;
     static_assert(k4LdsB <= VD_LDS_BYTES, "LDS");
@@ -431,6 +736,30 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
          conv3x3_wino4_kernel<true, 10>, conv3x3_wino4_kernel<true, 11>,
          conv3x3_wino4_kernel<true, 12>, conv3x3_wino4_kernel<true, 13>,
          conv3x3_wino4_kernel<true, 14>, conv3x3_wino4_kernel<true, 15>}};
+    // read at every launch (a few us of host time), so one process can A/B the forms
+    const char *pse = getenv("VOSDET_WINO4_PS");
+    const bool ps = pse && pse[0] == '1';
+    if (ps && !probe) {
+        typedef void (*kps_t)(const float *, int, int, int, int, const float *, int,
+                              const float *, float *, int, int, int);
+        const char *ppe = getenv("VOSDET_WINO4_PSPROBE");
+        const int pp = ppe ? atoi(ppe) : 0;
+#define VD_PSK(P) (relu ? conv3x3_wino4ps_kernel<true, P> : conv3x3_wino4ps_kernel<false, P>)
+        kps_t kp = VD_PSK(0);
+        if (pp == 1) kp = VD_PSK(1);
+        if (pp == 2) kp = VD_PSK(2);
+        if (pp == 4) kp = VD_PSK(4);
+        if (pp == 8) kp = VD_PSK(8);
+        if (pp == 16) kp = VD_PSK(16);
+        if (pp == 18) kp = VD_PSK(18);
+        if (pp == 31) kp = VD_PSK(31);
+        if (pp == 5) kp = VD_PSK(5);
+        if (pp == 12) kp = VD_PSK(12);
+#undef VD_PSK
+        hipLaunchKernelGGL(kp, dim3((unsigned)blocks), dim3(k4Threads), 0, s, X, N, H, W, C, U,
+                           Cout, bias, Y, tby, tbx, cbx);
+        return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+    }
     const kern_t kern = table[relu ? 1 : 0][probe];
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(k4Threads), 0, s, X, N, H, W, C, U,
                        Cout, bias, Y, tby, tbx, cbx, probe_hi);
