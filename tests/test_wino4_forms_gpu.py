@@ -1,5 +1,6 @@
 """Winograd F(4x4,3x3), position-split form (csrc/conv3x3_wino4.hip,
-VOSDET_WINO4_PS=1) vs the first form: the same MFMA operands in the same order and
+VOSDET_WINO4_PS=1) and the hand-counted-vmcnt form (VOSDET_WINO4_ACC=1) vs the first
+form: the same MFMA operands in the same order and
 the same output transform, so the outputs must be bit-identical -- on the step's
 shapes (incl. ragged blocks: H, W not multiples of 16 / 32), with and without bias
 and ReLU -- and within 5e-5 of torch fp32 (the F(4x4) tolerance)."""
@@ -12,26 +13,35 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 
-def _run(x, u, b, relu, ps):
+FORMS = {"first": {"VOSDET_WINO4_PS": "0", "VOSDET_WINO4_ACC": "0", "VOSDET_WINO4_VD": "1"},
+         "ps": {"VOSDET_WINO4_PS": "1", "VOSDET_WINO4_ACC": "0", "VOSDET_WINO4_VD": "1"},
+         "acc": {"VOSDET_WINO4_PS": "0", "VOSDET_WINO4_ACC": "1", "VOSDET_WINO4_VD": "1"},
+         "acc3": {"VOSDET_WINO4_PS": "0", "VOSDET_WINO4_ACC": "1", "VOSDET_WINO4_VD": "3"}}
+
+
+def _run(x, u, b, relu, form):
     from vosdetectron_amd import ops
-    old = os.environ.get("VOSDET_WINO4_PS")
-    os.environ["VOSDET_WINO4_PS"] = "1" if ps else "0"
+    env = FORMS[form]
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         y = ops.conv3x3_wino4_bias_act(x, u, b, relu=relu)
         torch.cuda.synchronize()
         return y
     finally:
-        if old is None:
-            del os.environ["VOSDET_WINO4_PS"]
-        else:
-            os.environ["VOSDET_WINO4_PS"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
 @pytest.mark.parametrize("N,C,H,W,Co", [(2, 64, 20, 36, 64), (1, 256, 50, 84, 256),
                                         (3, 128, 17, 45, 128), (2, 512, 25, 42, 512),
                                         (1, 8, 9, 9, 64), (4, 24, 33, 31, 128)])
 @pytest.mark.parametrize("bias", [True, False])
-def test_wino4ps_bit_identical_to_first_form(N, C, H, W, Co, bias):
+@pytest.mark.parametrize("form", ["ps", "acc", "acc3"])
+def test_wino4_forms_bit_identical_to_first_form(N, C, H, W, Co, bias, form):
     from vosdetectron_amd import ops
     g = torch.Generator(device="cuda").manual_seed(N * 1000 + C + H)
     x = torch.randn(N, C, H, W, device="cuda", generator=g).contiguous(
@@ -39,8 +49,8 @@ def test_wino4ps_bit_identical_to_first_form(N, C, H, W, Co, bias):
     w = torch.randn(Co, C, 3, 3, device="cuda", generator=g) / (3. * C ** .5)
     b = torch.randn(Co, device="cuda", generator=g) if bias else None
     u = ops.conv3x3_wino4_weight(w)
-    y1 = _run(x, u, b, bias, False)
-    y2 = _run(x, u, b, bias, True)
+    y1 = _run(x, u, b, bias, "first")
+    y2 = _run(x, u, b, bias, form)
     assert torch.equal(y1, y2), float((y1 - y2).abs().max())
     ref = F.conv2d(x, w, b, padding=1)
     if bias:
@@ -49,7 +59,8 @@ def test_wino4ps_bit_identical_to_first_form(N, C, H, W, Co, bias):
     assert err <= 5e-5 * max(1., float(ref.abs().max())), err
 
 
-def test_wino4ps_benched_p2():
+@pytest.mark.parametrize("form", ["ps", "acc", "acc3"])
+def test_wino4_forms_benched_p2(form):
     from vosdetectron_amd import ops
     g = torch.Generator(device="cuda").manual_seed(7)
     x = torch.randn(32, 256, 200, 336, device="cuda", generator=g).contiguous(
@@ -57,6 +68,6 @@ def test_wino4ps_benched_p2():
     w = torch.randn(256, 256, 3, 3, device="cuda", generator=g) / 48.
     b = torch.randn(256, device="cuda", generator=g)
     u = ops.conv3x3_wino4_weight(w)
-    y1 = _run(x, u, b, False, False)
-    y2 = _run(x, u, b, False, True)
+    y1 = _run(x, u, b, False, "first")
+    y2 = _run(x, u, b, False, form)
     assert torch.equal(y1, y2), float((y1 - y2).abs().max())

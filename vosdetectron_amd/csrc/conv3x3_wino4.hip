@@ -30,6 +30,15 @@
 // (1 KiB each); per transforming lane: 36 ds_read_b32 (patch), ~170 VALU, 36
 // ds_write_b32 (V).
 //
+// Default form (ACC, round 5): the U loads are inline asm with the loop's own vmcnt
+// accounting, so no U wait covers a patch DMA piece (the compiler cannot see the asm
+// DMAs and, vmcnt retiring in issue order, its own waits did from the fourth position
+// of every chunk); the patch DMA is spread over all 8 waves (3 pieces each); V is
+// stored [pos][tg][ch / 2][tile % 16][ch & 1] with an XOR swizzle, which makes the
+// MFMA waves' V reads conflict-free (the first form's were 4-way conflicted: 66 % of
+// its LDS-array cycles).  Bit-identical to the first form (VOSDET_WINO4_ACC=0); P2
+// 7.33 -> 7.16 ms, MFMA busy 0.61 -> 0.64 (profiles/r05/wino4acc/).
+//
 // LDS (120 KiB, one workgroup per CU):
 //   V [2][36 pos][32 tiles][8 ch] fp32 (36 KiB a stage): a wave's B fragment of a
 //     position is one conflict-free ds_read_b64 (lane (j, q) -> tile 16 tg + j,
@@ -77,6 +86,26 @@ __device__ __forceinline__ void w4_dma_1k(const float *src, uint32_t lds) {
         : "memory");
 }
 
+// ACC form: the U fragments through inline-asm buffer loads with the loop's own vmcnt
+// accounting.  The compiler cannot see the (inline-asm) patch DMAs, so its own waits
+// for compiler-issued U loads undercount the queue by the DMA pieces and, vmcnt
+// retiring in issue order, from the fourth position of a chunk every U wait also waits
+// for the patch's HBM fetch.  Counted by hand, a DMA is waited for only at the chunk's
+// end barrier.
+typedef int w4i4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void w4_uload_asm(f4v &r, w4i4 rsrc, uint32_t voff, uint32_t soff) {
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen"
+                 : "+v"(r)
+                 : "v"(voff), "s"(rsrc), "s"(soff)
+                 : "memory");
+}
+// all but the N youngest vector-memory ops of this wave retired; the fragment passes
+// through so its MFMAs cannot be scheduled above the wait
+template <int N>
+__device__ __forceinline__ void w4_wait_u(f4v &a) {
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(a) : "n"(N) : "memory");
+}
+
 // y = B^T x, B^T = [4 0 -5 0 1 0; 0 -4 -4 1 1 0; 0 4 -4 -1 1 0; 0 -2 -1 2 1 0;
 //                   0 2 -1 -2 1 0; 0 4 0 -5 0 1]
 __device__ __forceinline__ void w4_bt6(const float (&x)[6], float (&y)[6]) {
@@ -100,8 +129,11 @@ __device__ __forceinline__ void w4_at6(const float (&m)[6], float (&y)[4]) {
 }
 
 // PROBE (research timing only, VOSDET_WINO4_PROBE; results are wrong when set): bit 0
-// no transform, bit 1 no MFMA, bit 2 no patch DMA, bit 3 no U reloads
-template <bool RELU, int PROBE>
+// no transform, bit 1 no MFMA, bit 2 no patch DMA, bit 3 no U reloads.
+// ACC: U loads and their waits counted by hand (w4_uload_asm), the patch DMA spread over
+// all 8 waves (3 pieces each, a zero-page piece where no chunk is left) so every wave's
+// queue has the same shape
+template <bool RELU, int PROBE, bool ACC = false, int VD = 1>
 __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
@@ -141,28 +173,32 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     const float *const Xn = X + (int64_t)n * H * W * C;
     // kept in LDS (after the patch stages), not in six registers the MFMA phase needs
     uint32_t *const poff = reinterpret_cast<uint32_t *>(pst + 2 * k4PStageB) + tid;
+    constexpr int kDW = ACC ? 8 : 4;  // waves issuing the patch DMA
+    constexpr int kDK = 24 / kDW;     // its wave instructions per issuing wave
+    constexpr int kPS = ACC ? 512 : 256;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        if (wave >= 4) break;
-        const int s = 64 * (wave + 4 * k) + lane;
+    for (int k = 0; k < kDK; ++k) {
+        if (!ACC && wave >= 4) break;
+        const int s = 64 * (wave + kDW * k) + lane;
         const int R = s / k4RP, u = s - R * k4RP;
         const int m = u / 5, r5 = u - 5 * m;
         const int Cc = 2 * m + (r5 >> 1), hf = r5 & 1;
         const int y = iy0 + R, x = ix0 + Cc;
         const bool ok = R < k4PR && r5 < 4 && Cc < k4PC && (unsigned)y < (unsigned)H &&
                         (unsigned)x < (unsigned)W;
-        poff[256 * k] = ok ? (uint32_t)((y * W + x) * C + 4 * hf) : 0x80000000u | (uint32_t)(4 * hf);
+        poff[kPS * k] = ok ? (uint32_t)((y * W + x) * C + 4 * hf) : 0x80000000u | (uint32_t)(4 * hf);
     }
     const float *const zero = reinterpret_cast<const float *>(g_wino4_zero);
-    auto dma = [&](int ch, int stage) {
-        uint32_t oo[6];  // all six offsets read before the first DMA (one LDS round trip)
+    auto dma = [&](int ch, int stage) {  // ch < 0 (ACC): zero-page pieces, queue shape only
+        uint32_t oo[kDK];  // all offsets read before the first DMA (one LDS round trip)
 #pragma unroll
-        for (int k = 0; k < 6; ++k) oo[k] = poff[256 * k];
+        for (int k = 0; k < kDK; ++k) oo[k] = poff[kPS * k];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
+        for (int k = 0; k < kDK; ++k) {
             const uint32_t o = oo[k];
             const float *src = (o & 0x80000000u) ? zero + (o & 7u) : Xn + o + ch * k4KC;
-            w4_dma_1k(src, pbase + (uint32_t)(stage * k4PStageB + (wave + 4 * k) * 1024));
+            if (ACC && ch < 0) src = zero;
+            w4_dma_1k(src, pbase + (uint32_t)(stage * k4PStageB + (wave + kDW * k) * 1024));
         }
     };
 
@@ -173,7 +209,15 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     const float *const tread =
         reinterpret_cast<const float *>(pst) + ((4 * wave) * k4RP + 10 * ttc + (tci >> 2)) * 4 +
         (tci & 3);
-    float *const twrite = vst + 64 * wave + lane;
+    // V[pos][tile][ch] (first form), or (ACC) V[pos][tg][q = ch / 2][j = tile % 16][ch & 1]
+    // with the 32-dword row XOR-swizzled by 8 q: the MFMA waves' ds_read2st64_b64 (16-lane
+    // groups, bank = dword mod 32) and the transform's ds_write_b32 (32-lane groups) are
+    // both conflict-free -- the first form's reads are 4-way conflicted (PMC: 66 % of
+    // the LDS-array cycles were conflict cycles)
+    const int wtile_j = 8 * (wave & 1) + ttc;
+    float *const twrite =
+        ACC ? vst + (wave >> 1) * 128 + 32 * (tci >> 1) + ((2 * wtile_j + (tci & 1)) ^ (8 * (tci >> 1)))
+            : vst + 64 * wave + lane;
     auto transform = [&](int stage) {
         const float *tp = tread + stage * (k4PStageB / 4);
         float t[6][6];  // B^T d: column c's 6 values
@@ -202,7 +246,8 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     // conv3x3_wino4_weight_kernel)
     const int tg = wave >> 2, cg = wave & 3;
     const int j = lane & 15, q = lane >> 4;
-    const f2v *const vread = reinterpret_cast<const f2v *>(vst + (16 * tg + j) * 8 + 2 * q);
+    const f2v *const vread = reinterpret_cast<const f2v *>(
+        ACC ? vst + 128 * tg + 32 * q + ((2 * j) ^ (8 * q)) : vst + (16 * tg + j) * 8 + 2 * q);
     // U through a buffer resource: wave-uniform base and per-position offsets in scalar
     // registers, one VGPR (the lane's 16 B) for all loads
     const __amdgpu_buffer_rsrc_t urs = __builtin_amdgcn_make_buffer_rsrc(
@@ -214,6 +259,16 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
         return __builtin_bit_cast(
             f4v, __builtin_amdgcn_raw_buffer_load_b128(urs, uvoff,
                                                        (ch * 4 * 18 + pos) * 1024, 0));
+    };
+    // the same resource as four SGPR words for the inline-asm loads (ACC)
+    const uintptr_t uaddr = (uintptr_t)(U + (int64_t)__builtin_amdgcn_readfirstlane(
+                                                (cb * nch * 4 + cg) * (18 * 64)) * 4);
+    const w4i4 ursv = {__builtin_amdgcn_readfirstlane((int)(uint32_t)uaddr),
+                       __builtin_amdgcn_readfirstlane((int)(uint32_t)(uaddr >> 32) & 0xffff),
+                       __builtin_amdgcn_readfirstlane(nch * 4 * 18 * 64 * 16), 0x00020000};
+    auto uload_acc = [&](f4v &r, int ch, int pos) {
+        w4_uload_asm(r, ursv, (uint32_t)uvoff,
+                     (uint32_t)__builtin_amdgcn_readfirstlane((ch * 4 * 18 + pos) * 1024));
     };
     f4v acc[36];
 #pragma unroll
@@ -234,13 +289,29 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     auto mfma_chunk = [&](bool xon, int stage, int ch, int chn, int tstage) {
         const f2v *vp = vread + stage * (k4VStageB / 8);
         if (xon) transform(tstage);
-        f2v b0 = vp[0], b1 = vp[128];
+        // V of positions pp .. pp + VD - 1 in a ring (VD > 1: more LDS latency hidden
+        // behind one wave's own MFMAs while its SIMD partner transforms)
+        f2v vq[VD][2];
+#pragma unroll
+        for (int d = 0; d < VD; ++d) {
+            vq[d][0] = vp[(2 * d) * 128];
+            vq[d][1] = vp[(2 * d + 1) * 128];
+        }
+        f2v b0 = vq[0][0], b1 = vq[0][1];
 #pragma unroll
         for (int pp = 0; pp < 18; ++pp) {
             f2v n0, n1;
-            if (pp < 17) {
-                n0 = vp[(2 * pp + 2) * 128];
-                n1 = vp[(2 * pp + 3) * 128];
+            if (pp + VD < 18) {
+                n0 = vp[(2 * (pp + VD)) * 128];
+                n1 = vp[(2 * (pp + VD) + 1) * 128];
+            }
+            if constexpr (ACC) {
+                // younger than U(ch, pp <= 8) (issued last chunk): its 8 - pp successors,
+                // the 3 DMA pieces, this chunk's pp reloads; U(ch, pp >= 9): 8 reloads
+                if (pp < kUR)
+                    w4_wait_u<kUR - 1 + kDK>(u[pp % kUR]);
+                else
+                    w4_wait_u<kUR - 1>(u[pp % kUR]);
             }
             const f4v uf = u[pp % kUR];
             if constexpr (!(PROBE & 2)) {
@@ -253,21 +324,52 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
             } else {
                 acc[2 * pp][0] += b0.x + b1.y;
             }
-            if constexpr (!(PROBE & 8)) {
+            if constexpr (ACC) {
+                if (pp + kUR < 18)
+                    uload_acc(u[pp % kUR], ch, pp + kUR);
+                else
+                    uload_acc(u[pp % kUR], chn, pp + kUR - 18);
+            } else if constexpr (!(PROBE & 8)) {
                 if (pp + kUR < 18)
                     u[pp % kUR] = uload(ch, pp + kUR);
                 else
                     u[pp % kUR] = uload(chn, pp + kUR - 18);
             }
             __builtin_amdgcn_sched_barrier(0);
+            if (pp + VD < 18) {
+                vq[pp % VD][0] = n0;
+                vq[pp % VD][1] = n1;
+            }
             if (pp < 17) {
-                b0 = n0;
-                b1 = n1;
+                b0 = vq[(pp + 1) % VD][0];
+                b1 = vq[(pp + 1) % VD][1];
             }
         }
     };
 
     // ---- pipeline: prologue (chunk 0 transformed, chunk 1's patch landed)
+    if constexpr (ACC) {
+#pragma unroll
+        for (int i = 0; i < kUR; ++i) {
+            u[i] = f4v{0.f, 0.f, 0.f, 0.f};
+            uload_acc(u[i], 0, i);
+        }
+        dma(0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (wave < 4) transform(0);
+        dma(nch > 1 ? 1 : -1, 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int ch = 0; ch < nch; ++ch) {
+            const int sv = ch & 1;
+            const int chn = ch + 1 < nch ? ch + 1 : ch;
+            dma(ch + 2 < nch ? ch + 2 : -1, sv);  // every wave, every chunk: 3 pieces
+            mfma_chunk(wave < 4 && ch + 1 < nch, sv, ch, chn, sv ^ 1);
+            asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+            __syncthreads();
+        }
+    } else {
 #pragma unroll
     for (int i = 0; i < kUR; ++i) u[i] = uload(0, i);
     if (wave < 4) dma(0, 0);
@@ -288,6 +390,7 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
         // phase) landed; the next chunk's 9 U loads may stay in flight
         asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
         __syncthreads();
+    }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
@@ -760,7 +863,19 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
                            Cout, bias, Y, tby, tbx, cbx);
         return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
     }
-    const kern_t kern = table[relu ? 1 : 0][probe];
+    // the ACC form (hand-counted vmcnt, conflict-free V layout) is the default;
+    // VOSDET_WINO4_ACC=0 selects the first form (bit-identical, 2-6 % slower)
+    const char *acce = getenv("VOSDET_WINO4_ACC");
+    const bool acc = !(acce && acce[0] == '0');
+    // VOSDET_WINO4_VD (ACC form): V fragments read 1-3 positions ahead
+    const char *vde = getenv("VOSDET_WINO4_VD");
+    const int vd = vde ? atoi(vde) : 1;
+    kern_t kacc = relu ? conv3x3_wino4_kernel<true, 0, true, 1> : conv3x3_wino4_kernel<false, 0, true, 1>;
+    if (vd == 2)
+        kacc = relu ? conv3x3_wino4_kernel<true, 0, true, 2> : conv3x3_wino4_kernel<false, 0, true, 2>;
+    if (vd == 3)
+        kacc = relu ? conv3x3_wino4_kernel<true, 0, true, 3> : conv3x3_wino4_kernel<false, 0, true, 3>;
+    const kern_t kern = (acc && !probe) ? kacc : table[relu ? 1 : 0][probe];
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(k4Threads), 0, s, X, N, H, W, C, U,
                        Cout, bias, Y, tby, tbx, cbx, probe_hi);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
