@@ -192,6 +192,13 @@ int vd_conv3x3_wino_bias_act(const float *X, int N, int H, int W, int C, const f
 int vd_conv3x3_wino4_weight(const float *w, int Cout, int Cin, float *U, void *stream);
 int vd_conv3x3_wino4_bias_act(const float *X, int N, int H, int W, int C, const float *U,
                               int Cout, const float *bias, int relu, float *Y, void *stream);
+/* The same over N small maps (H, W <= 15: the mask head's 14 x 14 RoI features,
+ * mask_rcnn_heads.py:178-188), two maps per 16 x 32 output block, each padded by its
+ * own zeros: bit-identical to vd_conv3x3_wino4_bias_act, which gives every map a
+ * block of its own.  VD_ERR_SHAPE for larger maps. */
+int vd_conv3x3_wino4_mosaic_bias_act(const float *X, int N, int H, int W, int C, const float *U,
+                                     int Cout, const float *bias, int relu, float *Y,
+                                     void *stream);
 
 /* The Winograd convolution of R images of seg_h x W pixels stored back to back
  * (R x seg_h x W x C, i.e. one H = R * seg_h image), each padded by its own zeros:

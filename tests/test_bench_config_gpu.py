@@ -54,7 +54,8 @@ def test_bench_batch_routes(bench_setup):
     """The benched shapes take the hand-written routes (not a silent fallback):
     every 3x3 conv of the benched step ran on a Winograd kernel -- res2 / res3
     / res4 / res5 conv2 (stride-1 blocks), FPN posthoc P2-P4 and the RPN conv on
-    P2-P4 on F(4x4); P5 / P6 and the mask head's four convs on F(2x2) mosaics."""
+    P2-P4 on F(4x4); the mask head's four convs on F(4x4) two maps per block; P5 /
+    P6 on F(2x2) mosaics."""
     from vosdetectron_amd import modeling
     cfg, sd, pipe, frames, out, routes = bench_setup
     p2 = out["feats"][-1]
@@ -64,13 +65,15 @@ def test_bench_batch_routes(bench_setup):
     assert modeling.conv3x3_route(BATCH, 256, 256, 200, 336) == ("wino4", None)
     assert modeling.conv3x3_route(BATCH, 256, 256, 100, 168) == ("wino4", None)
     assert modeling.conv3x3_route(BATCH, 256, 256, 25, 42) == ("wino", "2d")
-    assert modeling.conv3x3_route(BATCH * 100, 256, 256, 14, 14) == ("wino", "2d")
+    assert modeling.conv3x3_route(BATCH * 100, 256, 256, 14, 14) == ("wino4", "pair")
+    assert modeling.conv3x3_route(8000, 512, 512, 7, 7) == ("wino", "2d")  # C4 res5 head
     assert routes.get("igemm", 0) == 0 and routes.get("miopen", 0) == 0, routes
     n_wino = routes.get("wino", 0) + routes.get("wino_rows", 0) + routes.get("wino_2d", 0)
-    # F(4x4): FPN posthoc + RPN conv on P2-P4 (6) and the body's stride-1 conv2s;
-    # F(2x2): posthoc P5 + RPN P5 / P6 + the mask head's four convs at least
+    # F(4x4): FPN posthoc + RPN conv on P2-P4 (6) and the body's stride-1 conv2s, the
+    # mask head's four convs as map pairs; F(2x2): posthoc P5 + RPN P5 / P6 at least
     assert routes.get("wino4", 0) >= 6 + 3 + 3 + 5 + 2, routes
-    assert n_wino >= 7 and routes.get("wino_2d", 0) >= 7, routes
+    assert routes.get("wino4_pair", 0) == 4, routes
+    assert n_wino >= 3 and routes.get("wino_2d", 0) >= 3, routes
     # the P2 top-down lateral step as one fused MFMA launch (modeling._fpn_lateral_fused_k)
     assert routes.get("fpn_lateral", 0) == 1, routes
 
@@ -98,7 +101,7 @@ def test_bench_batch_e2e_vs_cpu(bench_setup, f):
 def test_conv3x3_wino_benched_shapes(N, C, H, W, bias):
     """The Winograd kernel the step runs at the benched sizes, in the route and
     layout the engine picks (modeling.conv3x3_route: F(4x4) for P2 / P3 / P4, res2
-    and res5; the F(2x2) 2-D mosaic for the mask head's 3200 RoI maps) vs torch
+    and res5, two maps per block for the mask head's 3200 RoI maps) vs torch
     fp32 at 2e-5 (F(2x2)) / 5e-5 (F(4x4): its transforms scale by up to 8 and 5)
     of the output range."""
     from vosdetectron_amd import modeling, ops
@@ -110,7 +113,8 @@ def test_conv3x3_wino_benched_shapes(N, C, H, W, bias):
     w = torch.randn(C, C, 3, 3, device="cuda", generator=g) / (3. * C ** .5)
     b = torch.randn(C, device="cuda", generator=g) if bias else None
     if algo == "wino4":
-        got = ops.conv3x3_wino4_bias_act(x, ops.conv3x3_wino4_weight(w), b, relu=bias)
+        got = ops.conv3x3_wino4_bias_act(x, ops.conv3x3_wino4_weight(w), b, relu=bias,
+                                         mosaic=mos == "pair")
     else:
         got = ops.conv3x3_wino_bias_act(x, ops.conv3x3_wino_weight(w), b, relu=bias,
                                         mosaic=mos)

@@ -111,9 +111,14 @@ def test_winograd4_route_gate():
     for args in [(32, 256, 256, 200, 336), (32, 256, 256, 100, 168), (32, 256, 256, 50, 84),
                  (32, 64, 64, 200, 336), (32, 128, 128, 100, 168), (32, 512, 512, 25, 42)]:
         assert r(*args) == ("wino4", None), args
-    for args in [(32, 256, 256, 25, 42), (32, 256, 256, 13, 21), (3200, 256, 256, 14, 14),
-                 (1, 256, 256, 200, 336), (32, 256, 96, 200, 336)]:
+    for args in [(32, 256, 256, 25, 42), (32, 256, 256, 13, 21), (8000, 512, 512, 7, 7),
+                 (1, 256, 256, 200, 336), (32, 256, 96, 200, 336), (100, 256, 256, 14, 14)]:
         assert r(*args)[0] != "wino4", args
+    # the mask head's RoI maps: F(4x4) two per block (>= 1024 workgroups, maps >= half
+    # a 16 x 16 cell); VOSDET_WINO4_MOSAIC=0 keeps the F(2x2) 2-D mosaic
+    assert r(3200, 256, 256, 14, 14) == ("wino4", "pair")
+    assert r(1600, 256, 256, 14, 14) == ("wino4", "pair")
+    assert r(3200, 256, 256, 14, 14, mosaic=False)[0] != "wino4"
     assert abs(modeling._wino4_block_use(25, 42) - 1050 / 2048) < 1e-12
     old = os.environ.get("VOSDET_WINO4")
     try:

@@ -71,3 +71,33 @@ def test_wino4_forms_benched_p2(form):
     y1 = _run(x, u, b, False, "first")
     y2 = _run(x, u, b, False, form)
     assert torch.equal(y1, y2), float((y1 - y2).abs().max())
+
+
+@pytest.mark.parametrize("N,C,H,W,Co", [(7, 256, 14, 14, 256), (4, 64, 15, 13, 128),
+                                        (2, 8, 1, 1, 64), (1, 24, 9, 15, 64),
+                                        (3200, 256, 14, 14, 256)])
+def test_wino4_pair_mosaic_bit_identical(N, C, H, W, Co):
+    """vd_conv3x3_wino4_mosaic_bias_act (two maps per block) == one map per block,
+    and within the F(4x4) tolerance of torch; odd N leaves the last pair half empty."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(N + C + H * W)
+    x = torch.randn(N, C, H, W, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    w = torch.randn(Co, C, 3, 3, device="cuda", generator=g) / (3. * C ** .5)
+    b = torch.randn(Co, device="cuda", generator=g)
+    u = ops.conv3x3_wino4_weight(w)
+    y1 = ops.conv3x3_wino4_bias_act(x, u, b, relu=True)
+    y2 = ops.conv3x3_wino4_bias_act(x, u, b, relu=True, mosaic=True)
+    torch.cuda.synchronize()
+    assert y2 is not None
+    assert torch.equal(y1, y2), float((y1 - y2).abs().max())
+    ref = F.relu(F.conv2d(x[:64], w, b, padding=1))
+    err = float((y2[:64] - ref).abs().max())
+    assert err <= 5e-5 * max(1., float(ref.abs().max())), err
+
+
+def test_wino4_pair_mosaic_refuses_large_maps():
+    from vosdetectron_amd import ops
+    x = torch.zeros(2, 64, 16, 14, device="cuda").contiguous(memory_format=torch.channels_last)
+    u = ops.conv3x3_wino4_weight(torch.zeros(64, 64, 3, 3, device="cuda"))
+    assert ops.conv3x3_wino4_bias_act(x, u, None, mosaic=True) is None

@@ -137,7 +137,7 @@ template <bool RELU, int PROBE, bool ACC = false, int VD = 1>
 __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
-    int cb_per_xcd, int probe_hi) {
+    int cb_per_xcd, int probe_hi, int mos) {
     // static, not dynamic: a > 64 KiB dynamic allocation is honoured by a direct launch
     // after hipFuncSetAttribute but not by the same launch captured into a hipGraph
     // (every replayed P2 conv came out unwritten, round 5)
@@ -157,9 +157,13 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
         cb = r8 / 8;
         sp = (blockIdx.x / (8 * ncb)) * 8 + (r8 & 7);
     }
-    if (sp >= N * tby * tbx) return;
-    const int n = sp / (tby * tbx);
-    const int rem = sp - n * tby * tbx;
+    // mos: map-pair mosaic (H, W <= 15, vd_conv3x3_wino4_mosaic_bias_act) -- block sp
+    // holds maps 2 sp (columns 0..15) and 2 sp + 1 (columns 16..31), each at the
+    // origin of its 16 x 16 cell; taps outside a map read zero, so every output is
+    // the map's own padded convolution, bit-identical to one map per block
+    if (sp >= (mos ? (N + 1) >> 1 : N * tby * tbx)) return;
+    const int n = mos ? 2 * sp : sp / (tby * tbx);
+    const int rem = mos ? 0 : sp - n * tby * tbx;
     const int tyb = rem / tbx, txb = rem - (rem / tbx) * tbx;
     const int oy0 = 4 * k4TR * tyb, ox0 = 4 * k4TC * txb;
     const int iy0 = oy0 - 1, ix0 = ox0 - 1;
@@ -184,9 +188,12 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
         const int m = u / 5, r5 = u - 5 * m;
         const int Cc = 2 * m + (r5 >> 1), hf = r5 & 1;
         const int y = iy0 + R, x = ix0 + Cc;
+        // mosaic: cell x >> 4 (map n + cell), column x & 15 of that map
+        const int cell = mos ? (x >> 4) : 0, xm = mos ? (x & 15) : x;
         const bool ok = R < k4PR && r5 < 4 && Cc < k4PC && (unsigned)y < (unsigned)H &&
-                        (unsigned)x < (unsigned)W;
-        poff[kPS * k] = ok ? (uint32_t)((y * W + x) * C + 4 * hf) : 0x80000000u | (uint32_t)(4 * hf);
+                        x >= 0 && (unsigned)xm < (unsigned)W && n + cell < N;
+        poff[kPS * k] = ok ? (uint32_t)(((cell * H + y) * W + xm) * C + 4 * hf)
+                           : 0x80000000u | (uint32_t)(4 * hf);
     }
     const float *const zero = reinterpret_cast<const float *>(g_wino4_zero);
     auto dma = [&](int ch, int stage) {  // ch < 0 (ACC): zero-page pieces, queue shape only
@@ -354,11 +361,12 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
             u[i] = f4v{0.f, 0.f, 0.f, 0.f};
             uload_acc(u[i], 0, i);
         }
+        // chunks 0 and 1 fetched together: one HBM round trip in the prologue, not two
         dma(0, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        dma(nch > 1 ? 1 : -1, 1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDK) : "memory");  // U and chunk 0 landed
         __syncthreads();
         if (wave < 4) transform(0);
-        dma(nch > 1 ? 1 : -1, 1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         for (int ch = 0; ch < nch; ++ch) {
@@ -427,8 +435,9 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
         if (yy >= H) continue;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int xx = ox0 + 4 * tc + k;
-            if (xx >= W) continue;
+            const int xc = ox0 + 4 * tc + k;
+            const int ncell = mos ? n + (xc >> 4) : n, xx = mos ? (xc & 15) : xc;
+            if (xx >= W || ncell >= N) continue;
             float4 v = make_float4(o[4 * i + k][0] + bv.x, o[4 * i + k][1] + bv.y,
                                    o[4 * i + k][2] + bv.z, o[4 * i + k][3] + bv.w);
             if (RELU) {
@@ -440,7 +449,7 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
             // probe_hi bit 0 (research, VOSDET_WINO4_PROBE bit 4): no output stores (a
             // store the data never takes keeps the values live)
             if (!(probe_hi & 1) || v.x == 1234.5678f)
-                *reinterpret_cast<float4 *>(Y + (((int64_t)n * H + yy) * W + xx) * Cout + co) = v;
+                *reinterpret_cast<float4 *>(Y + (((int64_t)ncell * H + yy) * W + xx) * Cout + co) = v;
         }
     }
 }
@@ -796,13 +805,18 @@ int launch_conv3x3_wino4_weight(const float *w, int Cout, int C, float *U, hipSt
 }
 
 int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float *U, int Cout,
-                         const float *bias, int relu, float *Y, hipStream_t s) {
+                         const float *bias, int relu, float *Y, hipStream_t s, int mos) {
     if ((int64_t)N * H * W == 0) return VD_OK;
     if (!conv3x3_wino4_supported(C, Cout)) return VD_ERR_SHAPE;
     if ((int64_t)N * H * W * C >= ((int64_t)1 << 40) || (int64_t)H * W * C >= ((int64_t)1 << 31))
         return VD_ERR_SHAPE;
-    const int tby = (H + 4 * k4TR - 1) / (4 * k4TR), tbx = (W + 4 * k4TC - 1) / (4 * k4TC);
-    const int64_t nsp = (int64_t)N * tby * tbx;
+    // the map-pair mosaic: two maps of at most 15 x 15 per 16 x 32 block (the 16 x 16
+    // cell keeps a zero column / row after each map), 2 H W C floats of offsets < 2^31
+    if (mos && (H > 15 || W > 15 || (int64_t)2 * H * W * C >= ((int64_t)1 << 31)))
+        return VD_ERR_SHAPE;
+    const int tby = mos ? 1 : (H + 4 * k4TR - 1) / (4 * k4TR);
+    const int tbx = mos ? 1 : (W + 4 * k4TC - 1) / (4 * k4TC);
+    const int64_t nsp = mos ? ((int64_t)N + 1) / 2 : (int64_t)N * tby * tbx;
     const int ncb = Cout / k4Co;
     // VOSDET_WINO4_CBX=0: the four channel blocks of a spatial block on one XCD (the
     // patch then comes from that XCD's L2 three times in four), not one channel block
@@ -821,7 +835,7 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
         return e ? (atoi(e) >> 4) & 1 : 0;
     }();
     typedef void (*kern_t)(const float *, int, int, int, int, const float *, int, const float *,
-                           float *, int, int, int, int);
+                           float *, int, int, int, int, int);
     static const kern_t table[2][16] = {
         {conv3x3_wino4_kernel<false, 0>, conv3x3_wino4_kernel<false, 1>,
          conv3x3_wino4_kernel<false, 2>, conv3x3_wino4_kernel<false, 3>,
@@ -842,7 +856,7 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
     // read at every launch (a few us of host time), so one process can A/B the forms
     const char *pse = getenv("VOSDET_WINO4_PS");
     const bool ps = pse && pse[0] == '1';
-    if (ps && !probe) {
+    if (ps && !probe && !mos) {
         typedef void (*kps_t)(const float *, int, int, int, int, const float *, int,
                               const float *, float *, int, int, int);
         const char *ppe = getenv("VOSDET_WINO4_PSPROBE");
@@ -877,7 +891,7 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
         kacc = relu ? conv3x3_wino4_kernel<true, 0, true, 3> : conv3x3_wino4_kernel<false, 0, true, 3>;
     const kern_t kern = (acc && !probe) ? kacc : table[relu ? 1 : 0][probe];
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(k4Threads), 0, s, X, N, H, W, C, U,
-                       Cout, bias, Y, tby, tbx, cbx, probe_hi);
+                       Cout, bias, Y, tby, tbx, cbx, probe_hi, mos);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 

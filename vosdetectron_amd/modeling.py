@@ -114,7 +114,7 @@ def _pick_mosaic(N: int, H: int, W: int, allow=True):
 # F(2x2) on every 32-frame step shape with >= 4 workgroups per CU and blocks >= 50 %
 # real output (profiles/r05/wino4/ab_v3.jsonl: P2 7.41 vs 9.31 ms, P3 2.13 vs 2.61,
 # P4 0.65 vs 0.81, res2 0.63 vs 0.85, res5 0.79 vs 0.91); below that its coarse blocks
-# leave CUs idle.  No mosaic: the mask head's 14 x 14 RoI maps stay on F(2x2).
+# leave CUs idle.  The mask head's 14 x 14 RoI maps run two per block (_wino4_pair_ok).
 _WINO4_MIN_WGS = 1024
 _WINO4_MIN_BLOCK_USE = 0.5
 
@@ -136,6 +136,21 @@ def _wino4_ok(N: int, Cin: int, Cout: int, H: int, W: int) -> bool:
     return wgs >= _WINO4_MIN_WGS and _wino4_block_use(H, W) >= _WINO4_MIN_BLOCK_USE
 
 
+def _wino4_pair_ok(N: int, Cin: int, Cout: int, H: int, W: int) -> bool:
+    """F(4x4) over small maps two per 16 x 32 block (vd_conv3x3_wino4_mosaic_bias_act;
+    the mask head's 14 x 14 RoI maps: 77 % of each block real output; 2.43 vs 2.87 ms
+    per 3200-map conv for F(2x2) on its 2-D mosaic, profiles/r05/wino4_pair/).  Maps
+    under half a 16 x 16 cell (C4's 7 x 7 res5 head) stay on the F(2x2) mosaic.
+    VOSDET_WINO4_MOSAIC=0 turns it off."""
+    if os.environ.get("VOSDET_WINO4_MOSAIC", "1") == "0" or os.environ.get("VOSDET_WINO4", "1") == "0":
+        return False
+    if Cout % 64 or Cin % 8 or Cout == 0 or Cin == 0 or Cin > ops.WINO_MAX_CIN:
+        return False
+    if H > 15 or W > 15 or 2 * H * W * Cin >= (1 << 31) or H * W < 0.5 * 256:
+        return False
+    return -(-N // 2) * (Cout // 64) >= _WINO4_MIN_WGS
+
+
 def conv3x3_route(N: int, Cin: int, Cout: int, H: int, W: int, mosaic=True):
     """(algorithm, mosaic) the engine runs a 3x3 / stride-1 / pad-1 fp32 conv of an
     N x Cin x H x W channels_last batch with: ('wino4', None) -- Winograd F(4x4,3x3),
@@ -150,6 +165,8 @@ def conv3x3_route(N: int, Cin: int, Cout: int, H: int, W: int, mosaic=True):
             and Cin % 8 == 0 and Cout > 0 and Cin <= ops.WINO_MAX_CIN)
     if wino and _wino4_ok(N, Cin, Cout, H, W):
         return "wino4", None
+    if wino and mosaic and _wino4_pair_ok(N, Cin, Cout, H, W):
+        return "wino4", "pair"
     if wino and npx >= _WINO_MIN_PIXELS and use >= _WINO_MIN_BLOCK_USE:
         return "wino", mos
     if npx < _CONV3X3_MIN_PIXELS:
@@ -196,9 +213,9 @@ def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=True):
         if getattr(conv, "_vd_u4_key", None) != key:
             conv._vd_u4 = ops.conv3x3_wino4_weight(w.detach())
             conv._vd_u4_key = key
-        y = ops.conv3x3_wino4_bias_act(x, conv._vd_u4, b, relu=relu)
+        y = ops.conv3x3_wino4_bias_act(x, conv._vd_u4, b, relu=relu, mosaic=mos == "pair")
         if y is not None:
-            _count_route("wino4")
+            _count_route("wino4_pair" if mos == "pair" else "wino4")
             return y
         algo, mos = "wino", _pick_mosaic(x.shape[0], x.shape[2], x.shape[3], mosaic)[0]
     if algo == "wino":
