@@ -13,10 +13,13 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 
-FORMS = {"first": {"VOSDET_WINO4_PS": "0", "VOSDET_WINO4_ACC": "0", "VOSDET_WINO4_VD": "1"},
+FORMS = {"first": {"VOSDET_WINO4_PS": "0", "VOSDET_WINO4_ACC": "0", "VOSDET_WINO4_VD": "1",
+                   "VOSDET_WINO4_IL": "0"},
          "ps": {"VOSDET_WINO4_PS": "1", "VOSDET_WINO4_ACC": "0", "VOSDET_WINO4_VD": "1"},
          "acc": {"VOSDET_WINO4_PS": "0", "VOSDET_WINO4_ACC": "1", "VOSDET_WINO4_VD": "1"},
-         "acc3": {"VOSDET_WINO4_PS": "0", "VOSDET_WINO4_ACC": "1", "VOSDET_WINO4_VD": "3"}}
+         "acc3": {"VOSDET_WINO4_PS": "0", "VOSDET_WINO4_ACC": "1", "VOSDET_WINO4_VD": "3"},
+         "il": {"VOSDET_WINO4_PS": "0", "VOSDET_WINO4_ACC": "1", "VOSDET_WINO4_VD": "1",
+                "VOSDET_WINO4_IL": "1"}}
 
 
 def _run(x, u, b, relu, form):
@@ -40,7 +43,7 @@ def _run(x, u, b, relu, form):
                                         (3, 128, 17, 45, 128), (2, 512, 25, 42, 512),
                                         (1, 8, 9, 9, 64), (4, 24, 33, 31, 128)])
 @pytest.mark.parametrize("bias", [True, False])
-@pytest.mark.parametrize("form", ["ps", "acc", "acc3"])
+@pytest.mark.parametrize("form", ["ps", "acc", "acc3", "il"])
 def test_wino4_forms_bit_identical_to_first_form(N, C, H, W, Co, bias, form):
     from vosdetectron_amd import ops
     g = torch.Generator(device="cuda").manual_seed(N * 1000 + C + H)
@@ -59,7 +62,7 @@ def test_wino4_forms_bit_identical_to_first_form(N, C, H, W, Co, bias, form):
     assert err <= 5e-5 * max(1., float(ref.abs().max())), err
 
 
-@pytest.mark.parametrize("form", ["ps", "acc", "acc3"])
+@pytest.mark.parametrize("form", ["ps", "acc", "acc3", "il"])
 def test_wino4_forms_benched_p2(form):
     from vosdetectron_amd import ops
     g = torch.Generator(device="cuda").manual_seed(7)

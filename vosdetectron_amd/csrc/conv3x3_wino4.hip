@@ -133,7 +133,18 @@ __device__ __forceinline__ void w4_at6(const float (&m)[6], float (&y)[4]) {
 // ACC: U loads and their waits counted by hand (w4_uload_asm), the patch DMA spread over
 // all 8 waves (3 pieces each, a zero-page piece where no chunk is left) so every wave's
 // queue has the same shape
-template <bool RELU, int PROBE, bool ACC = false, int VD = 1>
+// STAMP (research, VOSDET_WINO4_STAMP=1; outputs unchanged): lane 0 of every wave of
+// workgroups < 512 records s_memtime at six points of chunks 8..11 into
+// g_wino4_stamps (vd_research_wino4_stamps copies them out)
+constexpr int kStampWg = 512, kStampCh0 = 8, kStampNch = 4;
+__device__ unsigned long long g_wino4_stamps[kStampWg * 8 * kStampNch * 6];
+
+// IL (ACC form, VOSDET_WINO4_IL): the next chunk's transform interleaved with the
+// transforming wave's own MFMAs -- column c of B^T d after position c's MFMAs (its patch
+// reads issued one position ahead), row a of (B^T d) B and its V writes after position
+// 6 + a -- instead of one block before them (the chunk stamps: 3.6 k cycles of
+// transform, during which the SIMD's MFMA pipe is fed by the partner wave alone)
+template <bool RELU, int PROBE, bool ACC = false, int VD = 1, bool STAMP = false, bool IL = false>
 __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
@@ -295,7 +306,19 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     // the four SIMDs' two waves reach the barrier together.
     auto mfma_chunk = [&](bool xon, int stage, int ch, int chn, int tstage) {
         const f2v *vp = vread + stage * (k4VStageB / 8);
-        if (xon) transform(tstage);
+        const float *tpi = tread + tstage * (k4PStageB / 4);
+        float *vpw = twrite + tstage * (k4VStageB / 4);
+        float xc[6], tt[6][6];
+        if (IL && xon) {
+#pragma unroll
+            for (int r = 0; r < 6; ++r) xc[r] = tpi[(r * k4RP) * 4];
+        }
+        if (!IL && xon) {
+            // probe_hi bit 1 (VOSDET_WINO4_PRIO=1): the transform at wave priority 1
+            if (probe_hi & 2) asm volatile("s_setprio 1" ::: "memory");
+            transform(tstage);
+            if (probe_hi & 2) asm volatile("s_setprio 0" ::: "memory");
+        }
         // V of positions pp .. pp + VD - 1 in a ring (VD > 1: more LDS latency hidden
         // behind one wave's own MFMAs while its SIMD partner transforms)
         f2v vq[VD][2];
@@ -342,6 +365,25 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
                 else
                     u[pp % kUR] = uload(chn, pp + kUR - 18);
             }
+            if constexpr (IL) {
+                if (xon && pp < 6) {  // column pp of B^T d, then column pp + 1's reads
+                    float y[6];
+                    w4_bt6(xc, y);
+#pragma unroll
+                    for (int a = 0; a < 6; ++a) tt[a][pp] = y[a];
+                    if (pp < 5) {
+                        const int c = pp + 1;
+#pragma unroll
+                        for (int r = 0; r < 6; ++r) xc[r] = tpi[(r * k4RP + 2 * c + (c >> 1)) * 4];
+                    }
+                } else if (xon && pp < 12) {  // row pp - 6 of (B^T d) B -> V
+                    const int a = pp - 6;
+                    float y[6];
+                    w4_bt6(tt[a], y);
+#pragma unroll
+                    for (int b = 0; b < 6; ++b) vpw[(6 * a + b) * 256] = y[b];
+                }
+            }
             __builtin_amdgcn_sched_barrier(0);
             if (pp + VD < 18) {
                 vq[pp % VD][0] = n0;
@@ -372,6 +414,28 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
         for (int ch = 0; ch < nch; ++ch) {
             const int sv = ch & 1;
             const int chn = ch + 1 < nch ? ch + 1 : ch;
+            if constexpr (STAMP) {
+                const bool st = blockIdx.x < kStampWg && ch >= kStampCh0 && ch < kStampCh0 + kStampNch;
+                unsigned long long *sp_ = g_wino4_stamps +
+                    ((blockIdx.x * 8 + wave) * kStampNch + (ch - kStampCh0)) * 6;
+                unsigned long long t[6];
+                t[0] = __builtin_amdgcn_s_memtime();
+                dma(ch + 2 < nch ? ch + 2 : -1, sv);
+                t[1] = __builtin_amdgcn_s_memtime();
+                if (!IL && wave < 4 && ch + 1 < nch) transform(sv ^ 1);
+                t[2] = __builtin_amdgcn_s_memtime();
+                mfma_chunk(IL && wave < 4 && ch + 1 < nch, sv, ch, chn, sv ^ 1);
+                t[3] = __builtin_amdgcn_s_memtime();
+                asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+                t[4] = __builtin_amdgcn_s_memtime();
+                __syncthreads();
+                t[5] = __builtin_amdgcn_s_memtime();
+                if (st && lane == 0) {
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) sp_[i] = t[i];
+                }
+                continue;
+            }
             dma(ch + 2 < nch ? ch + 2 : -1, sv);  // every wave, every chunk: 3 pieces
             mfma_chunk(wave < 4 && ch + 1 < nch, sv, ch, chn, sv ^ 1);
             asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
@@ -889,10 +953,31 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
         kacc = relu ? conv3x3_wino4_kernel<true, 0, true, 2> : conv3x3_wino4_kernel<false, 0, true, 2>;
     if (vd == 3)
         kacc = relu ? conv3x3_wino4_kernel<true, 0, true, 3> : conv3x3_wino4_kernel<false, 0, true, 3>;
+    const char *pre = getenv("VOSDET_WINO4_PRIO");
+    const int prio = (pre && pre[0] == '1') ? 2 : 0;
+    const char *ste = getenv("VOSDET_WINO4_STAMP");
+    if (ste && ste[0] == '1')
+        kacc = relu ? conv3x3_wino4_kernel<true, 0, true, 1, true>
+                    : conv3x3_wino4_kernel<false, 0, true, 1, true>;
+    const char *ile = getenv("VOSDET_WINO4_IL");
+    if (ile && ile[0] == '1')
+        kacc = relu ? conv3x3_wino4_kernel<true, 0, true, 1, false, true>
+                    : conv3x3_wino4_kernel<false, 0, true, 1, false, true>;
+    if (ile && ile[0] == '2')  // interleaved + stamps
+        kacc = relu ? conv3x3_wino4_kernel<true, 0, true, 1, true, true>
+                    : conv3x3_wino4_kernel<false, 0, true, 1, true, true>;
     const kern_t kern = (acc && !probe) ? kacc : table[relu ? 1 : 0][probe];
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(k4Threads), 0, s, X, N, H, W, C, U,
-                       Cout, bias, Y, tby, tbx, cbx, probe_hi, mos);
+                       Cout, bias, Y, tby, tbx, cbx, probe_hi | prio, mos);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
 }  // namespace vd
+
+// research: the STAMP form's timestamps [512 workgroups][8 waves][4 chunks][6]
+extern "C" int vd_research_wino4_stamps(unsigned long long *host, int n) {
+    const int cap = vd::kStampWg * 8 * vd::kStampNch * 6;
+    if (n > cap) n = cap;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(vd::g_wino4_stamps), (size_t)n * 8, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
