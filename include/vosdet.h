@@ -199,6 +199,14 @@ int vd_conv3x3_wino4_bias_act(const float *X, int N, int H, int W, int C, const 
 int vd_conv3x3_wino4_mosaic_bias_act(const float *X, int N, int H, int W, int C, const float *U,
                                      int Cout, const float *bias, int relu, float *Y,
                                      void *stream);
+/* The same over N maps stacked in one column at a pitch of H + 1 rounded up to 4 rows
+ * (each map padded by its own zeros), so the 16-row output blocks run on through the
+ * stack: for heights that leave most of a map's last block row empty (50 x 84 res4 /
+ * P4, 25 x 42 res5).  Bit-identical to vd_conv3x3_wino4_bias_act; VD_ERR_SHAPE when
+ * N H W C >= 2^31. */
+int vd_conv3x3_wino4_rows_bias_act(const float *X, int N, int H, int W, int C, const float *U,
+                                   int Cout, const float *bias, int relu, float *Y,
+                                   void *stream);
 
 /* The Winograd convolution of R images of seg_h x W pixels stored back to back
  * (R x seg_h x W x C, i.e. one H = R * seg_h image), each padded by its own zeros:

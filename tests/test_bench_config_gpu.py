@@ -63,7 +63,7 @@ def test_bench_batch_routes(bench_setup):
     assert p2.is_contiguous(memory_format=torch.channels_last)
     assert all(int(c) > 0 for c in out["counts_host"])
     assert modeling.conv3x3_route(BATCH, 256, 256, 200, 336) == ("wino4", None)
-    assert modeling.conv3x3_route(BATCH, 256, 256, 100, 168) == ("wino4", None)
+    assert modeling.conv3x3_route(BATCH, 256, 256, 100, 168) == ("wino4", "rows")
     assert modeling.conv3x3_route(BATCH, 256, 256, 25, 42) == ("wino", "2d")
     assert modeling.conv3x3_route(BATCH * 100, 256, 256, 14, 14) == ("wino4", "pair")
     assert modeling.conv3x3_route(8000, 512, 512, 7, 7) == ("wino", "2d")  # C4 res5 head
@@ -71,7 +71,8 @@ def test_bench_batch_routes(bench_setup):
     n_wino = routes.get("wino", 0) + routes.get("wino_rows", 0) + routes.get("wino_2d", 0)
     # F(4x4): FPN posthoc + RPN conv on P2-P4 (6) and the body's stride-1 conv2s, the
     # mask head's four convs as map pairs; F(2x2): posthoc P5 + RPN P5 / P6 at least
-    assert routes.get("wino4", 0) >= 6 + 3 + 3 + 5 + 2, routes
+    assert routes.get("wino4", 0) + routes.get("wino4_rows", 0) >= 6 + 3 + 3 + 5 + 2, routes
+    assert routes.get("wino4_rows", 0) >= 10, routes  # P3 / P4 posthoc + RPN, res3 / res4 conv2s
     assert routes.get("wino4_pair", 0) == 4, routes
     assert n_wino >= 3 and routes.get("wino_2d", 0) >= 3, routes
     # the P2 top-down lateral step as one fused MFMA launch (modeling._fpn_lateral_fused_k)
@@ -114,7 +115,7 @@ def test_conv3x3_wino_benched_shapes(N, C, H, W, bias):
     b = torch.randn(C, device="cuda", generator=g) if bias else None
     if algo == "wino4":
         got = ops.conv3x3_wino4_bias_act(x, ops.conv3x3_wino4_weight(w), b, relu=bias,
-                                         mosaic=mos == "pair")
+                                         mosaic=mos or False)
     else:
         got = ops.conv3x3_wino_bias_act(x, ops.conv3x3_wino_weight(w), b, relu=bias,
                                         mosaic=mos)

@@ -104,3 +104,27 @@ def test_wino4_pair_mosaic_refuses_large_maps():
     x = torch.zeros(2, 64, 16, 14, device="cuda").contiguous(memory_format=torch.channels_last)
     u = ops.conv3x3_wino4_weight(torch.zeros(64, 64, 3, 3, device="cuda"))
     assert ops.conv3x3_wino4_bias_act(x, u, None, mosaic=True) is None
+
+
+@pytest.mark.parametrize("N,C,H,W,Co", [(3, 64, 50, 84, 64), (2, 256, 25, 42, 128),
+                                        (5, 8, 7, 33, 64), (2, 16, 16, 16, 64),
+                                        (1, 64, 13, 9, 64), (32, 256, 50, 84, 256)])
+def test_wino4_row_stack_bit_identical(N, C, H, W, Co):
+    """vd_conv3x3_wino4_rows_bias_act (maps stacked at a pitch of H + 1 rounded up to
+    4 rows) == one launch over the N maps, incl. H a multiple of 4 and blocks that
+    straddle maps; within the F(4x4) tolerance of torch."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(N * 7 + C + H * W)
+    x = torch.randn(N, C, H, W, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    w = torch.randn(Co, C, 3, 3, device="cuda", generator=g) / (3. * C ** .5)
+    b = torch.randn(Co, device="cuda", generator=g)
+    u = ops.conv3x3_wino4_weight(w)
+    y1 = ops.conv3x3_wino4_bias_act(x, u, b, relu=True)
+    y2 = ops.conv3x3_wino4_bias_act(x, u, b, relu=True, mosaic="rows")
+    torch.cuda.synchronize()
+    assert y2 is not None
+    assert torch.equal(y1, y2), float((y1 - y2).abs().max())
+    ref = F.relu(F.conv2d(x[:4], w, b, padding=1))
+    err = float((y2[:4] - ref).abs().max())
+    assert err <= 5e-5 * max(1., float(ref.abs().max())), err

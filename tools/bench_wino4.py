@@ -46,7 +46,9 @@ def main():
         scale = float(ref.abs().max())
         for name, wf, cf, exe in (("wino2", ops.conv3x3_wino_weight, ops.conv3x3_wino_bias_act,
                                    direct * 16 / 36),
-                                  ("wino4", ops.conv3x3_wino4_weight, ops.conv3x3_wino4_bias_act,
+                                  ("wino4", ops.conv3x3_wino4_weight,
+                                   lambda *a, **k: ops.conv3x3_wino4_bias_act(
+                                       *a, mosaic=os.environ.get("WINO4_MOSAIC") or False, **k),
                                    direct * 36 / 144)):
             u = wf(w)
             y = cf(x, u, b, relu=True)

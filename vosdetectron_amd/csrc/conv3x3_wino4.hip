@@ -172,9 +172,14 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     // holds maps 2 sp (columns 0..15) and 2 sp + 1 (columns 16..31), each at the
     // origin of its 16 x 16 cell; taps outside a map read zero, so every output is
     // the map's own padded convolution, bit-identical to one map per block
-    if (sp >= (mos ? (N + 1) >> 1 : N * tby * tbx)) return;
-    const int n = mos ? 2 * sp : sp / (tby * tbx);
-    const int rem = mos ? 0 : sp - n * tby * tbx;
+    // mos >= 4: row stack (vd_conv3x3_wino4_rows_bias_act) -- the N maps stacked at a
+    // pitch of hp = mos >> 2 rows (a multiple of 4, > H: every tile inside one map's
+    // pitch, the rows past a map zero), one image of N hp rows
+    const bool pair = mos == 1;
+    const int hp = mos >> 2;
+    if (sp >= (pair ? (N + 1) >> 1 : (hp ? tby * tbx : N * tby * tbx))) return;
+    const int n = pair ? 2 * sp : (hp ? 0 : sp / (tby * tbx));
+    const int rem = pair ? 0 : sp - n * tby * tbx;
     const int tyb = rem / tbx, txb = rem - (rem / tbx) * tbx;
     const int oy0 = 4 * k4TR * tyb, ox0 = 4 * k4TC * txb;
     const int iy0 = oy0 - 1, ix0 = ox0 - 1;
@@ -200,10 +205,12 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
         const int Cc = 2 * m + (r5 >> 1), hf = r5 & 1;
         const int y = iy0 + R, x = ix0 + Cc;
         // mosaic: cell x >> 4 (map n + cell), column x & 15 of that map
-        const int cell = mos ? (x >> 4) : 0, xm = mos ? (x & 15) : x;
-        const bool ok = R < k4PR && r5 < 4 && Cc < k4PC && (unsigned)y < (unsigned)H &&
-                        x >= 0 && (unsigned)xm < (unsigned)W && n + cell < N;
-        poff[kPS * k] = ok ? (uint32_t)(((cell * H + y) * W + xm) * C + 4 * hf)
+        const int cell = pair ? (x >> 4) : 0, xm = pair ? (x & 15) : x;
+        // row stack: map y / hp, its row y % hp
+        const int mr = (hp && y >= 0) ? y / hp : 0, ly = hp ? y - mr * hp : y;
+        const bool ok = R < k4PR && r5 < 4 && Cc < k4PC && (unsigned)ly < (unsigned)H &&
+                        y >= 0 && x >= 0 && (unsigned)xm < (unsigned)W && n + cell + mr < N;
+        poff[kPS * k] = ok ? (uint32_t)((((cell + mr) * H + ly) * W + xm) * C + 4 * hf)
                            : 0x80000000u | (uint32_t)(4 * hf);
     }
     const float *const zero = reinterpret_cast<const float *>(g_wino4_zero);
@@ -495,12 +502,13 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int yy = oy0 + 4 * tr + i;
-        if (yy >= H) continue;
+        const int yv = oy0 + 4 * tr + i;
+        const int mr = hp ? yv / hp : 0, yy = hp ? yv - mr * hp : yv;
+        if (yy >= H || n + mr >= N) continue;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int xc = ox0 + 4 * tc + k;
-            const int ncell = mos ? n + (xc >> 4) : n, xx = mos ? (xc & 15) : xc;
+            const int ncell = pair ? n + (xc >> 4) : n + mr, xx = pair ? (xc & 15) : xc;
             if (xx >= W || ncell >= N) continue;
             float4 v = make_float4(o[4 * i + k][0] + bv.x, o[4 * i + k][1] + bv.y,
                                    o[4 * i + k][2] + bv.z, o[4 * i + k][3] + bv.w);
@@ -876,11 +884,19 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
         return VD_ERR_SHAPE;
     // the map-pair mosaic: two maps of at most 15 x 15 per 16 x 32 block (the 16 x 16
     // cell keeps a zero column / row after each map), 2 H W C floats of offsets < 2^31
-    if (mos && (H > 15 || W > 15 || (int64_t)2 * H * W * C >= ((int64_t)1 << 31)))
+    if (mos == 1 && (H > 15 || W > 15 || (int64_t)2 * H * W * C >= ((int64_t)1 << 31)))
         return VD_ERR_SHAPE;
-    const int tby = mos ? 1 : (H + 4 * k4TR - 1) / (4 * k4TR);
-    const int tbx = mos ? 1 : (W + 4 * k4TC - 1) / (4 * k4TC);
-    const int64_t nsp = mos ? ((int64_t)N + 1) / 2 : (int64_t)N * tby * tbx;
+    // the row stack: pitch = H + 1 rounded up to 4 (a zero row after every map), one
+    // image whose offsets stay 32-bit
+    const int hp = (H + 1 + 3) / 4 * 4;
+    if (mos == 2) {
+        if ((int64_t)N * H * W * C >= ((int64_t)1 << 31) || (int64_t)N * hp >= ((int64_t)1 << 30))
+            return VD_ERR_SHAPE;
+        mos = hp << 2;
+    }
+    const int tby = mos == 1 ? 1 : ((mos ? N * hp : H) + 4 * k4TR - 1) / (4 * k4TR);
+    const int tbx = mos == 1 ? 1 : (W + 4 * k4TC - 1) / (4 * k4TC);
+    const int64_t nsp = mos == 1 ? ((int64_t)N + 1) / 2 : (int64_t)(mos ? 1 : N) * tby * tbx;
     const int ncb = Cout / k4Co;
     // VOSDET_WINO4_CBX=0: the four channel blocks of a spatial block on one XCD (the
     // patch then comes from that XCD's L2 three times in four), not one channel block

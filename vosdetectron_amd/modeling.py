@@ -124,16 +124,43 @@ def _wino4_block_use(H: int, W: int) -> float:
     return H * W / float(-(-H // 16) * 16 * -(-W // 32) * 32)
 
 
+def _wino4_rows_use(N: int, H: int, W: int) -> float:
+    """Real-output share of the F(4x4) blocks over the row stack (maps at a pitch of
+    H + 1 rounded up to 4 rows, vd_conv3x3_wino4_rows_bias_act)."""
+    hp = (H + 4) // 4 * 4
+    return N * H * W / float(-(-N * hp // 16) * 16 * -(-W // 32) * 32)
+
+
+def _wino4_mode(N: int, Cin: int, Cout: int, H: int, W: int):
+    """conv3x3_route's F(4x4) gate: None (not F(4x4)), False (one map per block
+    column) or "rows" (the row stack, where it wastes less of the blocks: 50 x 84 maps
+    84 % vs 68 %, 25 x 42 59 % vs 51 %; VOSDET_WINO4_ROWS=0 turns it off).
+    VOSDET_WINO4=0 turns F(4x4) off."""
+    if os.environ.get("VOSDET_WINO4", "1") == "0":
+        return None
+    if Cout % 64 or Cin % 8 or Cout == 0 or Cin == 0 or Cin > ops.WINO_MAX_CIN:
+        return None
+    if H * W * Cin >= (1 << 31):
+        return None
+    use = _wino4_block_use(H, W)
+    wgs = N * -(-H // 16) * -(-W // 32) * (Cout // 64)
+    plain = wgs >= _WINO4_MIN_WGS and use >= _WINO4_MIN_BLOCK_USE
+    if (os.environ.get("VOSDET_WINO4_ROWS", "1") != "0" and N > 1
+            and N * H * W * Cin < (1 << 31)):
+        # measured (profiles/r05/wino4_rows/): P3 2.09 -> 2.00 ms, P4 0.63 -> 0.53, res3
+        # 0.64 -> 0.60, res5 0.79 -> 0.75 (896 workgroups, fewer than one map per block
+        # column gives, and still faster)
+        ru = _wino4_rows_use(N, H, W)
+        rwgs = -(-N * ((H + 4) // 4 * 4) // 16) * -(-W // 32) * (Cout // 64)
+        if (ru > use + 0.02 and ru >= _WINO4_MIN_BLOCK_USE
+                and (rwgs >= _WINO4_MIN_WGS or (plain and rwgs >= _WINO4_MIN_WGS // 2))):
+            return "rows"
+    return False if plain else None
+
+
 def _wino4_ok(N: int, Cin: int, Cout: int, H: int, W: int) -> bool:
     """conv3x3_route's F(4x4) gate (VOSDET_WINO4=0 turns it off)."""
-    if os.environ.get("VOSDET_WINO4", "1") == "0":
-        return False
-    if Cout % 64 or Cin % 8 or Cout == 0 or Cin == 0 or Cin > ops.WINO_MAX_CIN:
-        return False
-    if H * W * Cin >= (1 << 31):
-        return False
-    wgs = N * -(-H // 16) * -(-W // 32) * (Cout // 64)
-    return wgs >= _WINO4_MIN_WGS and _wino4_block_use(H, W) >= _WINO4_MIN_BLOCK_USE
+    return _wino4_mode(N, Cin, Cout, H, W) is not None
 
 
 def _wino4_pair_ok(N: int, Cin: int, Cout: int, H: int, W: int) -> bool:
@@ -163,8 +190,9 @@ def conv3x3_route(N: int, Cin: int, Cout: int, H: int, W: int, mosaic=True):
     mos, use = _pick_mosaic(N, H, W, mosaic)
     wino = (os.environ.get("VOSDET_CONV3X3_ALGO", CONV3X3_ALGO) == "wino" and Cout % 64 == 0
             and Cin % 8 == 0 and Cout > 0 and Cin <= ops.WINO_MAX_CIN)
-    if wino and _wino4_ok(N, Cin, Cout, H, W):
-        return "wino4", None
+    w4 = _wino4_mode(N, Cin, Cout, H, W) if wino else None
+    if w4 is not None:
+        return "wino4", (w4 or None)
     if wino and mosaic and _wino4_pair_ok(N, Cin, Cout, H, W):
         return "wino4", "pair"
     if wino and npx >= _WINO_MIN_PIXELS and use >= _WINO_MIN_BLOCK_USE:
@@ -213,9 +241,9 @@ def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=True):
         if getattr(conv, "_vd_u4_key", None) != key:
             conv._vd_u4 = ops.conv3x3_wino4_weight(w.detach())
             conv._vd_u4_key = key
-        y = ops.conv3x3_wino4_bias_act(x, conv._vd_u4, b, relu=relu, mosaic=mos == "pair")
+        y = ops.conv3x3_wino4_bias_act(x, conv._vd_u4, b, relu=relu, mosaic=mos or False)
         if y is not None:
-            _count_route("wino4_pair" if mos == "pair" else "wino4")
+            _count_route({"pair": "wino4_pair", "rows": "wino4_rows"}.get(mos, "wino4"))
             return y
         algo, mos = "wino", _pick_mosaic(x.shape[0], x.shape[2], x.shape[3], mosaic)[0]
     if algo == "wino":

@@ -689,11 +689,13 @@ def conv3x3_wino4_weight(w: torch.Tensor) -> Optional[torch.Tensor]:
 
 def conv3x3_wino4_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch.Tensor],
                            relu: bool = False, out: Optional[torch.Tensor] = None,
-                           mosaic: bool = False):
+                           mosaic=False):
     """act(conv3x3(x, pad 1) + bias) on a channels_last fp32 tensor by Winograd
-    F(4x4,3x3) (vd_conv3x3_wino4_bias_act); u from conv3x3_wino4_weight.  mosaic:
-    maps of at most 15 x 15 two per output block (vd_conv3x3_wino4_mosaic_bias_act,
-    bit-identical).  None for a shape the kernel does not serve."""
+    F(4x4,3x3) (vd_conv3x3_wino4_bias_act); u from conv3x3_wino4_weight.  mosaic
+    True / "pair": maps of at most 15 x 15 two per output block
+    (vd_conv3x3_wino4_mosaic_bias_act); "rows": the maps stacked in one column at a
+    4-row pitch (vd_conv3x3_wino4_rows_bias_act); both bit-identical.  None for a
+    shape the kernel does not serve."""
     if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 4 \
             or not x.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("x must be a channels_last fp32 device tensor")
@@ -708,12 +710,14 @@ def conv3x3_wino4_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torc
     if out is None:
         out = torch.empty((N, Cout, H, W), dtype=torch.float32, device=x.device,
                           memory_format=torch.channels_last)
-    fn = lib().vd_conv3x3_wino4_mosaic_bias_act if mosaic else lib().vd_conv3x3_wino4_bias_act
+    fn = {False: lib().vd_conv3x3_wino4_bias_act, True: lib().vd_conv3x3_wino4_mosaic_bias_act,
+          "pair": lib().vd_conv3x3_wino4_mosaic_bias_act,
+          "rows": lib().vd_conv3x3_wino4_rows_bias_act}[mosaic]
     st = fn(x.data_ptr(), N, H, W, C, u_.data_ptr(), Cout,
             b_.data_ptr() if b_ is not None else None, int(relu), out.data_ptr(), _stream())
     if st == VD_ERR_SHAPE:
         return None
-    check(st, "vd_conv3x3_wino4_mosaic_bias_act" if mosaic else "vd_conv3x3_wino4_bias_act")
+    check(st, "vd_conv3x3_wino4_bias_act (mosaic %r)" % (mosaic,))
     return out
 
 
