@@ -110,12 +110,13 @@ __device__ __forceinline__ void w4_wait_u(f4v &a) {
 //                   0 2 -1 -2 1 0; 0 4 0 -5 0 1]
 __device__ __forceinline__ void w4_bt6(const float (&x)[6], float (&y)[6]) {
     const float t0 = __builtin_fmaf(-4.f, x[2], x[4]), t1 = __builtin_fmaf(-4.f, x[1], x[3]);
-    const float t2 = x[4] - x[2], t3 = 2.f * (x[3] - x[1]);
+    const float t2 = x[4] - x[2], d = x[3] - x[1];
     y[0] = __builtin_fmaf(4.f, x[0], __builtin_fmaf(-5.f, x[2], x[4]));
     y[1] = t0 + t1;
     y[2] = t0 - t1;
-    y[3] = t2 + t3;
-    y[4] = t2 - t3;
+    // t2 +- 2 d with 2 d exact: one rounding either way, as t2 +- (2 d) -- 12 VALU a call
+    y[3] = __builtin_fmaf(2.f, d, t2);
+    y[4] = __builtin_fmaf(-2.f, d, t2);
     y[5] = __builtin_fmaf(4.f, x[1], __builtin_fmaf(-5.f, x[3], x[5]));
 }
 
@@ -196,6 +197,12 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     constexpr int kDW = ACC ? 8 : 4;  // waves issuing the patch DMA
     constexpr int kDK = 24 / kDW;     // its wave instructions per issuing wave
     constexpr int kPS = ACC ? 512 : 256;
+    const float *const zero = reinterpret_cast<const float *>(g_wino4_zero);
+    // ACC: each piece's chunk-0 source kept per lane (2 VGPRs a piece; zero-page lanes
+    // point into the zero page, which holds C floats, so they may advance with the
+    // chunk too): a chunk's DMA address is one 64-bit add per piece, not the ~15 VALU of
+    // offset decode and selects per piece the first form spends
+    const float *srcp[kDK];
 #pragma unroll
     for (int k = 0; k < kDK; ++k) {
         if (!ACC && wave >= 4) break;
@@ -212,9 +219,16 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
                         y >= 0 && x >= 0 && (unsigned)xm < (unsigned)W && n + cell + mr < N;
         poff[kPS * k] = ok ? (uint32_t)((((cell + mr) * H + ly) * W + xm) * C + 4 * hf)
                            : 0x80000000u | (uint32_t)(4 * hf);
+        srcp[k] = ok ? Xn + (((cell + mr) * H + ly) * W + xm) * C + 4 * hf : zero + 4 * hf;
     }
-    const float *const zero = reinterpret_cast<const float *>(g_wino4_zero);
-    auto dma = [&](int ch, int stage) {  // ch < 0 (ACC): zero-page pieces, queue shape only
+    auto dma = [&](int ch, int stage) {
+        if constexpr (ACC) {  // ch: the chunk whose data the pieces copy (clamped by the caller)
+#pragma unroll
+            for (int k = 0; k < kDK; ++k)
+                w4_dma_1k(srcp[k] + ch * k4KC,
+                          pbase + (uint32_t)(stage * k4PStageB + (wave + kDW * k) * 1024));
+            return;
+        }  // ch < 0 (ACC): zero-page pieces, queue shape only
         uint32_t oo[kDK];  // all offsets read before the first DMA (one LDS round trip)
 #pragma unroll
         for (int k = 0; k < kDK; ++k) oo[k] = poff[kPS * k];
@@ -412,7 +426,7 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
         }
         // chunks 0 and 1 fetched together: one HBM round trip in the prologue, not two
         dma(0, 0);
-        dma(nch > 1 ? 1 : -1, 1);
+        dma(nch > 1 ? 1 : 0, 1);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDK) : "memory");  // U and chunk 0 landed
         __syncthreads();
         if (wave < 4) transform(0);
@@ -427,7 +441,7 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
                     ((blockIdx.x * 8 + wave) * kStampNch + (ch - kStampCh0)) * 6;
                 unsigned long long t[6];
                 t[0] = __builtin_amdgcn_s_memtime();
-                dma(ch + 2 < nch ? ch + 2 : -1, sv);
+                dma(ch + 2 < nch ? ch + 2 : nch - 1, sv);
                 t[1] = __builtin_amdgcn_s_memtime();
                 if (!IL && wave < 4 && ch + 1 < nch) transform(sv ^ 1);
                 t[2] = __builtin_amdgcn_s_memtime();
@@ -443,7 +457,9 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
                 }
                 continue;
             }
-            dma(ch + 2 < nch ? ch + 2 : -1, sv);  // every wave, every chunk: 3 pieces
+            // every wave, every chunk: 3 pieces (past the last chunk, a copy of it into
+            // the stage no transform reads again, so the queue keeps its shape)
+            dma(ch + 2 < nch ? ch + 2 : nch - 1, sv);
             mfma_chunk(wave < 4 && ch + 1 < nch, sv, ch, chn, sv ^ 1);
             asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
             __syncthreads();
