@@ -363,7 +363,8 @@ def measure_dominant_conv(dev, F, H, W, C=256, iters=None):
     algo, mos = modeling.conv3x3_route(F, C, C, H, W)
     if algo == "wino4":
         u = ops.conv3x3_wino4_weight(w)
-        run = lambda out=None: ops.conv3x3_wino4_bias_act(x, u, b, out=out)  # noqa: E731
+        run = lambda out=None: ops.conv3x3_wino4_bias_act(  # noqa: E731
+            x, u, b, out=out, mosaic=mos or False)
         name = "vd::conv3x3_wino4_kernel (Winograd F(4x4,3x3), v_mfma_f32_16x16x4_f32)"
         share, positions = 1 / 4, "36 positions per 4x4 tile, 1/4"
     else:
@@ -388,7 +389,7 @@ def measure_dominant_conv(dev, F, H, W, C=256, iters=None):
     alg = 2.0 * F * H * W * C * C * 9
     exe = alg * share
     del x, y, u
-    return {"kernel": name, "route": algo,
+    return {"kernel": name, "route": algo + ("_" + mos if isinstance(mos, str) else ""),
             "bound": "mfma", "shape": [F, C, H, W, C], "avg_launch_us": round(t * 1e6, 1),
             "unit": "TFLOP/s", "peak": MFMA_FP32_PEAK_TFS,
             "achieved": round(exe / t / 1e12, 1),

@@ -62,7 +62,7 @@ def test_bench_batch_routes(bench_setup):
     assert p2.shape == (BATCH, 256, 200, 336)
     assert p2.is_contiguous(memory_format=torch.channels_last)
     assert all(int(c) > 0 for c in out["counts_host"])
-    assert modeling.conv3x3_route(BATCH, 256, 256, 200, 336) == ("wino4", None)
+    assert modeling.conv3x3_route(BATCH, 256, 256, 200, 336) == ("wino4", "rows")
     assert modeling.conv3x3_route(BATCH, 256, 256, 100, 168) == ("wino4", "rows")
     assert modeling.conv3x3_route(BATCH, 256, 256, 25, 42) == ("wino", "2d")
     assert modeling.conv3x3_route(BATCH * 100, 256, 256, 14, 14) == ("wino4", "pair")

@@ -108,12 +108,12 @@ def test_winograd4_route_gate():
     import torch.nn.functional as F
     from vosdetectron_amd import modeling
     r = modeling.conv3x3_route
-    for args in [(32, 256, 256, 200, 336), (32, 64, 64, 200, 336)]:
-        assert r(*args) == ("wino4", None), args
+    for args in [(32, 256, 256, 192, 320), (32, 64, 64, 192, 320)]:
+        assert r(*args) == ("wino4", None), args  # blocks already full: no stack
     # P3 / P4-sized maps: the row stack wastes less of the 16-row blocks (84 vs 78 / 68 %;
     # res5 59 vs 51 % at 896 workgroups)
     for args in [(32, 256, 256, 100, 168), (32, 256, 256, 50, 84), (32, 128, 128, 100, 168),
-                 (32, 512, 512, 25, 42)]:
+                 (32, 512, 512, 25, 42), (32, 256, 256, 200, 336), (32, 64, 64, 200, 336)]:
         assert r(*args) == ("wino4", "rows"), args
     assert abs(modeling._wino4_rows_use(32, 50, 84) - 32 * 50 * 84 / (104 * 16 * 96)) < 1e-12
     for args in [(32, 256, 256, 25, 42), (32, 256, 256, 13, 21), (8000, 512, 512, 7, 7),

@@ -108,7 +108,8 @@ def test_wino4_pair_mosaic_refuses_large_maps():
 
 @pytest.mark.parametrize("N,C,H,W,Co", [(3, 64, 50, 84, 64), (2, 256, 25, 42, 128),
                                         (5, 8, 7, 33, 64), (2, 16, 16, 16, 64),
-                                        (1, 64, 13, 9, 64), (32, 256, 50, 84, 256)])
+                                        (1, 64, 13, 9, 64), (32, 256, 50, 84, 256),
+                                        (8, 64, 200, 336, 64)])
 def test_wino4_row_stack_bit_identical(N, C, H, W, Co):
     """vd_conv3x3_wino4_rows_bias_act (maps stacked at a pitch of H + 1 rounded up to
     4 rows) == one launch over the N maps, incl. H a multiple of 4 and blocks that

@@ -152,7 +152,8 @@ def _wino4_mode(N: int, Cin: int, Cout: int, H: int, W: int):
         # column gives, and still faster)
         ru = _wino4_rows_use(N, H, W)
         rwgs = -(-N * ((H + 4) // 4 * 4) // 16) * -(-W // 32) * (Cout // 64)
-        if (ru > use + 0.02 and ru >= _WINO4_MIN_BLOCK_USE
+        # (P2 200 x 336: 0.918 -> 0.936, 7.15 -> 7.11 ms, res2 0.64 -> 0.64 ms)
+        if (ru > use + 0.015 and ru >= _WINO4_MIN_BLOCK_USE
                 and (rwgs >= _WINO4_MIN_WGS or (plain and rwgs >= _WINO4_MIN_WGS // 2))):
             return "rows"
     return False if plain else None
