@@ -193,9 +193,10 @@ int vd_conv3x3_wino4_weight(const float *w, int Cout, int Cin, float *U, void *s
 int vd_conv3x3_wino4_bias_act(const float *X, int N, int H, int W, int C, const float *U,
                               int Cout, const float *bias, int relu, float *Y, void *stream);
 /* The same over N small maps (H, W <= 15: the mask head's 14 x 14 RoI features,
- * mask_rcnn_heads.py:178-188), two maps per 16 x 32 output block, each padded by its
- * own zeros: bit-identical to vd_conv3x3_wino4_bias_act, which gives every map a
- * block of its own.  VD_ERR_SHAPE for larger maps. */
+ * mask_rcnn_heads.py:178-188), two maps per 16 x 32 output block -- eight in 8 x 8
+ * cells when H, W <= 7 (C4's res5 head on 7 x 7 RoI maps, ResNet.py:17-155) -- each
+ * padded by its own zeros: bit-identical to vd_conv3x3_wino4_bias_act, which gives
+ * every map a block of its own.  VD_ERR_SHAPE for larger maps. */
 int vd_conv3x3_wino4_mosaic_bias_act(const float *X, int N, int H, int W, int C, const float *U,
                                      int Cout, const float *bias, int relu, float *Y,
                                      void *stream);

@@ -66,7 +66,7 @@ def test_bench_batch_routes(bench_setup):
     assert modeling.conv3x3_route(BATCH, 256, 256, 100, 168) == ("wino4", "rows")
     assert modeling.conv3x3_route(BATCH, 256, 256, 25, 42) == ("wino", "2d")
     assert modeling.conv3x3_route(BATCH * 100, 256, 256, 14, 14) == ("wino4", "pair")
-    assert modeling.conv3x3_route(8000, 512, 512, 7, 7) == ("wino", "2d")  # C4 res5 head
+    assert modeling.conv3x3_route(8000, 512, 512, 7, 7) == ("wino4", "pair")  # C4 res5 head: octets
     assert routes.get("igemm", 0) == 0 and routes.get("miopen", 0) == 0, routes
     n_wino = routes.get("wino", 0) + routes.get("wino_rows", 0) + routes.get("wino_2d", 0)
     # F(4x4): FPN posthoc + RPN conv on P2-P4 (6) and the body's stride-1 conv2s, the

@@ -116,7 +116,7 @@ def test_winograd4_route_gate():
                  (32, 512, 512, 25, 42), (32, 256, 256, 200, 336), (32, 64, 64, 200, 336)]:
         assert r(*args) == ("wino4", "rows"), args
     assert abs(modeling._wino4_rows_use(32, 50, 84) - 32 * 50 * 84 / (104 * 16 * 96)) < 1e-12
-    for args in [(32, 256, 256, 25, 42), (32, 256, 256, 13, 21), (8000, 512, 512, 7, 7),
+    for args in [(32, 256, 256, 25, 42), (32, 256, 256, 13, 21), (1000, 512, 512, 7, 7),
                  (1, 256, 256, 200, 336), (32, 256, 96, 200, 336), (100, 256, 256, 14, 14)]:
         assert r(*args)[0] != "wino4", args
     # the mask head's RoI maps: F(4x4) two per block (>= 1024 workgroups, maps >= half
@@ -124,6 +124,8 @@ def test_winograd4_route_gate():
     assert r(3200, 256, 256, 14, 14) == ("wino4", "pair")
     assert r(1600, 256, 256, 14, 14) == ("wino4", "pair")
     assert r(3200, 256, 256, 14, 14, mosaic=False)[0] != "wino4"
+    # C4's res5 head: 7 x 7 maps eight per block (8 x 8 cells, 77 % real)
+    assert r(8000, 512, 512, 7, 7) == ("wino4", "pair")
     assert abs(modeling._wino4_block_use(25, 42) - 1050 / 2048) < 1e-12
     old = os.environ.get("VOSDET_WINO4")
     try:

@@ -129,3 +129,26 @@ def test_wino4_row_stack_bit_identical(N, C, H, W, Co):
     ref = F.relu(F.conv2d(x[:4], w, b, padding=1))
     err = float((y2[:4] - ref).abs().max())
     assert err <= 5e-5 * max(1., float(ref.abs().max())), err
+
+
+@pytest.mark.parametrize("N,C,H,W,Co", [(5, 64, 7, 7, 64), (17, 128, 6, 5, 64),
+                                        (9, 8, 1, 7, 64), (8000, 512, 7, 7, 512)])
+def test_wino4_octet_mosaic_bit_identical(N, C, H, W, Co):
+    """Maps of at most 7 x 7 run eight per block (8 x 8 cells) through
+    vd_conv3x3_wino4_mosaic_bias_act: == one map per block, incl. a last block with
+    fewer than eight maps; within the F(4x4) tolerance of torch."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(N + 3 * C + H * W)
+    x = torch.randn(N, C, H, W, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    w = torch.randn(Co, C, 3, 3, device="cuda", generator=g) / (3. * C ** .5)
+    b = torch.randn(Co, device="cuda", generator=g)
+    u = ops.conv3x3_wino4_weight(w)
+    y1 = ops.conv3x3_wino4_bias_act(x, u, b, relu=True)
+    y2 = ops.conv3x3_wino4_bias_act(x, u, b, relu=True, mosaic=True)
+    torch.cuda.synchronize()
+    assert y2 is not None
+    assert torch.equal(y1, y2), float((y1 - y2).abs().max())
+    ref = F.relu(F.conv2d(x[:64], w, b, padding=1))
+    err = float((y2[:64] - ref).abs().max())
+    assert err <= 5e-5 * max(1., float(ref.abs().max())), err

@@ -176,11 +176,13 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     // mos >= 4: row stack (vd_conv3x3_wino4_rows_bias_act) -- the N maps stacked at a
     // pitch of hp = mos >> 2 rows (a multiple of 4, > H: every tile inside one map's
     // pitch, the rows past a map zero), one image of N hp rows
-    const bool pair = mos == 1;
+    // mos == 3: octets -- maps of at most 7 x 7, eight per block in 8 x 8 cells (2 rows
+    // of 4), map n + 4 (y >> 3) + (x >> 3)
+    const bool pair = mos == 1, oct = mos == 3;
     const int hp = mos >> 2;
-    if (sp >= (pair ? (N + 1) >> 1 : (hp ? tby * tbx : N * tby * tbx))) return;
-    const int n = pair ? 2 * sp : (hp ? 0 : sp / (tby * tbx));
-    const int rem = pair ? 0 : sp - n * tby * tbx;
+    if (sp >= (pair ? (N + 1) >> 1 : oct ? (N + 7) >> 3 : (hp ? tby * tbx : N * tby * tbx))) return;
+    const int n = pair ? 2 * sp : oct ? 8 * sp : (hp ? 0 : sp / (tby * tbx));
+    const int rem = (pair || oct) ? 0 : sp - n * tby * tbx;
     const int tyb = rem / tbx, txb = rem - (rem / tbx) * tbx;
     const int oy0 = 4 * k4TR * tyb, ox0 = 4 * k4TC * txb;
     const int iy0 = oy0 - 1, ix0 = ox0 - 1;
@@ -212,11 +214,14 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
         const int Cc = 2 * m + (r5 >> 1), hf = r5 & 1;
         const int y = iy0 + R, x = ix0 + Cc;
         // mosaic: cell x >> 4 (map n + cell), column x & 15 of that map
-        const int cell = pair ? (x >> 4) : 0, xm = pair ? (x & 15) : x;
-        // row stack: map y / hp, its row y % hp
-        const int mr = (hp && y >= 0) ? y / hp : 0, ly = hp ? y - mr * hp : y;
+        const int cell = pair ? (x >> 4) : oct ? (x >> 3) : 0;
+        const int xm = pair ? (x & 15) : oct ? (x & 7) : x;
+        // row stack: map y / hp, its row y % hp (octets: map row 4 (y >> 3), row y & 7)
+        const int mr = (hp && y >= 0) ? y / hp : (oct && y >= 0) ? 4 * (y >> 3) : 0;
+        const int ly = hp ? y - mr * hp : oct ? (y & 7) : y;
         const bool ok = R < k4PR && r5 < 4 && Cc < k4PC && (unsigned)ly < (unsigned)H &&
-                        y >= 0 && x >= 0 && (unsigned)xm < (unsigned)W && n + cell + mr < N;
+                        y >= 0 && x >= 0 && (unsigned)xm < (unsigned)W && n + cell + mr < N &&
+                        (!oct || (cell < 4 && mr < 8));
         poff[kPS * k] = ok ? (uint32_t)((((cell + mr) * H + ly) * W + xm) * C + 4 * hf)
                            : 0x80000000u | (uint32_t)(4 * hf);
         srcp[k] = ok ? Xn + (((cell + mr) * H + ly) * W + xm) * C + 4 * hf : zero + 4 * hf;
@@ -519,12 +524,14 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int yv = oy0 + 4 * tr + i;
-        const int mr = hp ? yv / hp : 0, yy = hp ? yv - mr * hp : yv;
+        const int mr = hp ? yv / hp : oct ? 4 * (yv >> 3) : 0;
+        const int yy = hp ? yv - mr * hp : oct ? (yv & 7) : yv;
         if (yy >= H || n + mr >= N) continue;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int xc = ox0 + 4 * tc + k;
-            const int ncell = pair ? n + (xc >> 4) : n + mr, xx = pair ? (xc & 15) : xc;
+            const int ncell = pair ? n + (xc >> 4) : oct ? n + mr + (xc >> 3) : n + mr;
+            const int xx = pair ? (xc & 15) : oct ? (xc & 7) : xc;
             if (xx >= W || ncell >= N) continue;
             float4 v = make_float4(o[4 * i + k][0] + bv.x, o[4 * i + k][1] + bv.y,
                                    o[4 * i + k][2] + bv.z, o[4 * i + k][3] + bv.w);
@@ -902,6 +909,8 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
     // cell keeps a zero column / row after each map), 2 H W C floats of offsets < 2^31
     if (mos == 1 && (H > 15 || W > 15 || (int64_t)2 * H * W * C >= ((int64_t)1 << 31)))
         return VD_ERR_SHAPE;
+    if (mos == 1 && H <= 7 && W <= 7) mos = 3;  // octets: eight maps per block
+    if (mos == 3 && (int64_t)8 * H * W * C >= ((int64_t)1 << 31)) return VD_ERR_SHAPE;
     // the row stack: pitch = H + 1 rounded up to 4 (a zero row after every map), one
     // image whose offsets stay 32-bit
     const int hp = (H + 1 + 3) / 4 * 4;
@@ -910,9 +919,12 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
             return VD_ERR_SHAPE;
         mos = hp << 2;
     }
-    const int tby = mos == 1 ? 1 : ((mos ? N * hp : H) + 4 * k4TR - 1) / (4 * k4TR);
-    const int tbx = mos == 1 ? 1 : (W + 4 * k4TC - 1) / (4 * k4TC);
-    const int64_t nsp = mos == 1 ? ((int64_t)N + 1) / 2 : (int64_t)(mos ? 1 : N) * tby * tbx;
+    const bool cells = mos == 1 || mos == 3;
+    const int tby = cells ? 1 : ((mos ? N * hp : H) + 4 * k4TR - 1) / (4 * k4TR);
+    const int tbx = cells ? 1 : (W + 4 * k4TC - 1) / (4 * k4TC);
+    const int64_t nsp = mos == 1 ? ((int64_t)N + 1) / 2
+                                 : mos == 3 ? ((int64_t)N + 7) / 8
+                                            : (int64_t)(mos ? 1 : N) * tby * tbx;
     const int ncb = Cout / k4Co;
     // VOSDET_WINO4_CBX=0: the four channel blocks of a spatial block on one XCD (the
     // patch then comes from that XCD's L2 three times in four), not one channel block

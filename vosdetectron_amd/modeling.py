@@ -168,15 +168,19 @@ def _wino4_pair_ok(N: int, Cin: int, Cout: int, H: int, W: int) -> bool:
     """F(4x4) over small maps two per 16 x 32 block (vd_conv3x3_wino4_mosaic_bias_act;
     the mask head's 14 x 14 RoI maps: 77 % of each block real output; 2.43 vs 2.87 ms
     per 3200-map conv for F(2x2) on its 2-D mosaic, profiles/r05/wino4_pair/).  Maps
-    under half a 16 x 16 cell (C4's 7 x 7 res5 head) stay on the F(2x2) mosaic.
-    VOSDET_WINO4_MOSAIC=0 turns it off."""
+    of at most 7 x 7 (C4's res5 head) run eight per block in 8 x 8 cells
+    (VOSDET_WINO4_OCTET=0 keeps them on the F(2x2) mosaic).  VOSDET_WINO4_MOSAIC=0
+    turns both off."""
     if os.environ.get("VOSDET_WINO4_MOSAIC", "1") == "0" or os.environ.get("VOSDET_WINO4", "1") == "0":
         return False
     if Cout % 64 or Cin % 8 or Cout == 0 or Cin == 0 or Cin > ops.WINO_MAX_CIN:
         return False
-    if H > 15 or W > 15 or 2 * H * W * Cin >= (1 << 31) or H * W < 0.5 * 256:
+    cell, per = (8, 8) if (H <= 7 and W <= 7) else (16, 2)  # octets / pairs per block
+    if cell == 8 and os.environ.get("VOSDET_WINO4_OCTET", "1") == "0":
         return False
-    return -(-N // 2) * (Cout // 64) >= _WINO4_MIN_WGS
+    if H > 15 or W > 15 or per * H * W * Cin >= (1 << 31) or H * W < 0.5 * cell * cell:
+        return False
+    return -(-N // per) * (Cout // 64) >= _WINO4_MIN_WGS
 
 
 def conv3x3_route(N: int, Cin: int, Cout: int, H: int, W: int, mosaic=True):
