@@ -82,6 +82,15 @@ def test_miopen_db_is_a_per_process_copy():
     parent, child = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
                                    env=env, cwd=root, timeout=120).stdout.splitlines()
     assert parent != child and not os.path.exists(child)
+    # a child that inherited the parent's copy but set its own
+    # MIOPEN_USER_DB_PATH keeps that path
+    code = ("import os, subprocess, sys, vosdetectron_amd; env = dict(os.environ); "
+            "env['MIOPEN_USER_DB_PATH'] = '/tmp/vosdet_own_db'; "
+            "subprocess.run([sys.executable, '-c', 'import os, vosdetectron_amd; "
+            "print(os.environ[\\'MIOPEN_USER_DB_PATH\\'])'], env=env)")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         env=env, cwd=root, timeout=120).stdout.splitlines()
+    assert out == ["/tmp/vosdet_own_db"], out
 
 
 @pytest.mark.gpu

@@ -85,3 +85,17 @@ def test_fpn_lateral_graph_replay_bit_identical():
         torch.cuda.synchronize()
         assert torch.equal(out, eager)
     _check(eager, ref)
+
+
+def test_fpn_lateral_module_follows_reloaded_weights():
+    """weights loaded after prepare (load_state_dict) reach the fused
+    path: the packed lateral weight is keyed by the live weight and repacked."""
+    from vosdetectron_amd import modeling
+    m = modeling.TopdownLateral(256, 256).to(DEV)
+    modeling.prepare_topdown_lateral(m)
+    assert m._vd_wf is not None  # K = 256: the default fused width
+    lat, w, b, t, ref = _case(2, 256, 40, 56, 11)
+    with torch.no_grad():
+        m.conv_lateral.weight.copy_(torch.randn_like(w))
+        m.load_state_dict({"conv_lateral.weight": w, "conv_lateral.bias": b})
+        _check(m(t, lat), ref)

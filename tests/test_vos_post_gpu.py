@@ -203,3 +203,37 @@ def test_vos_heuristics_refuse_unfinalized_steps(vos_seq):
         frame_segms(pipe, out, int(cfg.MODEL.NUM_CLASSES))
     pipe.frame_results(out)
     pipe.frame_results(pipe.run(torch.from_numpy(frames[1]).to(DEV)))  # now allowed
+    # a dropped step followed by a reset of every row starts new
+    # sequences, so the guard no longer applies; a partial reset keeps it
+    pipe.run(torch.from_numpy(frames[0]).to(DEV))
+    pipe.reset(rows=[0])
+    with pytest.raises(RuntimeError, match="frame_results"):
+        pipe.run(torch.from_numpy(frames[1]).to(DEV))
+    pipe.reset(rows=[0, 1])
+    pipe.frame_results(pipe.run(torch.from_numpy(frames[1]).to(DEV)))
+    pipe.run(torch.from_numpy(frames[2]).to(DEV))
+    pipe.reset()
+    pipe.frame_results(pipe.run(torch.from_numpy(frames[0]).to(DEV)))
+
+
+def test_prev_box_filter_keeps_failed_counts():
+    """a frame an upstream kernel failed (count -1, e.g. an
+    unbracketable proposal select) keeps its code through the previous-frame
+    filter instead of becoming an empty frame, and its rows are untouched."""
+    from vosdetectron_amd import _lib, ops
+    D = torch.rand((3, 8, 5), device=DEV) * 100
+    D[..., 2:4] += D[..., 0:2]
+    C = torch.tensor([[1, 1, 2, 3, 3, 3, 4, 5]] * 3, dtype=torch.int32, device=DEV)
+    N = torch.tensor([-1, 8, ops.COUNT_PREV_BOXES], dtype=torch.int32, device=DEV)
+    D0, C0 = D.clone(), C.clone()
+    PD = D.clone()[:, :4].contiguous()
+    PC = torch.tensor([[1, 2, 0, 0], [3, 0, 0, 0], [1, 2, 0, 0]], dtype=torch.int32, device=DEV)
+    PN = torch.tensor([2, 1, 2], dtype=torch.int32, device=DEV)
+    ops.detections_prev_box_filter(D, C, N, PD, PC, PN, 0.3, 0.0)
+    got = N.cpu().tolist()
+    assert got[0] == -1 and got[2] == ops.COUNT_PREV_BOXES
+    assert 0 <= got[1] <= 8
+    assert torch.equal(D[0], D0[0]) and torch.equal(C[0], C0[0])
+    assert torch.equal(D[2], D0[2]) and torch.equal(C[2], C0[2])
+    with pytest.raises(_lib.VosdetError):
+        ops.raise_on_failed_counts(got)

@@ -16,30 +16,39 @@ os.environ.setdefault("MIOPEN_FIND_MODE", "1")
 # so problems not in it are found and appended to the copy -- eight ranks never
 # write one shared file and no run dirties the repository.
 # A caller's own MIOPEN_USER_DB_PATH wins (VOSDET_MIOPEN_DB_SEED=0: no seed).  The
-# copy's owner PID travels with it (VOSDET_MIOPEN_DB_OWNER): a child process that
-# inherits the variable (a rank spawned by an importing parent) makes its own copy
-# instead of sharing the parent's, which the parent deletes at exit.
+# copy's owner PID and path travel with it (VOSDET_MIOPEN_DB_OWNER / _COPY): a child
+# process that inherits a parent's copy (a rank spawned by an importing parent) makes
+# its own instead of sharing the one the parent deletes at exit -- but only while
+# MIOPEN_USER_DB_PATH still names that copy; a path the child set itself wins.
 
 
 def _seed_miopen_db():
     if os.environ.get("VOSDET_MIOPEN_DB_SEED") == "0":
         return
-    owner = os.environ.get("VOSDET_MIOPEN_DB_OWNER")
-    if "MIOPEN_USER_DB_PATH" in os.environ and (owner is None or owner == str(os.getpid())):
-        return  # the caller's own path, or this process's copy
+    cur = os.environ.get("MIOPEN_USER_DB_PATH")
+    if cur is not None:
+        owner = os.environ.get("VOSDET_MIOPEN_DB_OWNER")
+        ours = owner is not None and cur == os.environ.get("VOSDET_MIOPEN_DB_COPY")
+        if not ours or owner == str(os.getpid()):
+            return  # the caller's own path, or this process's copy
     import atexit
     import shutil
     import tempfile
     seed = os.path.join(os.path.dirname(os.path.abspath(__file__)), "miopen_db")
     try:
         d = tempfile.mkdtemp(prefix="vosdet_miopen_db_")
+    except OSError:
+        return  # no writable temp dir: MIOpen uses its own default location
+    atexit.register(shutil.rmtree, d, True)  # before the copy: a failed copy leaks nothing
+    try:
         for name in os.listdir(seed):
             shutil.copy2(os.path.join(seed, name), os.path.join(d, name))
     except OSError:
-        return  # no writable temp dir: MIOpen uses its own default location
-    atexit.register(shutil.rmtree, d, True)
+        shutil.rmtree(d, True)
+        return
     os.environ["MIOPEN_USER_DB_PATH"] = d
     os.environ["VOSDET_MIOPEN_DB_OWNER"] = str(os.getpid())
+    os.environ["VOSDET_MIOPEN_DB_COPY"] = d
 
 
 _seed_miopen_db()

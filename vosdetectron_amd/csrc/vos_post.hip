@@ -211,7 +211,12 @@ __global__ __launch_bounds__(1024) void prev_box_filter_kernel(
     int det_cap, const float *__restrict__ prev_dets, const int32_t *__restrict__ prev_classes,
     const int32_t *__restrict__ prev_counts, int prev_cap, float iou_thresh, float score_thresh) {
     const int f = blockIdx.x, t = threadIdx.x;
-    const int n = counts[f] > 0 ? min(counts[f], det_cap) : 0;
+    // A frame an upstream kernel already failed (negative count) keeps its code:
+    // propagate, never hide (vosdet.h).  Every thread reads it before thread 0's
+    // only write below, so the whole workgroup leaves together.
+    const int c0 = counts[f];
+    if (c0 < 0) return;
+    const int n = min(c0, det_cap);
     const int np_ = prev_counts[f] > 0 ? min(prev_counts[f], prev_cap) : 0;
     float *d = dets + (int64_t)f * det_cap * 5;
     int32_t *c = classes + (int64_t)f * det_cap;

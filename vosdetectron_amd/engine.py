@@ -346,11 +346,14 @@ class VOSPipeline(FramePipeline):
 
     def reset(self, rows=None):
         """Zero the hidden states (and forget the previous-frame results) of batch
-        rows `rows` (all when None)."""
+        rows `rows` (all when None).  Resetting every row also drops the pending
+        'unfinalized step' guard: no row's next frame reads that result any more."""
         if rows is None:
             self.prev_counts.zero_()
         else:
             self.prev_counts[list(rows)] = 0
+        if rows is None or set(range(self.prev_counts.shape[0])) <= set(int(r) for r in rows):
+            self._unfinalized = False
         hs = self.model.hidden_states
         if rows is None or all(h is None for h in hs):
             self.model.clean_hidden_states()

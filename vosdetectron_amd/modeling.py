@@ -570,6 +570,14 @@ class TopdownLateral(nn.Module):
                                res=top, up=True)
             c = self.conv_lateral
             wf = getattr(self, "_vd_wf", None)
+            if wf is not None:
+                # the packed weight follows the live one (a load_state_dict after
+                # prepare_fpn_body), as the Winograd routes' U keys do
+                w = c.weight
+                key = (w.data_ptr(), w._version)
+                if self._vd_wf_key != key:
+                    wf = self._vd_wf = ops.fpn_lateral_weight(w.detach())
+                    self._vd_wf_key = key
             if wf is not None and _gemm_ok(lateral) and top.shape[2] * 2 == lateral.shape[2] \
                     and top.shape[3] * 2 == lateral.shape[3]:
                 # the lateral 1x1, its bias and the nearest-2x top-down add in one
@@ -1078,17 +1086,24 @@ def _fpn_lateral_fused_k():
     return tuple(int(k) for k in v.split(","))
 
 
+def prepare_topdown_lateral(m: TopdownLateral, epilogue: bool = True):
+    """One top-down lateral module: the fused-lateral weight (fragment order, keyed
+    by the live weight so a later load_state_dict repacks it) and the epilogue flag."""
+    m._vd_wf = m._vd_wf_key = None
+    c = m.conv_lateral
+    if epilogue and not m.use_gn and c.weight.is_cuda and _is_1x1(c) and c.stride == (1, 1) \
+            and c.bias is not None and c.in_channels in _fpn_lateral_fused_k():
+        m._vd_wf = ops.fpn_lateral_weight(c.weight.detach())
+        m._vd_wf_key = (c.weight.data_ptr(), c.weight._version)
+    m.epilogue = epilogue
+
+
 def prepare_fpn_body(fpn: FPNBody, epilogue: bool = True):
     """Inference-time rewrite of an FPNBody: AffineChannel2d folded into the
     convs (BN bodies) and the fused HIP epilogues switched on."""
     prepare_resnet_body(fpn.conv_body, epilogue)
     for m in fpn.topdown_lateral_modules:
-        m._vd_wf = None
-        c = m.conv_lateral
-        if epilogue and not m.use_gn and c.weight.is_cuda and _is_1x1(c) and c.stride == (1, 1) \
-                and c.bias is not None and c.in_channels in _fpn_lateral_fused_k():
-            m._vd_wf = ops.fpn_lateral_weight(c.weight.detach())
-        m.epilogue = epilogue
+        prepare_topdown_lateral(m, epilogue)
     fpn.epilogue = epilogue
     return fpn
 
