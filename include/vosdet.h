@@ -163,6 +163,26 @@ int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const 
                      const float *residual, int relu, float *D, void *workspace,
                      size_t workspace_bytes, void *stream);
 
+/* The same GEMM (D[M][N] = act(A[M][K] . W[N][K]^T + bias[N] (+ R[M][N])), fp32
+ * in and out) on the bf16 matrix cores at fp32 accuracy: every operand is split
+ * into three bf16 pieces carrying its 24-bit significand and the six largest piece
+ * products are accumulated in fp32 (csrc/gemm_split3.hip; error measured against
+ * fp64 beside torch's fp32 GEMM in tests/test_gemm_split3_gpu.py).  Wp is the
+ * weight in split form, vd_gemm_split3_weight_size(N, K) bytes, made once per
+ * model by vd_gemm_split3_weight.  K a multiple of 32, N of 64 (VD_ERR_SHAPE
+ * otherwise); residual may be NULL.  up_h, up_w > 0 (both even): residual is the
+ * top-down map of an FPN level, images x up_h/2 x up_w/2 x N, added at the nearest-2x
+ * row of each of the M = images x up_h x up_w pixels after the bias -- the FPN
+ * top-down lateral step (FPN.py:292-300) in one launch.  cfg 0 picks the tile shape (1: 256 pixels x
+ * 128 channels, 2: 256 x 64, 3: 128 x 256 per workgroup).  Replaces the same
+ * fp32 convolutions / Linear layers as vd_gemm_bias_act (ResNet.py:246-294
+ * bottleneck 1x1s, fast_rcnn_heads.py fc6 / fc7, mask_rcnn_heads.py upconv5). */
+size_t vd_gemm_split3_weight_size(int N, int K);
+int vd_gemm_split3_weight(const float *W, int N, int K, void *Wp, void *stream);
+int vd_gemm_split3_bias_act(const float *A, int M, int K, const void *Wp, int N,
+                            const float *bias, const float *residual, int up_h, int up_w,
+                            int relu, float *D, int cfg, void *stream);
+
 /* 3x3 stride-1 pad-1 convolution of a channels_last (NHWC) fp32 tensor with
  * the bias (+ ReLU) epilogue fused, one hand-written MFMA implicit-GEMM kernel:
  * Y[n][y][x][co] = act(sum_{ky,kx,ci} X[n][y+ky-1][x+kx-1][ci] W2[co][ky][kx][ci]

@@ -75,8 +75,14 @@ def test_bench_batch_routes(bench_setup):
     assert routes.get("wino4_rows", 0) >= 10, routes  # P3 / P4 posthoc + RPN, res3 / res4 conv2s
     assert routes.get("wino4_pair", 0) == 4, routes
     assert n_wino >= 3 and routes.get("wino_2d", 0) >= 3, routes
-    # the P2 top-down lateral step as one fused MFMA launch (modeling._fpn_lateral_fused_k)
-    assert routes.get("fpn_lateral", 0) == 1, routes
+    # the P2-P4 top-down lateral steps each as one launch with the nearest-2x add fused:
+    # on the bf16 matrix cores at fp32 accuracy (split3), or with VOSDET_GEMM_SPLIT3=0
+    # P2 on the fp32 MFMA kernel (modeling._fpn_lateral_fused_k)
+    from vosdetectron_amd import ops
+    if ops.split3_enabled():
+        assert routes.get("fpn_lateral_split3", 0) == 3, routes
+    else:
+        assert routes.get("fpn_lateral", 0) == 1, routes
 
 
 @pytest.mark.parametrize("f", [0, 7, BATCH - 1])

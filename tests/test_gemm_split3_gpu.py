@@ -1,0 +1,155 @@
+"""The split-bf16 GEMM (csrc/gemm_split3.hip, vd_gemm_split3_bias_act): fp32
+operands split into three bf16 pieces, the six largest piece products accumulated
+in fp32 on the bf16 matrix cores.  Its accuracy claim is "fp32's": on every shape
+the error against an fp64 reference stays within 2x of torch's own fp32 GEMM
+error (max and mean), and within the 2e-5 relative bound the fp32 GEMM tests use.
+Also: every tile configuration, ragged pixel counts, residual / ReLU epilogues,
+determinism, graph replay, the weight cache following in-place updates, and the
+routing rule of ops.gemm_bias_act."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _case(M, N, K, res, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    a = torch.randn(M, K, device=DEV, generator=g).relu_()
+    w = torch.randn(N, K, device=DEV, generator=g) / K ** .5
+    b = torch.randn(N, device=DEV, generator=g) * .1
+    r = torch.randn(M, N, device=DEV, generator=g) if res else None
+    return a, w, b, r
+
+
+def _ref64(a, w, b, r, relu):
+    y = a.double() @ w.double().t() + b.double()
+    if r is not None:
+        y = y + r.double()
+    return y.relu() if relu else y
+
+
+def _errs(got, ref):
+    e = (got.double() - ref).abs()
+    s = float(ref.abs().max())
+    return float(e.max()) / s, float(e.mean()) / s
+
+
+@pytest.mark.parametrize("M,N,K,res,relu", [
+    (1000, 64, 256, False, True), (777, 128, 512, True, True), (4099, 256, 1024, False, False),
+    (3000, 512, 2048, True, True), (2048, 1024, 256, False, True), (513, 2048, 512, True, False),
+    (333, 1024, 12544, False, True), (64, 64, 16, False, True), (1, 256, 32, True, True)])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+def test_split3_fp32_accuracy(M, N, K, res, relu, cfg):
+    from vosdetectron_amd import ops
+    if (cfg == 1 and N % 256) or (cfg == 2 and N % 128):
+        pytest.skip("tile needs N %% %d" % (256 if cfg == 1 else 128))
+    a, w, b, r = _case(M, N, K, res, M + N + K)
+    ref = _ref64(a, w, b, r, relu)
+    got = ops.gemm_split3_bias_act(a, ops.gemm_split3_weight(w), b, residual=r, relu=relu,
+                                   cfg=cfg)
+    t32 = a @ w.t() + b
+    if r is not None:
+        t32 = t32 + r
+    if relu:
+        t32 = t32.relu()
+    torch.cuda.synchronize()
+    mx, mean = _errs(got, ref)
+    tmx, tmean = _errs(t32, ref)
+    assert mx <= 2e-5, mx
+    assert mx <= 2 * tmx + 1e-7 and mean <= 2 * tmean + 1e-9, (mx, mean, tmx, tmean)
+
+
+def test_split3_deterministic_and_graph_replay():
+    from vosdetectron_amd import ops
+    a, w, b, r = _case(5000, 256, 512, True, 5)
+    wp = ops.gemm_split3_weight(w)
+    y0 = ops.gemm_split3_bias_act(a, wp, b, residual=r)
+    y1 = ops.gemm_split3_bias_act(a, wp, b, residual=r)
+    assert torch.equal(y0, y1)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            out = ops.gemm_split3_bias_act(a, wp, b, residual=r)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, y0)
+
+
+def test_gemm_bias_act_routes_and_cache():
+    """K >= SPLIT3_MIN_K runs split (matches the direct split call bit for bit);
+    the cached split image follows an in-place weight update; VOSDET_GEMM_SPLIT3=0
+    and K below the threshold keep the fp32 kernels (within 2e-5 of torch)."""
+    import os
+    from vosdetectron_amd import ops
+    a, w, b, _ = _case(3000, 256, 512, False, 9)
+    y = ops.gemm_bias_act(a, w, b, relu=True)
+    assert torch.equal(y, ops.gemm_split3_bias_act(a, ops.gemm_split3_weight(w), b))
+    with torch.no_grad():
+        w.mul_(0.5)
+    y2 = ops.gemm_bias_act(a, w, b, relu=True)
+    ref = (a @ w.t() + b).relu()
+    torch.cuda.synchronize()
+    assert float((y2 - ref).abs().max()) <= 2e-5 * float(ref.abs().max())
+    os.environ["VOSDET_GEMM_SPLIT3"] = "0"
+    try:
+        y3 = ops.gemm_bias_act(a, w, b, relu=True)
+    finally:
+        del os.environ["VOSDET_GEMM_SPLIT3"]
+    torch.cuda.synchronize()
+    assert float((y3 - ref).abs().max()) <= 2e-5 * float(ref.abs().max())
+    assert not torch.equal(y3, y2)  # the fp32 kernels sum in another order
+
+
+def test_split3_rejects_bad_shapes():
+    from vosdetectron_amd import _lib, ops
+    assert ops.gemm_split3_weight(torch.randn(96, 64, device=DEV)) is None   # N % 64
+    assert ops.gemm_split3_weight(torch.randn(64, 40, device=DEV)) is None   # K % 16
+    wp = ops.gemm_split3_weight(torch.randn(128, 64, device=DEV))
+    with pytest.raises(ValueError):
+        ops.gemm_split3_bias_act(torch.randn(10, 32, device=DEV), wp, torch.zeros(128, device=DEV))
+    with pytest.raises(_lib.VosdetError):  # a 256-channel tile on N = 128
+        ops.gemm_split3_bias_act(torch.randn(10, 64, device=DEV), wp,
+                                 torch.zeros(128, device=DEV), cfg=1)
+
+
+@pytest.mark.parametrize("n,K,H,W", [(2, 256, 16, 20), (3, 512, 10, 14), (1, 1024, 6, 8),
+                                     (32, 256, 200, 336)])
+def test_split3_fpn_topdown_lateral(n, K, H, W):
+    """The FPN top-down step (FPN.py:292-300: conv_lateral(lateral) + nearest-2x
+    upsample of top) in one split-bf16 launch, vs fp64 (and within 2x of torch
+    fp32's own error); through the module (modeling.TopdownLateral) as well."""
+    import torch.nn.functional as F
+    from vosdetectron_amd import modeling, ops
+    g = torch.Generator(device="cuda").manual_seed(K + H)
+    lat = torch.randn(n, K, H, W, device=DEV, generator=g).contiguous(
+        memory_format=torch.channels_last)
+    w = torch.randn(256, K, 1, 1, device=DEV, generator=g) / K ** .5
+    b = torch.randn(256, device=DEV, generator=g)
+    top = torch.randn(n, 256, H // 2, W // 2, device=DEV, generator=g).contiguous(
+        memory_format=torch.channels_last)
+    rows = min(n * H * W, 20000)
+    a2 = lat.permute(0, 2, 3, 1).reshape(-1, K)
+    up = F.interpolate(top, scale_factor=2, mode="nearest").permute(0, 2, 3, 1).reshape(-1, 256)
+    ref = (a2[:rows].double() @ w.view(256, K).double().t() + b.double()) + up[:rows].double()
+    got = ops.gemm_split3_bias_act(a2, ops.gemm_split3_weight(w.view(256, K)), b,
+                                   residual=top.permute(0, 2, 3, 1).reshape(-1, 256),
+                                   relu=False, up_hw=(H, W))
+    t32 = F.conv2d(lat, w, b) + F.interpolate(top, scale_factor=2, mode="nearest")
+    torch.cuda.synchronize()
+    mx, _ = _errs(got[:rows], ref)
+    tmx, _ = _errs(t32.permute(0, 2, 3, 1).reshape(-1, 256)[:rows], ref)
+    assert mx <= 2e-5 and mx <= 2 * tmx + 1e-7, (mx, tmx)
+    m = modeling.TopdownLateral(256, K).to(DEV)
+    with torch.no_grad():
+        m.conv_lateral.weight.copy_(w)
+        m.conv_lateral.bias.copy_(b)
+    modeling.prepare_topdown_lateral(m)
+    y = m(top, lat)
+    torch.cuda.synchronize()
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(y.permute(0, 2, 3, 1).reshape(-1, 256), got)
+    del lat, top, got, t32, y

@@ -131,6 +131,24 @@ int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const 
                                 workspace_bytes, VD_STREAM(stream));
 }
 
+size_t vd_gemm_split3_weight_size(int N, int K) {
+    return (N > 0 && K > 0 && gemm_split3_supported(K, N)) ? gemm_split3_weight_bytes(N, K) : 0;
+}
+
+int vd_gemm_split3_weight(const float *W, int N, int K, void *Wp, void *stream) {
+    if (N < 1 || K < 1 || !W || !Wp) return VD_ERR_ARG;
+    return launch_gemm_split3_weight(W, N, K, Wp, VD_STREAM(stream));
+}
+
+int vd_gemm_split3_bias_act(const float *A, int M, int K, const void *Wp, int N,
+                            const float *bias, const float *residual, int up_h, int up_w, int relu,
+                            float *D, int cfg, void *stream) {
+    if (M < 0 || K < 1 || N < 1 || !Wp || !bias || !D || (M > 0 && !A) || cfg < 0 || cfg > 13)
+        return VD_ERR_ARG;
+    return launch_gemm_split3(A, M, K, Wp, N, bias, residual, up_h, up_w, relu, D, cfg,
+                              VD_STREAM(stream));
+}
+
 int vd_conv3x3_bias_act(const float *X, int N, int H, int W, int C, const float *W2, int Cout,
                         const float *bias, int relu, float *Y, void *stream) {
     if (N < 0 || H < 1 || W < 1 || C < 1 || Cout < 1 || !W2 || !Y || (N > 0 && !X))

@@ -56,6 +56,12 @@ int gemm_plan_list(char *buf, int n);
 int launch_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const float *bias,
                          const float *R, int relu, float *D, void *ws, size_t ws_bytes,
                          hipStream_t s);
+bool gemm_split3_supported(int K, int N);
+size_t gemm_split3_weight_bytes(int N, int K);
+int launch_gemm_split3_weight(const float *W, int N, int K, void *Wp, hipStream_t s);
+int launch_gemm_split3(const float *A, int M, int K, const void *Wp, int N, const float *bias,
+                       const float *R, int up_h, int up_w, int relu, float *D, int cfg,
+                       hipStream_t s);
 bool gemm1x1_mfma_supported(int K, int N);
 bool conv3x3_mfma_supported(int C, int Cout);
 int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float *W2, int Cout,

@@ -569,6 +569,25 @@ class TopdownLateral(nn.Module):
                 return _gn_epi(self.conv_lateral[0], self.conv_lateral[1], lateral, act=None,
                                res=top, up=True)
             c = self.conv_lateral
+            w2d = getattr(self, "_vd_w2d", None)
+            if w2d is None or w2d.data_ptr() != c.weight.data_ptr():
+                # one persistent 2-D view of the weight (ops caches its split image)
+                w2d = self._vd_w2d = c.weight.reshape(c.out_channels, -1)
+            if ops.split3_enabled() and c.in_channels >= ops.SPLIT3_MIN_K and \
+                    c.out_channels % 64 == 0 and c.bias is not None and _is_1x1(c) and \
+                    c.stride == (1, 1) and _gemm_ok(lateral) and top.is_cuda and \
+                    top.shape[2] * 2 == lateral.shape[2] and top.shape[3] * 2 == lateral.shape[3]:
+                # the lateral 1x1, its bias and the nearest-2x top-down add in one launch
+                # on the bf16 matrix cores at fp32 accuracy (csrc/gemm_split3.hip)
+                wp = ops.split3_weight_cached(w2d)
+                if wp is not None:
+                    n, _, H, W = lateral.shape
+                    t = top if top.is_contiguous(memory_format=torch.channels_last) else \
+                        top.contiguous(memory_format=torch.channels_last)
+                    y = ops.gemm_split3_bias_act(_nhwc2d(lateral), wp, c.bias,
+                                                 residual=_nhwc2d(t), relu=False, up_hw=(H, W))
+                    _count_route("fpn_lateral_split3")
+                    return y.view(n, H, W, -1).permute(0, 3, 1, 2)
             wf = getattr(self, "_vd_wf", None)
             if wf is not None:
                 # the packed weight follows the live one (a load_state_dict after
@@ -588,8 +607,7 @@ class TopdownLateral(nn.Module):
                 # the lateral 1x1 as a GEMM with its bias fused, then the nearest-2x
                 # top-down add (MIOpen / CK took it before; at small batches their
                 # solvers were not run-to-run deterministic)
-                y = _gemm_conv1x1(lateral, c.weight.reshape(c.out_channels, -1), c.bias,
-                                  relu=False)
+                y = _gemm_conv1x1(lateral, w2d, c.bias, relu=False)
                 return ops.bias_act_(y, None, top, relu=False, upsample_residual=True)
             return _conv_epi(c, lateral, relu=False, res=top, up=True)
         return self.conv_lateral(lateral) + F.interpolate(top, scale_factor=2, mode="nearest")

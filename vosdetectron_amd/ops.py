@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from typing import Optional, Sequence
 
 import numpy as np
@@ -535,13 +536,45 @@ def gemm_plan_list() -> list:
     return rows
 
 
+# K from which a GEMM with a split-bf16 route runs it there (gemm_split3_bias_act):
+# below it the GEMMs are HBM-bound and the fp32 kernels are as fast
+# (profiles/r06/gemm_split3/)
+SPLIT3_MIN_K = 256
+# id(weight tensor) -> (weakref to it, key, split image); an entry leaves with its tensor
+_split3_cache = {}
+
+
+def split3_enabled() -> bool:
+    """VOSDET_GEMM_SPLIT3=0 keeps every GEMM on the fp32-MFMA kernels (A/B runs)."""
+    return os.environ.get("VOSDET_GEMM_SPLIT3", "1") != "0"
+
+
+def split3_weight_cached(w: torch.Tensor) -> Optional[torch.Tensor]:
+    """gemm_split3_weight(w), made once per weight tensor and remade when the tensor
+    changes (its storage or version counter: an in-place update, load_state_dict)."""
+    key = (w.data_ptr(), w._version, tuple(w.shape))
+    i = id(w)
+    ent = _split3_cache.get(i)
+    if ent is not None and ent[0]() is w and ent[1] == key:
+        return ent[2]
+    def _drop(r, i=i):
+        if _split3_cache.get(i, (None,))[0] is r:
+            del _split3_cache[i]
+    ref = weakref.ref(w, _drop)
+    wp = gemm_split3_weight(w)
+    _split3_cache[i] = (ref, key, wp)
+    return wp
+
+
 def gemm_bias_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
                   residual: Optional[torch.Tensor] = None, relu: bool = True,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """act(a @ w.T + bias (+ residual)) in one GEMM launch (vd_gemm_bias_act: hipBLASLt
-    with the epilogue fused, or the hand-written MFMA kernel where it is faster):
-    a [M,K], w [N,K], bias [N], residual / out [M,N], all fp32 contiguous.  Returns
-    None when neither serves the shape (the caller falls back)."""
+    """act(a @ w.T + bias (+ residual)) in one GEMM launch: a [M,K], w [N,K], bias [N],
+    residual / out [M,N], all fp32 contiguous.  From K = SPLIT3_MIN_K (N a multiple
+    of 64) on the bf16 matrix cores at fp32 accuracy (gemm_split3_bias_act, the
+    weight's split image cached per tensor); otherwise vd_gemm_bias_act (hipBLASLt
+    with the epilogue fused, or the hand-written fp32 MFMA kernel where it is
+    faster).  Returns None when nothing serves the shape (the caller falls back)."""
     a_ = _need(a, "a")
     w_ = _need(w, "w")
     b_ = _need(bias, "bias")
@@ -559,6 +592,10 @@ def gemm_bias_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
         out = torch.empty((M, N), dtype=torch.float32, device=a_.device)
     elif tuple(out.shape) != (M, N) or not out.is_contiguous():
         raise ValueError("out must be a contiguous %s tensor" % ((M, N),))
+    if K >= SPLIT3_MIN_K and N % 64 == 0 and K % 16 == 0 and M > 0 and split3_enabled():
+        wp = split3_weight_cached(w if w.is_contiguous() else w_)
+        if wp is not None:
+            return gemm_split3_bias_act(a_, wp, b_, residual=r_, relu=relu, out=out)
     ws = gemm_workspace(a_.device)
     st = lib().vd_gemm_bias_act(a_.data_ptr(), M, K, w_.data_ptr(), N, b_.data_ptr(),
                                 r_.data_ptr() if r_ is not None else None, int(relu),
@@ -566,6 +603,61 @@ def gemm_bias_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
     if st == VD_ERR_SHAPE:  # no hipBLASLt algorithm and no MFMA kernel for the shape
         return None
     check(st, "vd_gemm_bias_act")
+    return out
+
+
+def gemm_split3_weight(w: torch.Tensor) -> Optional[torch.Tensor]:
+    """W [N, K] fp32 (a 1x1 conv / Linear weight) -> the three-piece bf16 split image
+    vd_gemm_split3_bias_act reads (once per model; N * K * 6 bytes).  None when the
+    shape is not served (K a multiple of 32, N of 64)."""
+    w_ = _need(w.reshape(w.shape[0], -1), "w")
+    N, K = w_.shape
+    nbytes = lib().vd_gemm_split3_weight_size(N, K)
+    if not nbytes:
+        return None
+    wp = torch.empty(nbytes, dtype=torch.uint8, device=w_.device)
+    check(lib().vd_gemm_split3_weight(w_.data_ptr(), N, K, wp.data_ptr(), _stream()),
+          "vd_gemm_split3_weight")
+    wp.split3_shape = (N, K)
+    return wp
+
+
+def gemm_split3_bias_act(a: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor,
+                         residual: Optional[torch.Tensor] = None, relu: bool = True,
+                         out: Optional[torch.Tensor] = None, cfg: int = 0,
+                         up_hw: Optional[Sequence[int]] = None) -> torch.Tensor:
+    """act(a @ w.T + bias (+ residual)) with the fp32 operands split into three bf16
+    pieces on the bf16 matrix cores (vd_gemm_split3_bias_act, fp32 accuracy):
+    a [M,K], wp from gemm_split3_weight(w [N,K]), bias [N], out [M,N]; residual
+    [M,N], or with up_hw = (H, W) the top-down map [M / (H W), H/2, W/2, N] of an
+    FPN level added at the nearest-2x row of each pixel (FPN.py:292-300)."""
+    a_ = _need(a, "a")
+    N, K = wp.split3_shape
+    M = a_.shape[0]
+    b_ = _need(bias, "bias")
+    if a_.dim() != 2 or a_.shape[1] != K or b_.numel() != N:
+        raise ValueError("gemm_split3_bias_act: a %s, w (%d, %d), bias %s"
+                         % (tuple(a_.shape), N, K, tuple(b_.shape)))
+    r_ = None
+    uh = uw = 0
+    if residual is not None:
+        r_ = _need(residual, "residual")
+        if up_hw is not None:
+            uh, uw = int(up_hw[0]), int(up_hw[1])
+            if uh % 2 or uw % 2 or uh < 2 or uw < 2 or M % (uh * uw) or \
+                    r_.numel() != (M // 4) * N:
+                raise ValueError("top-down map %s does not match %d pixels of %s maps"
+                                 % (tuple(r_.shape), M, (uh, uw)))
+        elif tuple(r_.shape) != (M, N):
+            raise ValueError("residual must be %s, got %s" % ((M, N), tuple(r_.shape)))
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a_.device)
+    elif tuple(out.shape) != (M, N) or not out.is_contiguous():
+        raise ValueError("out must be a contiguous %s tensor" % ((M, N),))
+    check(lib().vd_gemm_split3_bias_act(a_.data_ptr(), M, K, wp.data_ptr(), N, b_.data_ptr(),
+                                        r_.data_ptr() if r_ is not None else None, uh, uw,
+                                        int(relu), out.data_ptr(), int(cfg), _stream()),
+          "vd_gemm_split3_bias_act")
     return out
 
 
