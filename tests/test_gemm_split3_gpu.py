@@ -1,8 +1,9 @@
 """The split-bf16 GEMM (csrc/gemm_split3.hip, vd_gemm_split3_bias_act): fp32
 operands split into three bf16 pieces, the six largest piece products accumulated
 in fp32 on the bf16 matrix cores.  Its accuracy claim is "fp32's": on every shape
-the error against an fp64 reference stays within 2x of torch's own fp32 GEMM
-error (max and mean), and within the 2e-5 relative bound the fp32 GEMM tests use.
+the error against an fp64 reference stays at torch's own fp32 GEMM error (mean
+within 1.5x, max within 3x: the max of a few hundred rows is a noisy statistic)
+and within the 2e-5 relative bound the fp32 GEMM tests use.
 Also: every tile configuration, ragged pixel counts, residual / ReLU epilogues,
 determinism, graph replay, the weight cache following in-place updates, and the
 routing rule of ops.gemm_bias_act."""
@@ -57,7 +58,7 @@ def test_split3_fp32_accuracy(M, N, K, res, relu, cfg):
     mx, mean = _errs(got, ref)
     tmx, tmean = _errs(t32, ref)
     assert mx <= 2e-5, mx
-    assert mx <= 2 * tmx + 1e-7 and mean <= 2 * tmean + 1e-9, (mx, mean, tmx, tmean)
+    assert mx <= 3 * tmx + 1e-7 and mean <= 1.5 * tmean + 1e-9, (mx, mean, tmx, tmean)
 
 
 def test_split3_deterministic_and_graph_replay():
@@ -138,11 +139,14 @@ def test_split3_fpn_topdown_lateral(n, K, H, W):
     got = ops.gemm_split3_bias_act(a2, ops.gemm_split3_weight(w.view(256, K)), b,
                                    residual=top.permute(0, 2, 3, 1).reshape(-1, 256),
                                    relu=False, up_hw=(H, W))
-    t32 = F.conv2d(lat, w, b) + F.interpolate(top, scale_factor=2, mode="nearest")
+    # torch's fp32 GEMM of the same sum (MIOpen's conv2d can reduce K in a tree, a
+    # different error class from any K-ordered GEMM, so the GEMM is the comparison)
+    t32 = (a2[:rows] @ w.view(256, K).t() + b) + up[:rows]
     torch.cuda.synchronize()
-    mx, _ = _errs(got[:rows], ref)
-    tmx, _ = _errs(t32.permute(0, 2, 3, 1).reshape(-1, 256)[:rows], ref)
-    assert mx <= 2e-5 and mx <= 2 * tmx + 1e-7, (mx, tmx)
+    mx, mean = _errs(got[:rows], ref)
+    tmx, tmean = _errs(t32, ref)
+    assert mx <= 2e-5 and mx <= 3 * tmx + 1e-7 and mean <= 1.5 * tmean + 1e-9, \
+        (mx, mean, tmx, tmean)
     m = modeling.TopdownLateral(256, K).to(DEV)
     with torch.no_grad():
         m.conv_lateral.weight.copy_(w)
@@ -152,4 +156,4 @@ def test_split3_fpn_topdown_lateral(n, K, H, W):
     torch.cuda.synchronize()
     assert y.is_contiguous(memory_format=torch.channels_last)
     assert torch.equal(y.permute(0, 2, 3, 1).reshape(-1, 256), got)
-    del lat, top, got, t32, y
+    del lat, top, got, t32, y, up, a2

@@ -21,7 +21,7 @@ SHAPES = [  # (M, N, K, residual) -- relu on, as the step's
     (33600, 512, 1024, False), (33600, 2048, 1024, False), (33600, 2048, 512, True),
     (33600, 512, 2048, False), (33600, 256, 2048, False), (32000, 1024, 12544, False),
     (32000, 1024, 1024, False), (627200, 1024, 256, False), (537600, 256, 512, False),
-    (134400, 256, 1024, False),
+    (134400, 256, 1024, False), (537600, 512, 128, False), (2150400, 256, 256, False),
 ]
 QUICK = [SHAPES[i] for i in (6, 8, 14, 16)]
 
@@ -73,7 +73,8 @@ def main():
         report("fp32", ms, out)
         wp = ops.gemm_split3_weight(w)
         for cfg in [int(c) for c in args.cfgs.split(",")]:
-            if (cfg in (1, 11, 12, 13) and N % 256) or (cfg == 2 and N % 128):
+            if (cfg in (1, 11, 12, 13) and N % 256) or (cfg in (2, 14) and N % 128) or \
+                    (cfg >= 10 and r is not None):
                 continue
             out.zero_()
             ms = timed(lambda: ops.gemm_split3_bias_act(a, wp, b, residual=r, relu=True, out=out,

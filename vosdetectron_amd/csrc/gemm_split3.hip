@@ -98,15 +98,16 @@ __global__ void split3_weight_kernel(const float *__restrict__ W, int N, int K,
 }
 
 // Workgroup: 4 waves (one per SIMD), BM pixels x BN channels; wave (wm, wn) owns
-// TPM x TPN 32 x 32 tiles (up to 4 x 4: 256 accumulator registers).  K walks in
+// TPM x TPN 32 x 32 tiles (up to 4 x 4: 256 accumulator registers).  OCC = 2: two
+// workgroups per CU (<= 256 registers a wave), so each SIMD interleaves two waves.  K walks in
 // 16-deep stages through two LDS buffers; stage c + 2's global loads are issued
 // into registers right after stage c + 1's registers were split into the other
 // buffer, all inside stage c's MFMA stream (one basic block, so the scheduler
 // interleaves them), one barrier per stage.
 // RES: 0 none, 1 R[M][N] (the identity residual), 2 R = the top-down map of an FPN
 // level, images x H/2 x W/2 x N, read at the nearest-2x row of pixel p (FPN.py:292-300).
-template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0>
-__global__ __launch_bounds__(kThreads, 1) void gemm_split3_kernel(
+template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0, int OCC = 1>
+__global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
     const float *__restrict__ A, const uint4 *__restrict__ Wp, const float *__restrict__ bias,
     const float *__restrict__ R, float *__restrict__ D, int M, int N, int K, int tiles_n,
     int num_tiles, int H, int W) {
@@ -280,13 +281,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_split3_kernel(
     }
 }
 
-template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0>
+template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0, int OCC = 1>
 int launch_cfg(const float *A, int M, int K, const uint4 *Wp, int N, const float *bias,
                const float *R, float *D, int H, int W, hipStream_t s) {
     constexpr int PT = BM / 32, NTW = BN / 32;
     constexpr size_t lds = 2 * (size_t)(3 * PT + NTW * 3) * kFragBytes;
     static_assert(lds <= VD_LDS_BYTES, "LDS");
-    auto kern = gemm_split3_kernel<BM, BN, TPM, TPN, RES, RELU, PROBE>;
+    auto kern = gemm_split3_kernel<BM, BN, TPM, TPN, RES, RELU, PROBE, OCC>;
     static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  (int)lds) == hipSuccess;
@@ -300,12 +301,14 @@ int launch_cfg(const float *A, int M, int K, const uint4 *Wp, int N, const float
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
-template <int BM, int BN, int TPM, int TPN>
+template <int BM, int BN, int TPM, int TPN, int OCC>
 int launch_epi(const float *A, int M, int K, const uint4 *Wp, int N, const float *bias,
                const float *R, int relu, float *D, int H, int W, hipStream_t s) {
-#define VD_S3_RELU(RES_)                                                                      \
-    return relu ? launch_cfg<BM, BN, TPM, TPN, RES_, true>(A, M, K, Wp, N, bias, R, D, H, W, s) \
-                : launch_cfg<BM, BN, TPM, TPN, RES_, false>(A, M, K, Wp, N, bias, R, D, H, W, s)
+#define VD_S3_RELU(RES_)                                                                       \
+    return relu ? launch_cfg<BM, BN, TPM, TPN, RES_, true, 0, OCC>(A, M, K, Wp, N, bias, R, D,  \
+                                                                   H, W, s)                     \
+                : launch_cfg<BM, BN, TPM, TPN, RES_, false, 0, OCC>(A, M, K, Wp, N, bias, R, D, \
+                                                                    H, W, s)
     if (R && H > 0) VD_S3_RELU(2);
     if (R) VD_S3_RELU(1);
     VD_S3_RELU(0);
@@ -327,8 +330,8 @@ int launch_gemm_split3_weight(const float *W, int N, int K, void *Wp, hipStream_
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
-// cfg: 0 = auto, 1 = 256 x 256, 2 = 256 x 128, 3 = 256 x 64 (pixels x channels per
-// workgroup; waves of 128 x 128 / 128 x 64 / 128 x 32)
+// cfg: 0 = auto, 1 = 256 x 256 (one workgroup per CU), 2 = 256 x 128, 3 = 256 x 64 (two
+// per CU) -- pixels x channels per workgroup; waves of 128 x 128 / 128 x 64 / 128 x 32
 // up_h / up_w > 0: R is the top-down map of an images x up_h x up_w level (M = images
 // x up_h x up_w, both even), read at the nearest-2x row of each pixel.
 int launch_gemm_split3(const float *A, int M, int K, const void *Wp, int N, const float *bias,
@@ -343,22 +346,22 @@ int launch_gemm_split3(const float *A, int M, int K, const void *Wp, int N, cons
     }
     const uint4 *w = reinterpret_cast<const uint4 *>(Wp);
     if (cfg == 0) {
-        // the widest tile that still gives every CU about two workgroups (a 256 x 256
-        // tile on a 33,600-row res5 GEMM would leave half the CUs idle): measured on
-        // the benched step's shapes (profiles/r06/gemm_split3/)
-        const int64_t tm = (M + 255) / 256;
-        cfg = (N % 256 == 0 && tm * (N / 256) >= 480) ? 1
-              : (N % 128 == 0 && tm * (N / 128) >= 480) ? 2 : 3;
+        // 256 x 128 tiles at two workgroups per CU (two waves per SIMD hide each
+        // other's LDS / barrier stalls: 10-20 % faster than one 256 x 256 workgroup on
+        // the step's shapes), the 256 x 256 single workgroup only for very deep K
+        // (fc6, K = 12,544: 4 % faster), 256 x 64 where N is not a multiple of 128
+        // (profiles/r06/gemm_split3/)
+        cfg = (N % 256 == 0 && K >= 4096) ? 1 : (N % 128 == 0 ? 2 : 3);
     }
     switch (cfg) {
     case 1:
         if (N % 256) return VD_ERR_SHAPE;
-        return launch_epi<256, 256, 4, 4>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, s);
+        return launch_epi<256, 256, 4, 4, 1>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, s);
     case 2:
         if (N % 128) return VD_ERR_SHAPE;
-        return launch_epi<256, 128, 4, 2>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, s);
+        return launch_epi<256, 128, 4, 2, 2>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, s);
     case 3:
-        return launch_epi<256, 64, 4, 1>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, s);
+        return launch_epi<256, 64, 4, 1, 2>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, s);
 #ifdef VD_RESEARCH_PROBES
     case 11: case 12: case 13:  // speed-of-light probes of cfg 1 (wrong results by design)
         if (N % 256 || R || !relu) return VD_ERR_SHAPE;

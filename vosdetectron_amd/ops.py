@@ -539,7 +539,7 @@ def gemm_plan_list() -> list:
 # K from which a GEMM with a split-bf16 route runs it there (gemm_split3_bias_act):
 # below it the GEMMs are HBM-bound and the fp32 kernels are as fast
 # (profiles/r06/gemm_split3/)
-SPLIT3_MIN_K = 256
+SPLIT3_MIN_K = 128
 # id(weight tensor) -> (weakref to it, key, split image); an entry leaves with its tensor
 _split3_cache = {}
 
