@@ -173,7 +173,10 @@ int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const 
  * otherwise); residual may be NULL.  up_h, up_w > 0 (both even): residual is the
  * top-down map of an FPN level, images x up_h/2 x up_w/2 x N, added at the nearest-2x
  * row of each of the M = images x up_h x up_w pixels after the bias -- the FPN
- * top-down lateral step (FPN.py:292-300) in one launch.  cfg 0 picks the tile shape (1: 256 pixels x
+ * top-down lateral step (FPN.py:292-300) in one launch.  sub_h, sub_w > 0: A is an
+ * images x sub_h x sub_w NHWC map read at stride 2 (M = images x ceil(sub_h/2) x
+ * ceil(sub_w/2)): a stage's stride-2 1x1 convs (ResNet.py:246-294 with STRIDE_1X1, and
+ * the downsample shortcut) without the subsampled copy.  cfg 0 picks the tile shape (1: 256 pixels x
  * 128 channels, 2: 256 x 64, 3: 128 x 256 per workgroup).  Replaces the same
  * fp32 convolutions / Linear layers as vd_gemm_bias_act (ResNet.py:246-294
  * bottleneck 1x1s, fast_rcnn_heads.py fc6 / fc7, mask_rcnn_heads.py upconv5). */
@@ -181,7 +184,7 @@ size_t vd_gemm_split3_weight_size(int N, int K);
 int vd_gemm_split3_weight(const float *W, int N, int K, void *Wp, void *stream);
 int vd_gemm_split3_bias_act(const float *A, int M, int K, const void *Wp, int N,
                             const float *bias, const float *residual, int up_h, int up_w,
-                            int relu, float *D, int cfg, void *stream);
+                            int sub_h, int sub_w, int relu, float *D, int cfg, void *stream);
 
 /* 3x3 stride-1 pad-1 convolution of a channels_last (NHWC) fp32 tensor with
  * the bias (+ ReLU) epilogue fused, one hand-written MFMA implicit-GEMM kernel:

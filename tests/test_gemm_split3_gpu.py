@@ -157,3 +157,23 @@ def test_split3_fpn_topdown_lateral(n, K, H, W):
     assert y.is_contiguous(memory_format=torch.channels_last)
     assert torch.equal(y.permute(0, 2, 3, 1).reshape(-1, 256), got)
     del lat, top, got, t32, y, up, a2
+
+
+@pytest.mark.parametrize("n,C,H,W,N", [(2, 256, 20, 34, 128), (3, 512, 11, 17, 1024),
+                                       (32, 256, 200, 336, 512)])
+def test_split3_stride2_rows(n, C, H, W, N):
+    """A stride-2 pad-0 1x1 conv read at stride 2 by the GEMM itself (sub_hw): equal
+    bit for bit to the same GEMM over the subsampled copy, odd sizes included."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(C + H)
+    x = torch.randn(n, C, H, W, device=DEV, generator=g).contiguous(
+        memory_format=torch.channels_last)
+    w = torch.randn(N, C, device=DEV, generator=g) / C ** .5
+    b = torch.randn(N, device=DEV, generator=g)
+    wp = ops.gemm_split3_weight(w)
+    xs = x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last)
+    want = ops.gemm_split3_bias_act(xs.permute(0, 2, 3, 1).reshape(-1, C), wp, b)
+    got = ops.gemm_split3_bias_act(x.permute(0, 2, 3, 1).reshape(-1, C), wp, b, sub_hw=(H, W))
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+    del x, xs, want, got

@@ -110,7 +110,7 @@ template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0, i
 __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
     const float *__restrict__ A, const uint4 *__restrict__ Wp, const float *__restrict__ bias,
     const float *__restrict__ R, float *__restrict__ D, int M, int N, int K, int tiles_n,
-    int num_tiles, int H, int W) {
+    int num_tiles, int H, int W, int SH, int SW) {
     constexpr int WM = BM / (32 * TPM), WN = BN / (32 * TPN);
     static_assert(WM * WN == 4, "4 waves");
     constexpr int PT = BM / 32, NTW = BN / 32;                 // pixel / channel tiles
@@ -143,6 +143,12 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
     for (int j = 0; j < AL; ++j) {
         int64_t m = m0 + (t >> 2) + 64 * j;
         if (m >= M) m = M - 1;
+        if (SH > 0) {  // A read at stride 2 from images x SH x SW (a strided 1x1 conv)
+            const int Ho = (SH + 1) >> 1, Wo = (SW + 1) >> 1;
+            const int64_t hw = (int64_t)Ho * Wo, n = m / hw;
+            const int rem = (int)(m - n * hw), y = rem / Wo, x = rem - y * Wo;
+            m = (n * SH + 2 * y) * (int64_t)SW + 2 * x;
+        }
         arow[j] = A + m * K + 4 * kq;
     }
     // the workgroup's weight slice of stage s: NTW consecutive (s, t) blocks
@@ -283,7 +289,7 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
 
 template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0, int OCC = 1>
 int launch_cfg(const float *A, int M, int K, const uint4 *Wp, int N, const float *bias,
-               const float *R, float *D, int H, int W, hipStream_t s) {
+               const float *R, float *D, int H, int W, int SH, int SW, hipStream_t s) {
     constexpr int PT = BM / 32, NTW = BN / 32;
     constexpr size_t lds = 2 * (size_t)(3 * PT + NTW * 3) * kFragBytes;
     static_assert(lds <= VD_LDS_BYTES, "LDS");
@@ -297,18 +303,18 @@ int launch_cfg(const float *A, int M, int K, const uint4 *Wp, int N, const float
     if (num_tiles >= (1ll << 31) - 8) return VD_ERR_SHAPE;
     const int64_t grid = (num_tiles + 7) / 8 * 8;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), lds, s, A, Wp, bias, R, D, M, N,
-                       K, tiles_n, (int)num_tiles, H, W);
+                       K, tiles_n, (int)num_tiles, H, W, SH, SW);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
 template <int BM, int BN, int TPM, int TPN, int OCC>
 int launch_epi(const float *A, int M, int K, const uint4 *Wp, int N, const float *bias,
-               const float *R, int relu, float *D, int H, int W, hipStream_t s) {
+               const float *R, int relu, float *D, int H, int W, int SH, int SW, hipStream_t s) {
 #define VD_S3_RELU(RES_)                                                                       \
     return relu ? launch_cfg<BM, BN, TPM, TPN, RES_, true, 0, OCC>(A, M, K, Wp, N, bias, R, D,  \
-                                                                   H, W, s)                     \
+                                                                   H, W, SH, SW, s)             \
                 : launch_cfg<BM, BN, TPM, TPN, RES_, false, 0, OCC>(A, M, K, Wp, N, bias, R, D, \
-                                                                    H, W, s)
+                                                                    H, W, SH, SW, s)
     if (R && H > 0) VD_S3_RELU(2);
     if (R) VD_S3_RELU(1);
     VD_S3_RELU(0);
@@ -333,12 +339,18 @@ int launch_gemm_split3_weight(const float *W, int N, int K, void *Wp, hipStream_
 // cfg: 0 = auto, 1 = 256 x 256 (one workgroup per CU), 2 = 256 x 128, 3 = 256 x 64 (two
 // per CU) -- pixels x channels per workgroup; waves of 128 x 128 / 128 x 64 / 128 x 32
 // up_h / up_w > 0: R is the top-down map of an images x up_h x up_w level (M = images
-// x up_h x up_w, both even), read at the nearest-2x row of each pixel.
+// x up_h x up_w, both even), read at the nearest-2x row of each pixel.  sub_h / sub_w
+// > 0: A is an images x sub_h x sub_w map read at stride 2 (M = images x ceil(sub_h / 2)
+// x ceil(sub_w / 2)): a stride-2 pad-0 1x1 convolution without the subsampled copy.
 int launch_gemm_split3(const float *A, int M, int K, const void *Wp, int N, const float *bias,
-                       const float *R, int up_h, int up_w, int relu, float *D, int cfg,
-                       hipStream_t s) {
+                       const float *R, int up_h, int up_w, int sub_h, int sub_w, int relu,
+                       float *D, int cfg, hipStream_t s) {
     if (M == 0) return VD_OK;
     if (!gemm_split3_supported(K, N)) return VD_ERR_SHAPE;
+    if (sub_h || sub_w) {
+        if (sub_h < 1 || sub_w < 1 || M % ((int64_t)((sub_h + 1) / 2) * ((sub_w + 1) / 2)))
+            return VD_ERR_ARG;
+    }
     if (up_h || up_w) {
         if (!R || up_h < 2 || up_w < 2 || (up_h & 1) || (up_w & 1) ||
             M % ((int64_t)up_h * up_w))
@@ -356,18 +368,21 @@ int launch_gemm_split3(const float *A, int M, int K, const void *Wp, int N, cons
     switch (cfg) {
     case 1:
         if (N % 256) return VD_ERR_SHAPE;
-        return launch_epi<256, 256, 4, 4, 1>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, s);
+        return launch_epi<256, 256, 4, 4, 1>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
+                                             s);
     case 2:
         if (N % 128) return VD_ERR_SHAPE;
-        return launch_epi<256, 128, 4, 2, 2>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, s);
+        return launch_epi<256, 128, 4, 2, 2>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
+                                             s);
     case 3:
-        return launch_epi<256, 64, 4, 1, 2>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, s);
+        return launch_epi<256, 64, 4, 1, 2>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
+                                             s);
 #ifdef VD_RESEARCH_PROBES
     case 11: case 12: case 13:  // speed-of-light probes of cfg 1 (wrong results by design)
         if (N % 256 || R || !relu) return VD_ERR_SHAPE;
-        if (cfg == 11) return launch_cfg<256, 256, 4, 4, 0, true, 1>(A, M, K, w, N, bias, R, D, 0, 0, s);
-        if (cfg == 12) return launch_cfg<256, 256, 4, 4, 0, true, 2>(A, M, K, w, N, bias, R, D, 0, 0, s);
-        return launch_cfg<256, 256, 4, 4, 0, true, 3>(A, M, K, w, N, bias, R, D, 0, 0, s);
+        if (cfg == 11) return launch_cfg<256, 256, 4, 4, 0, true, 1>(A, M, K, w, N, bias, R, D, 0, 0, 0, 0, s);
+        if (cfg == 12) return launch_cfg<256, 256, 4, 4, 0, true, 2>(A, M, K, w, N, bias, R, D, 0, 0, 0, 0, s);
+        return launch_cfg<256, 256, 4, 4, 0, true, 3>(A, M, K, w, N, bias, R, D, 0, 0, 0, 0, s);
 #endif
     default:
         return VD_ERR_ARG;

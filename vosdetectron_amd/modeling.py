@@ -331,13 +331,21 @@ class Bottleneck(nn.Module):
         # copy kernel) instead of MIOpen / CK strided convs: 2.78 -> 2.27 ms per
         # 16-frame step over res3-res5 (profiles/r04/stride2/ab.jsonl)
         xs = None
-        if self.downsample is not None and self.fd.stride != (1, 1) and _is_1x1(self.fd):
+        strided = self.downsample is not None and self.fd.stride != (1, 1) and _is_1x1(self.fd)
+        # round 6: the split-bf16 GEMM reads x at stride 2 itself (no subsampled copy)
+        s2 = strided and self.fd.stride == (2, 2) and _split3_s2_ok(x, self.wd)
+        if strided and not s2:
             xs = _subsample(x, self.fd.stride)
+        out = None
         if self.f1.stride == (1, 1):
             out = _gemm_conv1x1(x, self.w1, self.f1.bias, relu=True)
-        elif xs is not None and self.f1.stride == self.fd.stride and _is_1x1(self.f1):
+        elif s2 and self.f1.stride == (2, 2) and _is_1x1(self.f1) and _split3_s2_ok(x, self.w1):
+            out = _gemm_conv1x1_s2(x, self.w1, self.f1.bias, relu=True)
+        elif strided and self.f1.stride == self.fd.stride and _is_1x1(self.f1):
+            if xs is None:
+                xs = _subsample(x, self.fd.stride)
             out = _gemm_conv1x1(xs, self.w1, self.f1.bias, relu=True)
-        else:
+        if out is None:
             out = _conv_epi(self.f1, x)
         y = _conv3x3_mfma(self.f2, out, relu=True)  # res2 / res3 3x3s (>= 2^18 px)
         out = y if y is not None else _conv_epi(self.f2, out)
@@ -348,6 +356,9 @@ class Bottleneck(nn.Module):
                 y = ops.gemm_dual_bias_act(_nhwc2d(out), _nhwc2d(x), self.w3d, self.b3d)
                 if y is not None:
                     return y.view(N, H, W, -1).permute(0, 3, 1, 2)
+            if s2:  # relu(h W3^T + b3 + (x[::2, ::2] Wd^T + bd))
+                r = _gemm_conv1x1_s2(x, self.wd, self.fd.bias, relu=False)
+                return _gemm_conv1x1(out, self.w3, self.f3.bias, relu=True, res=r)
             if xs is not None:  # relu(h W3^T + b3 + (xs Wd^T + bd))
                 r = _gemm_conv1x1(xs, self.wd, self.fd.bias, relu=False)
                 return _gemm_conv1x1(out, self.w3, self.f3.bias, relu=True, res=r)
@@ -363,6 +374,24 @@ def _subsample(x, stride):
     """x[:, :, ::sh, ::sw] as a channels_last tensor: the pixels a pad-0 strided 1x1
     conv reads (output size ceil(H / s), as the conv's)."""
     return x[:, :, ::stride[0], ::stride[1]].contiguous(memory_format=torch.channels_last)
+
+
+def _split3_s2_ok(x, w2d) -> bool:
+    """A stride-2 1x1 conv of x runs as a split-bf16 GEMM reading x at stride 2."""
+    return (ops.split3_enabled() and x.shape[1] >= ops.SPLIT3_MIN_K and x.shape[1] % 16 == 0
+            and w2d.shape[0] % 64 == 0 and _gemm_ok(x))
+
+
+def _gemm_conv1x1_s2(x, w2d, bias, relu=True, res=None):
+    """Stride-2 pad-0 1x1 conv of a channels_last NCHW tensor as act(x[::2, ::2] W^T + b
+    [+ res]) in one split-bf16 GEMM that reads x at stride 2 (no subsampled copy)."""
+    N, C, H, W = x.shape
+    wp = ops.split3_weight_cached(w2d)
+    r = None
+    if res is not None:
+        r = _nhwc2d(res.contiguous(memory_format=torch.channels_last))
+    y = ops.gemm_split3_bias_act(_nhwc2d(x), wp, bias, residual=r, relu=relu, sub_hw=(H, W))
+    return y.view(N, (H + 1) // 2, (W + 1) // 2, w2d.shape[0]).permute(0, 3, 1, 2)
 
 
 def _gemm_ok(x) -> bool:
@@ -827,7 +856,32 @@ class FastRCNNOutputs(nn.Module):
         self.cls_agnostic = cls_agnostic
 
     def forward(self, x):
+        if x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.shape[0] > 0 and \
+                ops.split3_enabled() and x.shape[1] >= ops.SPLIT3_MIN_K and x.shape[1] % 16 == 0:
+            # cls_score and bbox_pred as ONE GEMM over the concatenated weights (N = 81 +
+            # 324 padded to 448: a multiple of the 64-channel tile) on the split-bf16
+            # kernel; hipBLASLt ran the two skinny GEMMs at ~0.1 of the fp32 peak
+            w, b = self._cat_weights()
+            y = ops.gemm_bias_act(x.contiguous(), w, b, relu=False)
+            if y is not None:
+                nc, nb = self.cls_score.out_features, self.bbox_pred.out_features
+                return F.softmax(y[:, :nc], dim=1), y[:, nc:nc + nb].contiguous()
         return F.softmax(self.cls_score(x), dim=1), self.bbox_pred(x)
+
+    @torch.no_grad()
+    def _cat_weights(self):
+        ws = (self.cls_score.weight, self.bbox_pred.weight, self.cls_score.bias,
+              self.bbox_pred.bias)
+        key = tuple((t.data_ptr(), t._version) for t in ws)
+        if getattr(self, "_vd_cat_key", None) != key:
+            n = ws[0].shape[0] + ws[1].shape[0]
+            npad = (n + 63) // 64 * 64
+            w = torch.zeros((npad, ws[0].shape[1]), dtype=ws[0].dtype, device=ws[0].device)
+            b = torch.zeros((npad,), dtype=ws[0].dtype, device=ws[0].device)
+            w[:n] = torch.cat([ws[0], ws[1]])
+            b[:n] = torch.cat([ws[2], ws[3]])
+            self._vd_cat, self._vd_cat_key = (w, b), key
+        return self._vd_cat
 
     def per_class_deltas(self, bbox_pred, num_classes):
         """vos_test.py:179-190 decodes the fg deltas once and tiles the boxes over

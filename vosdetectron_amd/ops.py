@@ -625,15 +625,24 @@ def gemm_split3_weight(w: torch.Tensor) -> Optional[torch.Tensor]:
 def gemm_split3_bias_act(a: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor,
                          residual: Optional[torch.Tensor] = None, relu: bool = True,
                          out: Optional[torch.Tensor] = None, cfg: int = 0,
-                         up_hw: Optional[Sequence[int]] = None) -> torch.Tensor:
+                         up_hw: Optional[Sequence[int]] = None,
+                         sub_hw: Optional[Sequence[int]] = None) -> torch.Tensor:
     """act(a @ w.T + bias (+ residual)) with the fp32 operands split into three bf16
     pieces on the bf16 matrix cores (vd_gemm_split3_bias_act, fp32 accuracy):
     a [M,K], wp from gemm_split3_weight(w [N,K]), bias [N], out [M,N]; residual
     [M,N], or with up_hw = (H, W) the top-down map [M / (H W), H/2, W/2, N] of an
-    FPN level added at the nearest-2x row of each pixel (FPN.py:292-300)."""
+    FPN level added at the nearest-2x row of each pixel (FPN.py:292-300).  With
+    sub_hw = (H, W): a is an images x H x W map's rows [images H W, K] read at
+    stride 2, M = images x ceil(H/2) x ceil(W/2) output rows (a stride-2 1x1 conv)."""
     a_ = _need(a, "a")
     N, K = wp.split3_shape
     M = a_.shape[0]
+    sh = sw = 0
+    if sub_hw is not None:
+        sh, sw = int(sub_hw[0]), int(sub_hw[1])
+        if sh < 1 or sw < 1 or M % (sh * sw):
+            raise ValueError("a %s is not a stack of %s maps" % (tuple(a_.shape), (sh, sw)))
+        M = M // (sh * sw) * ((sh + 1) // 2) * ((sw + 1) // 2)
     b_ = _need(bias, "bias")
     if a_.dim() != 2 or a_.shape[1] != K or b_.numel() != N:
         raise ValueError("gemm_split3_bias_act: a %s, w (%d, %d), bias %s"
@@ -656,7 +665,7 @@ def gemm_split3_bias_act(a: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor,
         raise ValueError("out must be a contiguous %s tensor" % ((M, N),))
     check(lib().vd_gemm_split3_bias_act(a_.data_ptr(), M, K, wp.data_ptr(), N, b_.data_ptr(),
                                         r_.data_ptr() if r_ is not None else None, uh, uw,
-                                        int(relu), out.data_ptr(), int(cfg), _stream()),
+                                        sh, sw, int(relu), out.data_ptr(), int(cfg), _stream()),
           "vd_gemm_split3_bias_act")
     return out
 
