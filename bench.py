@@ -278,7 +278,7 @@ def frame_flops(sd, cfg, frames=16):
     ref, fr, _ = ref_cpu_pipeline(sd, 0, cfg)
     with FlopCounterMode(display=False) as fc, _WinoFlops(frames) as wf:
         res = ref(fr[0])
-    return int(fc.get_total_flops()), int(len(res[1])), wf.flops, wf.flops4
+    return int(fc.get_total_flops()), int(len(res[1])), wf.flops, wf.flops4, wf.split3
 
 
 class _WinoFlops(torch.overrides.TorchFunctionMode):
@@ -293,11 +293,30 @@ class _WinoFlops(torch.overrides.TorchFunctionMode):
 
     def __init__(self, frames=16):
         super().__init__()
-        self.flops, self.flops4, self.frames = 0, 0, frames
+        self.flops, self.flops4, self.split3, self.frames = 0, 0, 0, frames
 
     def __torch_function__(self, func, types, args=(), kwargs=None):
+        from vosdetectron_amd import ops
         kwargs = kwargs or {}
         out = func(*args, **kwargs)
+        # GEMM-shaped contractions the engine runs on the split-bf16 kernel
+        # (ops.gemm_bias_act's rule: K >= SPLIT3_MIN_K, N a multiple of 64; the box
+        # head's cls_score / bbox_pred run fused, N padded to 448)
+        if ops.split3_enabled():
+            if func in (torch.nn.functional.linear,):
+                x, w = args[0], args[1]
+                if w.shape[1] >= ops.SPLIT3_MIN_K and w.shape[1] % 16 == 0:
+                    self.split3 += 2 * x.numel() // x.shape[-1] * w.shape[0] * w.shape[1]
+            elif func in (torch.nn.functional.conv2d, torch.conv2d):
+                w = args[1]
+                if tuple(w.shape[2:]) == (1, 1) and w.shape[1] >= ops.SPLIT3_MIN_K and \
+                        w.shape[1] % 16 == 0 and w.shape[0] % 64 == 0:
+                    self.split3 += 2 * out.numel() * w.shape[1]
+            elif func in (torch.nn.functional.conv_transpose2d, torch.conv_transpose2d):
+                x, w = args[0], args[1]  # w: Cin x Cout x kh x kw
+                n = w.shape[1] * w.shape[2] * w.shape[3]
+                if w.shape[0] >= ops.SPLIT3_MIN_K and n % 64 == 0:
+                    self.split3 += 2 * x.numel() * n
         if func in (torch.nn.functional.conv2d, torch.conv2d):
             from vosdetectron_amd.modeling import conv3x3_route
             x, w = args[0], args[1]
@@ -401,8 +420,11 @@ def measure_dominant_conv(dev, F, H, W, C=256, iters=None):
                    "not a fraction" % (iters, positions)}
 
 
+MFMA_BF16_PEAK_TFS = 2516.6  # dense bf16 matrix peak: 256 CUs x 4 SIMDs x 1024 flop/clk x 2.4 GHz
+
+
 def step_roofline(flops_frame, dets_cpu, frames, ms_per_step, engine_launch, frame_hw, blob_hw,
-                  wino_flops_frame=0, wino4_flops_frame=0):
+                  wino_flops_frame=0, wino4_flops_frame=0, split3_flops_frame=0):
     """the FPS as a fraction of the roofline = sum of per-stage
     bound times / measured step time.  MFMA-bound stages: the FLOPs the engine's
     MFMAs execute for one frame at the fp32 matrix peak -- the reference's
@@ -413,10 +435,14 @@ def step_roofline(flops_frame, dets_cpu, frames, ms_per_step, engine_launch, fra
     + fp32 blob write) at 8 TB/s; latency-bound stages (proposals, NMS) carry no
     bound.  `frac` is that executed-work fraction (<= 1 by construction).  Pricing
     every conv in its direct form instead gives a rate, not a fraction (Winograd
-    takes it past 1): reported as `direct_conv_equivalent`, never as a frac."""
+    takes it past 1): reported as `direct_conv_equivalent`, never as a frac.  The
+    1x1 convs / fc layers the engine runs on the split-bf16 GEMM (round 6) execute
+    six bf16 products per fp32 MAC on the bf16 matrix cores: priced at 6 x their
+    FLOPs at the dense bf16 peak (0.38 of their time at the fp32 peak)."""
     exec_flops = (flops_frame - wino_flops_frame * (1 - 1 / 2.25)
                   - wino4_flops_frame * (1 - 1 / 4.0))
-    exec_ms = exec_flops * frames / (MFMA_FP32_PEAK_TFS * 1e12) * 1e3
+    exec_ms = ((exec_flops - split3_flops_frame) / (MFMA_FP32_PEAK_TFS * 1e12)
+               + 6 * split3_flops_frame / (MFMA_BF16_PEAK_TFS * 1e12)) * frames * 1e3
     direct_ms = flops_frame * frames / (MFMA_FP32_PEAK_TFS * 1e12) * 1e3
     h, w = frame_hw
     blob_bytes = frames * (h * w * 3 + 3 * 4 * blob_hw[0] * blob_hw[1])
@@ -428,6 +454,7 @@ def step_roofline(flops_frame, dets_cpu, frames, ms_per_step, engine_launch, fra
             "executed_gflop_per_frame": round(exec_flops / 1e9, 2),
             "winograd_direct_gflop_per_frame": round(wino_flops_frame / 1e9, 2),
             "winograd4_direct_gflop_per_frame": round(wino4_flops_frame / 1e9, 2),
+            "split_bf16_gemm_gflop_per_frame": round(split3_flops_frame / 1e9, 2),
             "mfma_util_step": round(exec_ms / ms_per_step, 4),
             "direct_conv_equivalent": {
                 "gflop_per_frame": round(flops_frame / 1e9, 2),
@@ -436,7 +463,8 @@ def step_roofline(flops_frame, dets_cpu, frames, ms_per_step, engine_launch, fra
                 "note": "reference FLOPs (every conv direct) / step time: a rate, not a "
                         "roofline fraction"},
             "dets_in_counted_frame": dets_cpu,
-            "peaks": {"fp32_matrix_TFs": MFMA_FP32_PEAK_TFS, "hbm_GBs": HBM_PEAK_GBS},
+            "peaks": {"fp32_matrix_TFs": MFMA_FP32_PEAK_TFS, "bf16_matrix_TFs": MFMA_BF16_PEAK_TFS,
+                      "hbm_GBs": HBM_PEAK_GBS},
             "flops_source": "torch.utils.flop_counter over one frame of the reference CPU path "
                             "(oracle/pipeline.py), 2 flop per MAC; Winograd convs by the "
                             "engine's routing rule (modeling.conv3x3_route)"}
@@ -1131,14 +1159,15 @@ def main():
                 dev, F, getattr(pipe, "Hp", fh) // 4, getattr(pipe, "Wp", fw) // 4)
         nthr = torch.get_num_threads()
         torch.set_num_threads(cpu_share()[0])
-        flops, dets_cpu, wino_flops, wino4_flops = frame_flops(sd, cfg, F)
+        flops, dets_cpu, wino_flops, wino4_flops, split3_flops = frame_flops(sd, cfg, F)
         torch.set_num_threads(nthr)
         extra["step_roofline"] = step_roofline(
             flops, dets_cpu, F, dt / args.steps * 1e3, roof.get("engine_launch") if roof else None,
             (fh, fw),
             (getattr(pipe, "Hp", fh), getattr(pipe, "Wp", fw)),
             wino_flops if getattr(pipe, "ASYNC", False) and not vos else 0,
-            wino4_flops if getattr(pipe, "ASYNC", False) and not vos else 0)
+            wino4_flops if getattr(pipe, "ASYNC", False) and not vos else 0,
+            split3_flops if getattr(pipe, "ASYNC", False) and not vos else 0)
     cpu = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:
         cpu = cpu_baseline(args.config, sd, args.cpu_frames, cfg=cfg)
@@ -1154,6 +1183,13 @@ def main():
             "value": round(fps, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "arith": "fp32 tensors end to end; the 1x1 convs / fc layers with K >= %d run on "
+                     "the bf16 matrix cores with each fp32 operand split into three bf16 "
+                     "pieces (six products, fp32 accumulate: error vs fp64 at or below the "
+                     "fp32 GEMM's, tests/test_gemm_split3_gpu.py)%s" % (
+                         __import__("vosdetectron_amd.ops", fromlist=["ops"]).SPLIT3_MIN_K,
+                         "" if __import__("vosdetectron_amd.ops", fromlist=["ops"])
+                         .split3_enabled() else " -- OFF in this run (VOSDET_GEMM_SPLIT3=0)"),
             "data": "synthetic (u8 800x1333 frames, RandomState seeds; deterministic "
                     "N(0,1/fan_in) weights)",
             "config": {"workload": (
