@@ -186,6 +186,19 @@ int vd_gemm_split3_bias_act(const float *A, int M, int K, const void *Wp, int N,
                             const float *bias, const float *residual, int up_h, int up_w,
                             int sub_h, int sub_w, int relu, float *D, int cfg, void *stream);
 
+/* The mask head's tail in one split-bf16 GEMM launch: the 2x2 / 2 transposed conv
+ * upconv5 + ReLU (mask_rcnn_heads.py:62-68) and the class-selected 1x1 mask logits +
+ * sigmoid (mask_rcnn_outputs, mask_rcnn_heads.py:20-35, at each RoI's class as
+ * segm_results reads them, test.py:801-855): X = the RoI maps, M = RoIs x P x P
+ * NHWC rows of K = 256 channels; Wp = vd_gemm_split3_weight of the upconv weight as
+ * [(i, j, co) = 1024][K]; bias [1024] = the upconv bias per (i, j); cls_w [classes][256],
+ * cls_b [classes]; roi_ch [RoIs] the class channel of each RoI; masks [RoIs][2P][2P]
+ * = sigmoid(sum_co relu(upconv)[2y+i][2x+j][co] * cls_w[ch][co] + cls_b[ch]).  The
+ * M x 1024 upconv output never reaches HBM. */
+int vd_mask_head_upconv_logits(const float *X, int M, int K, const void *Wp, const float *bias,
+                               const float *cls_w, const float *cls_b, const int32_t *roi_ch,
+                               int P, float *masks, void *stream);
+
 /* 3x3 stride-1 pad-1 convolution of a channels_last (NHWC) fp32 tensor with
  * the bias (+ ReLU) epilogue fused, one hand-written MFMA implicit-GEMM kernel:
  * Y[n][y][x][co] = act(sum_{ky,kx,ci} X[n][y+ky-1][x+kx-1][ci] W2[co][ky][kx][ci]

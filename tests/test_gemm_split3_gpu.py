@@ -177,3 +177,42 @@ def test_split3_stride2_rows(n, C, H, W, N):
     torch.cuda.synchronize()
     assert torch.equal(got, want)
     del x, xs, want, got
+
+
+@pytest.mark.parametrize("R,ncls", [(64, 81), (333, 81), (7, 1)])
+@torch.no_grad()
+def test_mask_head_upconv_logits_fused(R, ncls):
+    """The mask head's upconv5 + ReLU + class-selected logits + sigmoid in one launch
+    (vd_mask_head_upconv_logits) vs the unfused path (the upconv GEMM's output written,
+    then the per-RoI class dot product of MaskRCNNOutputs.selected_from_up) and vs
+    an fp64 reference: within 1e-5 (probabilities)."""
+    from vosdetectron_amd import modeling, ops
+    from vosdetectron_amd import config as vcfg
+    cfg = vcfg.get("e2e_mask_rcnn_R-50-FPN_1x")
+    g = torch.Generator(device="cuda").manual_seed(R + ncls)
+    head = modeling.MaskHeadV1upXconvs(256, None, 1. / 16, cfg).to(DEV)
+    outs = modeling.MaskRCNNOutputs(256, ncls).to(DEV)
+    with torch.no_grad():
+        head.upconv.weight.copy_(torch.randn(256, 256, 2, 2, device=DEV, generator=g) / 16)
+        head.upconv.bias.copy_(torch.randn(256, device=DEV, generator=g) * .1)
+        outs.classify.weight.copy_(torch.randn(ncls, 256, 1, 1, device=DEV, generator=g) / 16)
+        outs.classify.bias.copy_(torch.randn(ncls, device=DEV, generator=g))
+    head.prepare()
+    P = 14
+    x = torch.randn(R * P * P, 256, device=DEV, generator=g).relu_()
+    cls = torch.randint(0, 81, (R,), device=DEV, generator=g, dtype=torch.int32)
+    ch = outs._channel(cls).to(torch.int32)
+    got = ops.mask_head_upconv_logits(x, ops.gemm_split3_weight(head.up_wt), head.up_b,
+                                      outs.classify.weight.view(ncls, -1), outs.classify.bias,
+                                      ch, P)
+    unf = outs.selected_from_up(head._upconv_nhwc(x, R, P), cls)
+    # fp64: upconv as the GEMM over (i, j, co), relu, the class dot product, sigmoid
+    y = (x.double() @ head.up_wt.double().t() + head.up_b.double()).relu()
+    y = y.view(R, P, P, 2, 2, 256)
+    w = outs.classify.weight.view(ncls, 256).double()[ch.long()]
+    z = torch.einsum("rhwijc,rc->rhiwj", y, w).reshape(R, 2 * P, 2 * P)
+    ref = torch.sigmoid(z + outs.classify.bias.double()[ch.long()].view(-1, 1, 1))
+    torch.cuda.synchronize()
+    assert got.shape == (R, 2 * P, 2 * P)
+    assert float((got.double() - ref).abs().max()) <= 1e-5
+    assert float((got - unf).abs().max()) <= 1e-5

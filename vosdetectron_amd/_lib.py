@@ -61,6 +61,7 @@ SIGNATURES = {
     "vd_gemm_bias_act": (_I, [_P, _I, _I, _P, _I, _P, _P, _I, _P, _P, _S, _P]),
     "vd_gemm_dual_bias_act": (_I, [_P, _I, _P, _I, _I, _P, _I, _P, _I, _P, _P]),
     "vd_gemm_split3_weight_size": (_S, [_I, _I]),
+    "vd_mask_head_upconv_logits": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _I, _P, _P]),
     "vd_gemm_split3_weight": (_I, [_P, _I, _I, _P, _P]),
     "vd_gemm_split3_bias_act": (_I, [_P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _I,
                                      _P]),

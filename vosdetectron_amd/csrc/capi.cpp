@@ -149,6 +149,14 @@ int vd_gemm_split3_bias_act(const float *A, int M, int K, const void *Wp, int N,
                               cfg, VD_STREAM(stream));
 }
 
+int vd_mask_head_upconv_logits(const float *X, int M, int K, const void *Wp, const float *bias,
+                               const float *cls_w, const float *cls_b, const int32_t *roi_ch,
+                               int P, float *masks, void *stream) {
+    if (M < 0 || K < 1 || P < 1 || !Wp || !bias || !masks || (M > 0 && !X)) return VD_ERR_ARG;
+    return launch_gemm_split3_mask_logits(X, M, K, Wp, 1024, bias, cls_w, cls_b, roi_ch, P, masks,
+                                          VD_STREAM(stream));
+}
+
 int vd_conv3x3_bias_act(const float *X, int N, int H, int W, int C, const float *W2, int Cout,
                         const float *bias, int relu, float *Y, void *stream) {
     if (N < 0 || H < 1 || W < 1 || C < 1 || Cout < 1 || !W2 || !Y || (N > 0 && !X))

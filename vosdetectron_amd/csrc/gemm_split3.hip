@@ -106,11 +106,18 @@ __global__ void split3_weight_kernel(const float *__restrict__ W, int N, int K,
 // interleaves them), one barrier per stage.
 // RES: 0 none, 1 R[M][N] (the identity residual), 2 R = the top-down map of an FPN
 // level, images x H/2 x W/2 x N, read at the nearest-2x row of pixel p (FPN.py:292-300).
+// RES 3: the mask head's upconv with the class-selected 1x1 mask logits fused
+// (mask_rcnn_heads.py:62-68 + the MaskRCNNOutputs classify conv at each RoI's class,
+// sigmoid): BN = 256 = one (i, j) tap group of the 2x2 / 2 transposed conv, R = the
+// classify weights [classes][256], cb its bias, rch each RoI's class channel, H = P
+// (the RoI map side), D = masks [RoIs][2P][2P]; the relu'd upconv output never leaves
+// the workgroup.
 template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0, int OCC = 1>
 __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
     const float *__restrict__ A, const uint4 *__restrict__ Wp, const float *__restrict__ bias,
     const float *__restrict__ R, float *__restrict__ D, int M, int N, int K, int tiles_n,
-    int num_tiles, int H, int W, int SH, int SW) {
+    int num_tiles, int H, int W, int SH, int SW, const float *__restrict__ cb,
+    const int32_t *__restrict__ rch) {
     constexpr int WM = BM / (32 * TPM), WN = BN / (32 * TPN);
     static_assert(WM * WN == 4, "4 waves");
     constexpr int PT = BM / 32, NTW = BN / 32;                 // pixel / channel tiles
@@ -249,6 +256,54 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
 
     // epilogue: lane = pixel (r), registers 4g..4g+3 = channels 8g + 4h .. + 3
     const int h = lane >> 5, r = lane & 31;
+    if constexpr (RES == 3) {
+        static_assert(BN == 256 && WN == 2 && RELU, "one (i, j) group per workgroup");
+        // per pixel: sum over this wave's 128 channels of relu(acc + b) * Wc[class][co],
+        // the two lane halves' channel sets added by a shuffle, the two channel waves
+        // through LDS (the K loop's last barrier has passed: the buffers are free)
+        float *part = reinterpret_cast<float *>(lds);  // [BM] partials of wave wn = 1
+        float dot[TPM];
+#pragma unroll
+        for (int a = 0; a < TPM; ++a) {
+            const int64_t p = min(m0 + (wm * TPM + a) * 32 + r, (int64_t)M - 1);
+            const int roi = (int)(p / (H * H));
+            const float *wc = R + (int64_t)rch[roi] * BN;
+            float sacc = 0.f;
+#pragma unroll
+            for (int b = 0; b < TPN; ++b) {
+                const int cl = (wn * TPN + b) * 32 + 4 * h;  // channel within the group
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const float4 bb = *reinterpret_cast<const float4 *>(bias + n0 + cl + 8 * g);
+                    const float4 ww = *reinterpret_cast<const float4 *>(wc + cl + 8 * g);
+                    sacc += fmaxf(acc[a][b][4 * g] + bb.x, 0.f) * ww.x;
+                    sacc += fmaxf(acc[a][b][4 * g + 1] + bb.y, 0.f) * ww.y;
+                    sacc += fmaxf(acc[a][b][4 * g + 2] + bb.z, 0.f) * ww.z;
+                    sacc += fmaxf(acc[a][b][4 * g + 3] + bb.w, 0.f) * ww.w;
+                }
+            }
+            dot[a] = sacc + __shfl_xor(sacc, 32);
+        }
+        if (wn == 1 && h == 0) {
+#pragma unroll
+            for (int a = 0; a < TPM; ++a) part[(wm * TPM + a) * 32 + r] = dot[a];
+        }
+        __syncthreads();
+        if (wn == 0 && h == 0) {
+            const int P = H, ij = tn;  // tap group (i, j) = (ij / 2, ij % 2)
+#pragma unroll
+            for (int a = 0; a < TPM; ++a) {
+                const int64_t p = m0 + (wm * TPM + a) * 32 + r;
+                if (p >= M) continue;
+                const int roi = (int)(p / (P * P)), hw = (int)(p - (int64_t)roi * P * P);
+                const int y = hw / P, x = hw - y * P;
+                const float z = (dot[a] + part[(wm * TPM + a) * 32 + r]) + cb[rch[roi]];
+                D[((int64_t)roi * 2 * P + 2 * y + (ij >> 1)) * 2 * P + 2 * x + (ij & 1)] =
+                    1.f / (1.f + __expf(-z));
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int a = 0; a < TPM; ++a) {
         const int64_t p = m0 + (wm * TPM + a) * 32 + r;
@@ -289,7 +344,8 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
 
 template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0, int OCC = 1>
 int launch_cfg(const float *A, int M, int K, const uint4 *Wp, int N, const float *bias,
-               const float *R, float *D, int H, int W, int SH, int SW, hipStream_t s) {
+               const float *R, float *D, int H, int W, int SH, int SW, hipStream_t s,
+               const float *cb = nullptr, const int32_t *rch = nullptr) {
     constexpr int PT = BM / 32, NTW = BN / 32;
     constexpr size_t lds = 2 * (size_t)(3 * PT + NTW * 3) * kFragBytes;
     static_assert(lds <= VD_LDS_BYTES, "LDS");
@@ -303,7 +359,7 @@ int launch_cfg(const float *A, int M, int K, const uint4 *Wp, int N, const float
     if (num_tiles >= (1ll << 31) - 8) return VD_ERR_SHAPE;
     const int64_t grid = (num_tiles + 7) / 8 * 8;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), lds, s, A, Wp, bias, R, D, M, N,
-                       K, tiles_n, (int)num_tiles, H, W, SH, SW);
+                       K, tiles_n, (int)num_tiles, H, W, SH, SW, cb, rch);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
@@ -383,10 +439,26 @@ int launch_gemm_split3(const float *A, int M, int K, const void *Wp, int N, cons
         if (cfg == 11) return launch_cfg<256, 256, 4, 4, 0, true, 1>(A, M, K, w, N, bias, R, D, 0, 0, 0, 0, s);
         if (cfg == 12) return launch_cfg<256, 256, 4, 4, 0, true, 2>(A, M, K, w, N, bias, R, D, 0, 0, 0, 0, s);
         return launch_cfg<256, 256, 4, 4, 0, true, 3>(A, M, K, w, N, bias, R, D, 0, 0, 0, 0, s);
+    case 16: case 17: case 18:  // the same probes of cfg 2
+        if (N % 128 || R || !relu) return VD_ERR_SHAPE;
+        if (cfg == 16) return launch_cfg<256, 128, 4, 2, 0, true, 1, 2>(A, M, K, w, N, bias, R, D, 0, 0, 0, 0, s);
+        if (cfg == 17) return launch_cfg<256, 128, 4, 2, 0, true, 2, 2>(A, M, K, w, N, bias, R, D, 0, 0, 0, 0, s);
+        return launch_cfg<256, 128, 4, 2, 0, true, 3, 2>(A, M, K, w, N, bias, R, D, 0, 0, 0, 0, s);
 #endif
     default:
         return VD_ERR_ARG;
     }
+}
+
+int launch_gemm_split3_mask_logits(const float *A, int M, int K, const void *Wp, int N,
+                                   const float *bias, const float *cls_w, const float *cls_b,
+                                   const int32_t *roi_ch, int P, float *masks, hipStream_t s) {
+    if (M == 0) return VD_OK;
+    if (N != 4 * 256 || !gemm_split3_supported(K, N)) return VD_ERR_SHAPE;
+    if (P < 1 || M % (P * P) || !cls_w || !cls_b || !roi_ch || !masks) return VD_ERR_ARG;
+    return launch_cfg<256, 256, 4, 4, 3, true, 0, 1>(A, M, K, reinterpret_cast<const uint4 *>(Wp),
+                                                     N, bias, cls_w, masks, P, P, 0, 0, s,
+                                                     cls_b, roi_ch);
 }
 
 }  // namespace vd

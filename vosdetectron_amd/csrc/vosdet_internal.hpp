@@ -62,6 +62,9 @@ int launch_gemm_split3_weight(const float *W, int N, int K, void *Wp, hipStream_
 int launch_gemm_split3(const float *A, int M, int K, const void *Wp, int N, const float *bias,
                        const float *R, int up_h, int up_w, int sub_h, int sub_w, int relu,
                        float *D, int cfg, hipStream_t s);
+int launch_gemm_split3_mask_logits(const float *A, int M, int K, const void *Wp, int N,
+                                   const float *bias, const float *cls_w, const float *cls_b,
+                                   const int32_t *roi_ch, int P, float *masks, hipStream_t s);
 bool gemm1x1_mfma_supported(int K, int N);
 bool conv3x3_mfma_supported(int C, int Cout);
 int launch_conv3x3_mfma(const float *X, int N, int H, int W, int C, const float *W2, int Cout,

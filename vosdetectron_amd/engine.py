@@ -251,9 +251,8 @@ class FramePipeline:
         if fast and getattr(self.model.Mask_Head, "nhwc_ready", False):
             mfeat = ops.roi_align_fpn(pyr, self.roi_scales, mrois, mlvl, mc.ROI_XFORM_RESOLUTION,
                                       mc.ROI_XFORM_SAMPLING_RATIO, out_layout="nhwc")
-            up = self.model.Mask_Head.head_nhwc(mfeat)
-            return (self.model.Mask_Outs.selected_from_up(up, mcls),
-                    mfeat.permute(0, 3, 1, 2))
+            masks = self.model.Mask_Head.masks_nhwc(mfeat, self.model.Mask_Outs, mcls)
+            return masks, mfeat.permute(0, 3, 1, 2)
         mfeat = ops.roi_align_fpn(pyr, self.roi_scales, mrois, mlvl, mc.ROI_XFORM_RESOLUTION,
                                   mc.ROI_XFORM_SAMPLING_RATIO)
         mh = self.model.Mask_Head.head(mfeat)

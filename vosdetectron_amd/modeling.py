@@ -936,6 +936,32 @@ class MaskHeadV1upXconvs(nn.Module):
             y = torch._addmm_activation(self.up_b, x, self.up_w)
         return y.view(M, P, P, 2, 2, -1)
 
+    def masks_nhwc(self, x_nhwc, outs, cls_idx):
+        """x_nhwc: M x P x P x C RoI features -> M x 2P x 2P mask probabilities at each
+        RoI's class (outs: the MaskRCNNOutputs).  With the split-bf16 GEMM on, the upconv
+        and the class-selected logits run as ONE launch (ops.mask_head_upconv_logits):
+        the M x P x P x 1024 relu'd upconv output never reaches HBM."""
+        M, P, _, C = x_nhwc.shape
+        cw = outs.classify.weight
+        if ops.split3_enabled() and C == 256 and tuple(self.up_wt.shape) == (1024, 256) and \
+                cw.shape[1] == 256 and M > 0:
+            x = self._convs_nhwc(x_nhwc.permute(0, 3, 1, 2))
+            x = x.permute(0, 2, 3, 1).reshape(M * P * P, -1)
+            wp = ops.split3_weight_cached(self.up_wt)
+            if wp is not None:
+                ch = outs._channel(cls_idx).to(torch.int32)
+                return ops.mask_head_upconv_logits(x.contiguous(), wp, self.up_b,
+                                                   cw.view(cw.shape[0], -1), outs.classify.bias,
+                                                   ch, P)
+            return outs.selected_from_up(self._upconv_nhwc(x, M, P), cls_idx)
+        return outs.selected_from_up(self.head_nhwc(x_nhwc), cls_idx)
+
+    def _upconv_nhwc(self, x, M, P):
+        y = ops.gemm_bias_act(x.contiguous(), self.up_wt, self.up_b, relu=True)
+        if y is None:
+            y = torch._addmm_activation(self.up_b, x, self.up_w)
+        return y.view(M, P, P, 2, 2, -1)
+
     def _convs_nhwc(self, x):
         for m in self.conv_fcn:
             if isinstance(m, nn.Conv2d):

@@ -670,6 +670,33 @@ def gemm_split3_bias_act(a: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor,
     return out
 
 
+def mask_head_upconv_logits(x: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor,
+                            cls_w: torch.Tensor, cls_b: torch.Tensor, roi_ch: torch.Tensor,
+                            P: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The mask head's upconv5 + ReLU and the class-selected mask logits + sigmoid in one
+    split-bf16 launch (vd_mask_head_upconv_logits): x [R P P, 256] NHWC RoI map rows,
+    wp = gemm_split3_weight of the upconv weight as [(i, j, co), 256], bias [1024],
+    cls_w [classes, 256], cls_b [classes], roi_ch [R] (int32 class channels).  Returns
+    [R, 2P, 2P] mask probabilities."""
+    x_ = _need(x, "x")
+    R = int(roi_ch.numel())
+    if x_.dim() != 2 or x_.shape[0] != R * P * P or tuple(wp.split3_shape) != (1024, x_.shape[1]):
+        raise ValueError("mask_head_upconv_logits: x %s, %d RoIs of %d x %d, w %s"
+                         % (tuple(x_.shape), R, P, P, wp.split3_shape))
+    cw = _need(cls_w, "cls_w")
+    if cw.dim() != 2 or cw.shape[1] != 256:
+        raise ValueError("cls_w must be [classes, 256], got %s" % (tuple(cw.shape),))
+    ch = _need(roi_ch, "roi_ch", torch.int32)
+    if out is None:
+        out = torch.empty((R, 2 * P, 2 * P), dtype=torch.float32, device=x_.device)
+    check(lib().vd_mask_head_upconv_logits(x_.data_ptr(), x_.shape[0], x_.shape[1], wp.data_ptr(),
+                                           _need(bias, "bias").data_ptr(), cw.data_ptr(),
+                                           _need(cls_b, "cls_b").data_ptr(), ch.data_ptr(), P,
+                                           out.data_ptr(), _stream()),
+          "vd_mask_head_upconv_logits")
+    return out
+
+
 def conv3x3_weight(w: torch.Tensor) -> torch.Tensor:
     """PyTorch conv weight [Cout][Cin][3][3] -> the [Cout][3][3][Cin] layout
     vd_conv3x3_bias_act reads (once per model, at prepare time)."""
