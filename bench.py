@@ -1165,9 +1165,7 @@ def main():
             flops, dets_cpu, F, dt / args.steps * 1e3, roof.get("engine_launch") if roof else None,
             (fh, fw),
             (getattr(pipe, "Hp", fh), getattr(pipe, "Wp", fw)),
-            wino_flops if getattr(pipe, "ASYNC", False) and not vos else 0,
-            wino4_flops if getattr(pipe, "ASYNC", False) and not vos else 0,
-            split3_flops if getattr(pipe, "ASYNC", False) and not vos else 0)
+            wino_flops, wino4_flops, split3_flops)
     cpu = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:
         cpu = cpu_baseline(args.config, sd, args.cpu_frames, cfg=cfg)

@@ -24,6 +24,8 @@ SHAPES = [  # (M, N, K, residual) -- relu on, as the step's
     (134400, 256, 1024, False), (537600, 512, 128, False), (2150400, 256, 256, False),
 ]
 QUICK = [SHAPES[i] for i in (6, 8, 14, 16)]
+SMALLK = [(2150400, 64, 64, False), (2150400, 256, 64, True), (537600, 512, 128, True),
+          (537600, 128, 256, False), (134400, 256, 512, False)]
 
 
 def timed(fn, reps):
@@ -46,7 +48,7 @@ def main():
     ap.add_argument("--check-rows", type=int, default=4096)
     args = ap.parse_args()
     from vosdetectron_amd import ops
-    shapes = QUICK if args.shapes == "quick" else SHAPES
+    shapes = {"quick": QUICK, "smallk": SMALLK}.get(args.shapes, SHAPES)
     g = torch.Generator(device="cuda").manual_seed(0)
     for (M, N, K, res) in shapes:
         a = torch.randn(M, K, device="cuda", generator=g).relu_()  # post-ReLU activations
@@ -70,10 +72,14 @@ def main():
 
         out = torch.empty(M, N, device="cuda")
         ms = timed(lambda: ops.gemm_bias_act(a, w, b, residual=r, relu=True, out=out), args.reps)
+        report("auto", ms, out)
+        os.environ["VOSDET_GEMM_SPLIT3"] = "0"
+        ms = timed(lambda: ops.gemm_bias_act(a, w, b, residual=r, relu=True, out=out), args.reps)
+        del os.environ["VOSDET_GEMM_SPLIT3"]
         report("fp32", ms, out)
         wp = ops.gemm_split3_weight(w)
         for cfg in [int(c) for c in args.cfgs.split(",")]:
-            if (cfg in (1, 11, 12, 13) and N % 256) or (cfg in (2, 14) and N % 128) or \
+            if (cfg in (1, 11, 12, 13) and N % 256) or (cfg in (2, 14, 16, 17, 18, 19) and N % 128) or \
                     (cfg >= 10 and r is not None):
                 continue
             out.zero_()

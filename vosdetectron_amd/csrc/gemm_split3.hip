@@ -393,7 +393,8 @@ int launch_gemm_split3_weight(const float *W, int N, int K, void *Wp, hipStream_
 }
 
 // cfg: 0 = auto, 1 = 256 x 256 (one workgroup per CU), 2 = 256 x 128, 3 = 256 x 64 (two
-// per CU) -- pixels x channels per workgroup; waves of 128 x 128 / 128 x 64 / 128 x 32
+// per CU), 4 = 128 x 128 (three per CU) -- pixels x channels per workgroup; waves of
+// 128 x 128 / 128 x 64 / 128 x 32 / 64 x 64
 // up_h / up_w > 0: R is the top-down map of an images x up_h x up_w level (M = images
 // x up_h x up_w, both even), read at the nearest-2x row of each pixel.  sub_h / sub_w
 // > 0: A is an images x sub_h x sub_w map read at stride 2 (M = images x ceil(sub_h / 2)
@@ -420,6 +421,10 @@ int launch_gemm_split3(const float *A, int M, int K, const void *Wp, int N, cons
         // (fc6, K = 12,544: 4 % faster), 256 x 64 where N is not a multiple of 128
         // (profiles/r06/gemm_split3/)
         cfg = (N % 256 == 0 && K >= 4096) ? 1 : (N % 128 == 0 ? 2 : 3);
+        // 128 x 128 tiles at three workgroups per CU where 256 x 128 would give fewer
+        // than three workgroups per slot (res4 / res5 at 32 frames, N <= 512): more
+        // workgroups in flight, 5-15 % faster there (profiles/r06/gemm_split3/)
+        if (cfg == 2 && N <= 512 && (int64_t)((M + 255) / 256) * (N / 128) < 1536) cfg = 4;
     }
     switch (cfg) {
     case 1:
@@ -429,6 +434,10 @@ int launch_gemm_split3(const float *A, int M, int K, const void *Wp, int N, cons
     case 2:
         if (N % 128) return VD_ERR_SHAPE;
         return launch_epi<256, 128, 4, 2, 2>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
+                                             s);
+    case 4:
+        if (N % 128) return VD_ERR_SHAPE;
+        return launch_epi<128, 128, 2, 2, 3>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
                                              s);
     case 3:
         return launch_epi<256, 64, 4, 1, 2>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
