@@ -592,8 +592,8 @@ def measure_nms(dev, n=1000, thresh=0.7, reps=200):
             "iou_evals_per_s": round(evals / t, 1),
             "input": "SURVEY 8(d) synthetic RoIs (seed 3), uniform scores (seed 4)",
             "how": "HIP events over %d launches, preallocated workspace" % reps,
-            "rocprof": "profiles/r05/head_final/post_launches.txt: nms_prep 14.5 + nms_mask "
-                       "8.1 + nms_resolve 30.7 us per launch (rocprofv3 --kernel-trace, 203 calls)"}
+            "rocprof": "profiles/r06/head_d/trace/post_launches.txt: nms_prep 14.5 + nms_mask "
+                       "8.1 + nms_resolve 30.6 us per launch (rocprofv3 --kernel-trace, 203 calls)"}
 
 
 def measure_step_post(pipe, frames_dev, reps=20):
@@ -648,9 +648,9 @@ def measure_step_post(pipe, frames_dev, reps=20):
                 "avg_us": round(t_d * 1e6, 1), "frames": F, "rois_per_frame": post,
                 "us_per_frame": round(t_d * 1e6 / F, 2)},
             "how": "HIP events over %d launches on the engine's own step tensors" % reps,
-            "rocprof": "profiles/r05/head_final/post_launches.txt (32 frames): rpn_proposals "
-                       "51.6 (+ 6 rpn_sel_hist, rpn_sel_compact) + rpn_nms_mask 125.2 + "
-                       "rpn_nms_finish 33.9 us; class_nms 433.2 + det_limit 41.6 us per launch "
+            "rocprof": "profiles/r06/head_d/trace/post_launches.txt (32 frames): rpn_proposals "
+                       "51.7 (+ 6 rpn_sel_hist, rpn_sel_compact) + rpn_nms_mask 123.8 + "
+                       "rpn_nms_finish 33.9 us; class_nms 447.2 + det_limit 42.7 us per launch "
                        "(rocprofv3 --kernel-trace, 36 calls)"}
 
 
