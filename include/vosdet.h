@@ -170,7 +170,10 @@ int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const 
  * fp64 beside torch's fp32 GEMM in tests/test_gemm_split3_gpu.py).  Wp is the
  * weight in split form, vd_gemm_split3_weight_size(N, K) bytes, made once per
  * model by vd_gemm_split3_weight.  K a multiple of 32, N of 64 (VD_ERR_SHAPE
- * otherwise); residual may be NULL.  up_h, up_w > 0 (both even): residual is the
+ * otherwise); residual may be NULL.  A2 / K2 > 0 (a multiple of 16): the last K2 of the K
+ * input channels come from a second [M][K2] operand (A is then [M][K - K2]): a stage's
+ * first block, conv3 of h and the stride-1 downsample of x as ONE GEMM (ResNet.py:246-294
+ * with basic_bn_shortcut :195-205).  up_h, up_w > 0 (both even): residual is the
  * top-down map of an FPN level, images x up_h/2 x up_w/2 x N, added at the nearest-2x
  * row of each of the M = images x up_h x up_w pixels after the bias -- the FPN
  * top-down lateral step (FPN.py:292-300) in one launch.  sub_h, sub_w > 0: A is an
@@ -183,8 +186,8 @@ int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const 
  * bottleneck 1x1s, fast_rcnn_heads.py fc6 / fc7, mask_rcnn_heads.py upconv5). */
 size_t vd_gemm_split3_weight_size(int N, int K);
 int vd_gemm_split3_weight(const float *W, int N, int K, void *Wp, void *stream);
-int vd_gemm_split3_bias_act(const float *A, int M, int K, const void *Wp, int N,
-                            const float *bias, const float *residual, int up_h, int up_w,
+int vd_gemm_split3_bias_act(const float *A, int M, int K, const float *A2, int K2, const void *Wp,
+                            int N, const float *bias, const float *residual, int up_h, int up_w,
                             int sub_h, int sub_w, int relu, float *D, int cfg, void *stream);
 
 /* The mask head's tail in one split-bf16 GEMM launch: the 2x2 / 2 transposed conv

@@ -216,3 +216,25 @@ def test_mask_head_upconv_logits_fused(R, ncls):
     assert got.shape == (R, 2 * P, 2 * P)
     assert float((got.double() - ref).abs().max()) <= 1e-5
     assert float((got - unf).abs().max()) <= 1e-5
+
+
+@pytest.mark.parametrize("M,K1,K2,N", [(5000, 64, 64, 256), (2150400 // 16, 64, 64, 256),
+                                       (777, 128, 256, 512)])
+def test_split3_two_operands(M, K1, K2, N):
+    """A2: the last K2 input channels from a second operand -- a stage's first block
+    (conv3 of h + the stride-1 downsample of x) in one GEMM: equal bit for bit to the
+    same GEMM over the concatenated [h | x] rows, at torch fp32's error level."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(M + K1)
+    h = torch.randn(M, K1, device=DEV, generator=g).relu_()
+    x = torch.randn(M, K2, device=DEV, generator=g).relu_()
+    w = torch.randn(N, K1 + K2, device=DEV, generator=g) / (K1 + K2) ** .5
+    b = torch.randn(N, device=DEV, generator=g)
+    wp = ops.gemm_split3_weight(w)
+    got = ops.gemm_split3_bias_act(h, wp, b, a2=x)
+    want = ops.gemm_split3_bias_act(torch.cat([h, x], 1), wp, b)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+    ref = (torch.cat([h, x], 1).double() @ w.double().t() + b.double()).relu()
+    mx, _ = _errs(got, ref)
+    assert mx <= 2e-5, mx

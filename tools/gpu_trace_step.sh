@@ -11,5 +11,7 @@ python3 tools/analyze_trace.py $T/run_kernel_trace.csv image_to_blob 60 > $O/ste
 python3 tools/kernel_breakdown.py $T/run_kernel_trace.csv roi_align_fpn > $O/roialign_launches.txt || exit 1
 for k in nms_prep nms_mask nms_resolve rpn_ class_nms det_limit; do
     python3 tools/kernel_breakdown.py $T/run_kernel_trace.csv $k; done > $O/post_launches.txt || exit 1
+for k in conv3x3_wino gemm_split3 gemm1x1 stem_conv; do
+    python3 tools/kernel_breakdown.py $T/run_kernel_trace.csv $k; done > $O/conv_gemm_launches.txt || exit 1
 cp $T/run_kernel_stats.csv $O/kernel_stats.csv
 head -30 $O/steady_step.txt

@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
     const float *__restrict__ A, const uint4 *__restrict__ Wp, const float *__restrict__ bias,
     const float *__restrict__ R, float *__restrict__ D, int M, int N, int K, int tiles_n,
     int num_tiles, int H, int W, int SH, int SW, const float *__restrict__ cb,
-    const int32_t *__restrict__ rch) {
+    const int32_t *__restrict__ rch, const float *__restrict__ A2, int K2) {
     constexpr int WM = BM / (32 * TPM), WN = BN / (32 * TPN);
     static_assert(WM * WN == 4, "4 waves");
     constexpr int PT = BM / 32, NTW = BN / 32;                 // pixel / channel tiles
@@ -145,7 +145,10 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
 
     // this thread's A rows / K quads (row = t / 4 + 64 j, kq = t % 4)
     const int kq = t & 3;
-    const float *arow[AL];
+    // A2 (K2 > 0): the last K2 of the K input channels come from a second operand
+    // [M][K2] (a stage's first block: conv3 of h and the downsample of x, one GEMM)
+    const int K1 = K - K2;
+    const float *arow[AL], *arow2[AL];
 #pragma unroll
     for (int j = 0; j < AL; ++j) {
         int64_t m = m0 + (t >> 2) + 64 * j;
@@ -156,7 +159,8 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
             const int rem = (int)(m - n * hw), y = rem / Wo, x = rem - y * Wo;
             m = (n * SH + 2 * y) * (int64_t)SW + 2 * x;
         }
-        arow[j] = A + m * K + 4 * kq;
+        arow[j] = A + m * K1 + 4 * kq;
+        arow2[j] = K2 ? A2 + m * K2 + 4 * kq : arow[j];
     }
     // the workgroup's weight slice of stage s: NTW consecutive (s, t) blocks
     const uint4 *wsrc = Wp + (int64_t)(n0 / 32) * (3 * 64);
@@ -169,8 +173,9 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
 #define S3_LOAD(s_)                                                                       \
     do {                                                                                  \
         const int s = (s_) < nsteps ? (s_) : nsteps - 1;                                  \
+        const int k0_ = kStep * s;                                                        \
         _Pragma("unroll") for (int j = 0; j < AL; ++j) ar[j] =                            \
-            *reinterpret_cast<const float4 *>(arow[j] + kStep * s);                       \
+            *reinterpret_cast<const float4 *>(k0_ < K1 ? arow[j] + k0_ : arow2[j] + (k0_ - K1)); \
         _Pragma("unroll") for (int j = 0; j < WL; ++j) {                                  \
             const int i = t + kThreads * j;                                               \
             wr[j] = (WCELLS % kThreads == 0 || i < WCELLS) ? wsrc[s * wstep + i]          \
@@ -345,7 +350,8 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
 template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0, int OCC = 1>
 int launch_cfg(const float *A, int M, int K, const uint4 *Wp, int N, const float *bias,
                const float *R, float *D, int H, int W, int SH, int SW, hipStream_t s,
-               const float *cb = nullptr, const int32_t *rch = nullptr) {
+               const float *cb = nullptr, const int32_t *rch = nullptr,
+               const float *A2 = nullptr, int K2 = 0) {
     constexpr int PT = BM / 32, NTW = BN / 32;
     constexpr size_t lds = 2 * (size_t)(3 * PT + NTW * 3) * kFragBytes;
     static_assert(lds <= VD_LDS_BYTES, "LDS");
@@ -359,18 +365,19 @@ int launch_cfg(const float *A, int M, int K, const uint4 *Wp, int N, const float
     if (num_tiles >= (1ll << 31) - 8) return VD_ERR_SHAPE;
     const int64_t grid = (num_tiles + 7) / 8 * 8;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), lds, s, A, Wp, bias, R, D, M, N,
-                       K, tiles_n, (int)num_tiles, H, W, SH, SW, cb, rch);
+                       K, tiles_n, (int)num_tiles, H, W, SH, SW, cb, rch, A2, K2);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
 template <int BM, int BN, int TPM, int TPN, int OCC>
 int launch_epi(const float *A, int M, int K, const uint4 *Wp, int N, const float *bias,
-               const float *R, int relu, float *D, int H, int W, int SH, int SW, hipStream_t s) {
+               const float *R, int relu, float *D, int H, int W, int SH, int SW, hipStream_t s,
+               const float *A2, int K2) {
 #define VD_S3_RELU(RES_)                                                                       \
-    return relu ? launch_cfg<BM, BN, TPM, TPN, RES_, true, 0, OCC>(A, M, K, Wp, N, bias, R, D,  \
-                                                                   H, W, SH, SW, s)             \
-                : launch_cfg<BM, BN, TPM, TPN, RES_, false, 0, OCC>(A, M, K, Wp, N, bias, R, D, \
-                                                                    H, W, SH, SW, s)
+    return relu ? launch_cfg<BM, BN, TPM, TPN, RES_, true, 0, OCC>(                            \
+                      A, M, K, Wp, N, bias, R, D, H, W, SH, SW, s, nullptr, nullptr, A2, K2)   \
+                : launch_cfg<BM, BN, TPM, TPN, RES_, false, 0, OCC>(                           \
+                      A, M, K, Wp, N, bias, R, D, H, W, SH, SW, s, nullptr, nullptr, A2, K2)
     if (R && H > 0) VD_S3_RELU(2);
     if (R) VD_S3_RELU(1);
     VD_S3_RELU(0);
@@ -399,11 +406,13 @@ int launch_gemm_split3_weight(const float *W, int N, int K, void *Wp, hipStream_
 // x up_h x up_w, both even), read at the nearest-2x row of each pixel.  sub_h / sub_w
 // > 0: A is an images x sub_h x sub_w map read at stride 2 (M = images x ceil(sub_h / 2)
 // x ceil(sub_w / 2)): a stride-2 pad-0 1x1 convolution without the subsampled copy.
-int launch_gemm_split3(const float *A, int M, int K, const void *Wp, int N, const float *bias,
-                       const float *R, int up_h, int up_w, int sub_h, int sub_w, int relu,
-                       float *D, int cfg, hipStream_t s) {
+int launch_gemm_split3(const float *A, int M, int K, const float *A2, int K2, const void *Wp,
+                       int N, const float *bias, const float *R, int up_h, int up_w, int sub_h,
+                       int sub_w, int relu, float *D, int cfg, hipStream_t s) {
     if (M == 0) return VD_OK;
     if (!gemm_split3_supported(K, N)) return VD_ERR_SHAPE;
+    if (K2 < 0 || K2 >= K || (K2 && (!A2 || K2 % kStep || sub_h || sub_w))) return VD_ERR_ARG;
+    if (!K2) A2 = nullptr;
     if (sub_h || sub_w) {
         if (sub_h < 1 || sub_w < 1 || M % ((int64_t)((sub_h + 1) / 2) * ((sub_w + 1) / 2)))
             return VD_ERR_ARG;
@@ -430,18 +439,18 @@ int launch_gemm_split3(const float *A, int M, int K, const void *Wp, int N, cons
     case 1:
         if (N % 256) return VD_ERR_SHAPE;
         return launch_epi<256, 256, 4, 4, 1>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
-                                             s);
+                                             s, A2, K2);
     case 2:
         if (N % 128) return VD_ERR_SHAPE;
         return launch_epi<256, 128, 4, 2, 2>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
-                                             s);
+                                             s, A2, K2);
     case 4:
         if (N % 128) return VD_ERR_SHAPE;
         return launch_epi<128, 128, 2, 2, 3>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
-                                             s);
+                                             s, A2, K2);
     case 3:
         return launch_epi<256, 64, 4, 1, 2>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
-                                             s);
+                                             s, A2, K2);
 #ifdef VD_RESEARCH_PROBES
     case 11: case 12: case 13:  // speed-of-light probes of cfg 1 (wrong results by design)
         if (N % 256 || R || !relu) return VD_ERR_SHAPE;

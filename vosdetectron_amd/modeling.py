@@ -353,7 +353,14 @@ class Bottleneck(nn.Module):
             if self.fd.stride == (1, 1) and x.is_contiguous(memory_format=torch.channels_last):
                 # conv3 and the stride-1 downsample as one two-operand MFMA GEMM
                 N, _, H, W = out.shape
-                y = ops.gemm_dual_bias_act(_nhwc2d(out), _nhwc2d(x), self.w3d, self.b3d)
+                K = self.w3d.shape[1]
+                if ops.split3_enabled() and K >= ops.SPLIT3_MIN_K and K % 16 == 0 and \
+                        out.shape[1] % 16 == 0 and self.w3d.shape[0] % 64 == 0:
+                    # round 6: on the bf16 matrix cores at fp32 accuracy (split GEMM, A2)
+                    y = ops.gemm_split3_bias_act(_nhwc2d(out), ops.split3_weight_cached(self.w3d),
+                                                 self.b3d, a2=_nhwc2d(x))
+                else:
+                    y = ops.gemm_dual_bias_act(_nhwc2d(out), _nhwc2d(x), self.w3d, self.b3d)
                 if y is not None:
                     return y.view(N, H, W, -1).permute(0, 3, 1, 2)
             if s2:  # relu(h W3^T + b3 + (x[::2, ::2] Wd^T + bd))

@@ -626,17 +626,27 @@ def gemm_split3_bias_act(a: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor,
                          residual: Optional[torch.Tensor] = None, relu: bool = True,
                          out: Optional[torch.Tensor] = None, cfg: int = 0,
                          up_hw: Optional[Sequence[int]] = None,
-                         sub_hw: Optional[Sequence[int]] = None) -> torch.Tensor:
+                         sub_hw: Optional[Sequence[int]] = None,
+                         a2: Optional[torch.Tensor] = None) -> torch.Tensor:
     """act(a @ w.T + bias (+ residual)) with the fp32 operands split into three bf16
     pieces on the bf16 matrix cores (vd_gemm_split3_bias_act, fp32 accuracy):
     a [M,K], wp from gemm_split3_weight(w [N,K]), bias [N], out [M,N]; residual
     [M,N], or with up_hw = (H, W) the top-down map [M / (H W), H/2, W/2, N] of an
     FPN level added at the nearest-2x row of each pixel (FPN.py:292-300).  With
     sub_hw = (H, W): a is an images x H x W map's rows [images H W, K] read at
-    stride 2, M = images x ceil(H/2) x ceil(W/2) output rows (a stride-2 1x1 conv)."""
+    stride 2, M = images x ceil(H/2) x ceil(W/2) output rows (a stride-2 1x1 conv).
+    With a2 [M, K2]: w's last K2 input channels multiply a2 (a is [M, K - K2]): two
+    1x1 convs of two inputs summed in one GEMM."""
     a_ = _need(a, "a")
     N, K = wp.split3_shape
     M = a_.shape[0]
+    K2, a2_ = 0, None
+    if a2 is not None:
+        a2_ = _need(a2, "a2")
+        K2 = a2_.shape[1]
+        if a2_.shape[0] != M or a_.shape[1] + K2 != K or K2 % 16 or sub_hw is not None:
+            raise ValueError("gemm_split3_bias_act: a %s + a2 %s vs w (%d, %d)"
+                             % (tuple(a_.shape), tuple(a2_.shape), N, K))
     sh = sw = 0
     if sub_hw is not None:
         sh, sw = int(sub_hw[0]), int(sub_hw[1])
@@ -644,7 +654,7 @@ def gemm_split3_bias_act(a: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor,
             raise ValueError("a %s is not a stack of %s maps" % (tuple(a_.shape), (sh, sw)))
         M = M // (sh * sw) * ((sh + 1) // 2) * ((sw + 1) // 2)
     b_ = _need(bias, "bias")
-    if a_.dim() != 2 or a_.shape[1] != K or b_.numel() != N:
+    if a_.dim() != 2 or a_.shape[1] + K2 != K or b_.numel() != N:
         raise ValueError("gemm_split3_bias_act: a %s, w (%d, %d), bias %s"
                          % (tuple(a_.shape), N, K, tuple(b_.shape)))
     r_ = None
@@ -663,7 +673,9 @@ def gemm_split3_bias_act(a: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor,
         out = torch.empty((M, N), dtype=torch.float32, device=a_.device)
     elif tuple(out.shape) != (M, N) or not out.is_contiguous():
         raise ValueError("out must be a contiguous %s tensor" % ((M, N),))
-    check(lib().vd_gemm_split3_bias_act(a_.data_ptr(), M, K, wp.data_ptr(), N, b_.data_ptr(),
+    check(lib().vd_gemm_split3_bias_act(a_.data_ptr(), M, K,
+                                        a2_.data_ptr() if a2_ is not None else None, K2,
+                                        wp.data_ptr(), N, b_.data_ptr(),
                                         r_.data_ptr() if r_ is not None else None, uh, uw,
                                         sh, sw, int(relu), out.data_ptr(), int(cfg), _stream()),
           "vd_gemm_split3_bias_act")
