@@ -180,7 +180,8 @@ int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const 
  * images x sub_h x sub_w NHWC map read at stride 2 (M = images x ceil(sub_h/2) x
  * ceil(sub_w/2)): a stage's stride-2 1x1 convs (ResNet.py:246-294 with STRIDE_1X1, and
  * the downsample shortcut) without the subsampled copy.  cfg 0 picks the tile shape
- * (1: 256 pixels x 256 channels, 2: 256 x 128, 3: 256 x 64, 4: 128 x 128 per workgroup;
+ * (1: 256 pixels x 256 channels, 2: 256 x 128, 3: 256 x 64, 4: 128 x 128, 5: 256 x 256 in
+ * eight waves per workgroup;
  * VD_ERR_SHAPE when N does not divide by the tile's channels).  Replaces the same
  * fp32 convolutions / Linear layers as vd_gemm_bias_act (ResNet.py:246-294
  * bottleneck 1x1s, fast_rcnn_heads.py fc6 / fc7, mask_rcnn_heads.py upconv5). */

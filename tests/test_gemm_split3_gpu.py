@@ -40,11 +40,11 @@ def _errs(got, ref):
     (1000, 64, 256, False, True), (777, 128, 512, True, True), (4099, 256, 1024, False, False),
     (3000, 512, 2048, True, True), (2048, 1024, 256, False, True), (513, 2048, 512, True, False),
     (333, 1024, 12544, False, True), (64, 64, 16, False, True), (1, 256, 32, True, True)])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5])
 def test_split3_fp32_accuracy(M, N, K, res, relu, cfg):
     from vosdetectron_amd import ops
-    if (cfg == 1 and N % 256) or (cfg in (2, 4) and N % 128):
-        pytest.skip("tile needs N %% %d" % (256 if cfg == 1 else 128))
+    if (cfg in (1, 5) and N % 256) or (cfg in (2, 4) and N % 128):
+        pytest.skip("tile needs N %% %d" % (256 if cfg in (1, 5) else 128))
     a, w, b, r = _case(M, N, K, res, M + N + K)
     ref = _ref64(a, w, b, r, relu)
     got = ops.gemm_split3_bias_act(a, ops.gemm_split3_weight(w), b, residual=r, relu=relu,

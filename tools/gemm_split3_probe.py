@@ -79,7 +79,7 @@ def main():
         report("fp32", ms, out)
         wp = ops.gemm_split3_weight(w)
         for cfg in [int(c) for c in args.cfgs.split(",")]:
-            if (cfg in (1, 11, 12, 13) and N % 256) or (cfg in (2, 14, 16, 17, 18, 19) and N % 128) or \
+            if (cfg in (1, 11, 12, 13, 19) and N % 256) or (cfg in (2, 14, 15, 16, 17, 18) and N % 128) or \
                     (cfg >= 10 and r is not None):
                 continue
             out.zero_()

@@ -42,6 +42,8 @@
 // buffers: chunk c + 2's global loads are in registers while chunk c computes,
 // and chunk c + 1 (loaded one iteration earlier) is split into the other buffer
 // after chunk c's MFMAs, one barrier per chunk.
+#include <stdlib.h>
+
 #include "common.hpp"
 #include "vosdet_internal.hpp"
 
@@ -56,7 +58,6 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 
 constexpr int kStep = 16;           // fp32 K per pipeline stage (one MFMA k-step)
 constexpr int kFragBytes = 1024;    // one lane-linear 32 x 16 bf16 fragment
-constexpr int kThreads = 256;       // 4 waves, one per SIMD
 
 // Two fp32 -> three packed bf16 pairs (piece 0, 1, 2), round to nearest even.
 __device__ __forceinline__ void split_pair(float x0, float x1, uint32_t &p0, uint32_t &p1,
@@ -112,21 +113,23 @@ __global__ void split3_weight_kernel(const float *__restrict__ W, int N, int K,
 // classify weights [classes][256], cb its bias, rch each RoI's class channel, H = P
 // (the RoI map side), D = masks [RoIs][2P][2P]; the relu'd upconv output never leaves
 // the workgroup.
-template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0, int OCC = 1>
-__global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
+template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0, int OCC = 1,
+          int NW = 4>
+__global__ __launch_bounds__(64 * NW, OCC) void gemm_split3_kernel(
     const float *__restrict__ A, const uint4 *__restrict__ Wp, const float *__restrict__ bias,
     const float *__restrict__ R, float *__restrict__ D, int M, int N, int K, int tiles_n,
     int num_tiles, int H, int W, int SH, int SW, const float *__restrict__ cb,
     const int32_t *__restrict__ rch, const float *__restrict__ A2, int K2) {
-    constexpr int WM = BM / (32 * TPM), WN = BN / (32 * TPN);
-    static_assert(WM * WN == 4, "4 waves");
+    constexpr int WM = BM / (32 * TPM), WN = BN / (32 * TPN), NTH = 64 * NW;
+    static_assert(WM * WN == NW, "one (pixel, channel) block per wave");
     constexpr int PT = BM / 32, NTW = BN / 32;                 // pixel / channel tiles
     constexpr int A_BYTES = 3 * PT * kFragBytes;               // [piece][pt][lane]
     constexpr int W_BYTES = NTW * 3 * kFragBytes;              // [tw][piece][lane]
     constexpr int BUF = A_BYTES + W_BYTES;
-    constexpr int AL = BM * kStep / 4 / kThreads;              // A float4 loads per thread
-    constexpr int WCELLS = W_BYTES / 16, WL = (WCELLS + kThreads - 1) / kThreads;
-    static_assert(AL >= 1 && BM % 64 == 0, "A rows per thread");
+    constexpr int AL = BM * kStep / 4 / NTH;                   // A float4 loads per thread
+    constexpr int RPJ = NTH / 4;                               // A rows per load round
+    constexpr int WCELLS = W_BYTES / 16, WL = (WCELLS + NTH - 1) / NTH;
+    static_assert(AL >= 1 && BM % RPJ == 0, "A rows per thread");
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 
     // XCD-aware tile order: XCD x walks the x-th contiguous slice of the
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
     const int wm = w % WM, wn = w / WM;
     const int nsteps = K / kStep;
 
-    // this thread's A rows / K quads (row = t / 4 + 64 j, kq = t % 4)
+    // this thread's A rows / K quads (row = t / 4 + RPJ j, kq = t % 4)
     const int kq = t & 3;
     // A2 (K2 > 0): the last K2 of the K input channels come from a second operand
     // [M][K2] (a stage's first block: conv3 of h and the downsample of x, one GEMM)
@@ -151,7 +154,7 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
     const float *arow[AL], *arow2[AL];
 #pragma unroll
     for (int j = 0; j < AL; ++j) {
-        int64_t m = m0 + (t >> 2) + 64 * j;
+        int64_t m = m0 + (t >> 2) + RPJ * j;
         if (m >= M) m = M - 1;
         if (SH > 0) {  // A read at stride 2 from images x SH x SW (a strided 1x1 conv)
             const int Ho = (SH + 1) >> 1, Wo = (SW + 1) >> 1;
@@ -177,8 +180,8 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
         _Pragma("unroll") for (int j = 0; j < AL; ++j) ar[j] =                            \
             *reinterpret_cast<const float4 *>(k0_ < K1 ? arow[j] + k0_ : arow2[j] + (k0_ - K1)); \
         _Pragma("unroll") for (int j = 0; j < WL; ++j) {                                  \
-            const int i = t + kThreads * j;                                               \
-            wr[j] = (WCELLS % kThreads == 0 || i < WCELLS) ? wsrc[s * wstep + i]          \
+            const int i = t + NTH * j;                                                    \
+            wr[j] = (WCELLS % NTH == 0 || i < WCELLS) ? wsrc[s * wstep + i]               \
                                                            : make_uint4(0u, 0u, 0u, 0u);  \
         }                                                                                 \
     } while (0)
@@ -187,7 +190,7 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
     do {                                                                                  \
         unsigned char *base_ = lds + (buf) * BUF;                                         \
         _Pragma("unroll") for (int j = 0; j < AL; ++j) {                                  \
-            const int row = (t >> 2) + 64 * j, pt = row >> 5, r = row & 31;               \
+            const int row = (t >> 2) + RPJ * j, pt = row >> 5, r = row & 31;              \
             uint32_t p00, p10, p20, p01, p11, p21;                                        \
             split_pair(ar[j].x, ar[j].y, p00, p10, p20);                                  \
             split_pair(ar[j].z, ar[j].w, p01, p11, p21);                                  \
@@ -198,8 +201,8 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
                 make_uint2(p20, p21);                                                     \
         }                                                                                 \
         _Pragma("unroll") for (int j = 0; j < WL; ++j) {                                  \
-            const int i = t + kThreads * j;                                               \
-            if (WCELLS % kThreads == 0 || i < WCELLS)                                     \
+            const int i = t + NTH * j;                                                    \
+            if (WCELLS % NTH == 0 || i < WCELLS)                                          \
                 *reinterpret_cast<uint4 *>(base_ + A_BYTES + 16 * i) = wr[j];             \
         }                                                                                 \
     } while (0)
@@ -216,10 +219,13 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
     S3_STORE(0);
     S3_LOAD(1);
     __syncthreads();
+    bf16x8 wf[TPN][3], af[TPM][3];
 #pragma unroll 1
     for (int c = 0; c < nsteps; ++c) {
         const unsigned char *base = lds + (c & 1) * BUF;
-        bf16x8 wf[TPN][3], af[TPM][3];
+        // research probes 4 / 5: the fragments read once (MFMA stream alone, without /
+        // with the per-stage barrier)
+        if (PROBE < 4 || c == 0) {
 #pragma unroll
         for (int a = 0; a < TPM; ++a)
 #pragma unroll
@@ -232,6 +238,7 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
             for (int q = 0; q < 3; ++q)
                 wf[b][q] = *reinterpret_cast<const bf16x8 *>(
                     base + A_BYTES + ((wn * TPN + b) * 3 + q) * kFragBytes + lane * 16);
+        }
 #pragma unroll
         for (int b = 0; b < TPN; ++b)
 #pragma unroll
@@ -252,9 +259,9 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
         // stage c + 1 (its loads issued one stage ago) into the other buffer, whose
         // last readers passed the previous barrier; then stage c + 2's loads.  After
         // the last stage: a clamped copy into a buffer nobody reads.
-        if (PROBE != 2) S3_STORE((c + 1) & 1);
-        if (PROBE != 3) S3_LOAD(c + 2);
-        __syncthreads();
+        if (PROBE != 2 && PROBE < 4) S3_STORE((c + 1) & 1);
+        if (PROBE != 3 && PROBE < 4) S3_LOAD(c + 2);
+        if (PROBE != 4) __syncthreads();
     }
 #undef S3_LOAD
 #undef S3_STORE
@@ -262,11 +269,11 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
     // epilogue: lane = pixel (r), registers 4g..4g+3 = channels 8g + 4h .. + 3
     const int h = lane >> 5, r = lane & 31;
     if constexpr (RES == 3) {
-        static_assert(BN == 256 && WN == 2 && RELU, "one (i, j) group per workgroup");
+        static_assert(BN == 256 && RELU, "one (i, j) group per workgroup");
         // per pixel: sum over this wave's 128 channels of relu(acc + b) * Wc[class][co],
         // the two lane halves' channel sets added by a shuffle, the two channel waves
         // through LDS (the K loop's last barrier has passed: the buffers are free)
-        float *part = reinterpret_cast<float *>(lds);  // [BM] partials of wave wn = 1
+        float *part = reinterpret_cast<float *>(lds);  // [WN - 1][BM] partials, waves wn >= 1
         float dot[TPM];
 #pragma unroll
         for (int a = 0; a < TPM; ++a) {
@@ -289,9 +296,9 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
             }
             dot[a] = sacc + __shfl_xor(sacc, 32);
         }
-        if (wn == 1 && h == 0) {
+        if (wn >= 1 && h == 0) {
 #pragma unroll
-            for (int a = 0; a < TPM; ++a) part[(wm * TPM + a) * 32 + r] = dot[a];
+            for (int a = 0; a < TPM; ++a) part[(wn - 1) * BM + (wm * TPM + a) * 32 + r] = dot[a];
         }
         __syncthreads();
         if (wn == 0 && h == 0) {
@@ -302,7 +309,10 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
                 if (p >= M) continue;
                 const int roi = (int)(p / (P * P)), hw = (int)(p - (int64_t)roi * P * P);
                 const int y = hw / P, x = hw - y * P;
-                const float z = (dot[a] + part[(wm * TPM + a) * 32 + r]) + cb[rch[roi]];
+                float z = dot[a];
+#pragma unroll
+                for (int u = 1; u < WN; ++u) z += part[(u - 1) * BM + (wm * TPM + a) * 32 + r];
+                z += cb[rch[roi]];
                 D[((int64_t)roi * 2 * P + 2 * y + (ij >> 1)) * 2 * P + 2 * x + (ij & 1)] =
                     1.f / (1.f + __expf(-z));
             }
@@ -347,7 +357,8 @@ __global__ __launch_bounds__(kThreads, OCC) void gemm_split3_kernel(
     }
 }
 
-template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0, int OCC = 1>
+template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0, int OCC = 1,
+          int NW = 4>
 int launch_cfg(const float *A, int M, int K, const uint4 *Wp, int N, const float *bias,
                const float *R, float *D, int H, int W, int SH, int SW, hipStream_t s,
                const float *cb = nullptr, const int32_t *rch = nullptr,
@@ -355,7 +366,7 @@ int launch_cfg(const float *A, int M, int K, const uint4 *Wp, int N, const float
     constexpr int PT = BM / 32, NTW = BN / 32;
     constexpr size_t lds = 2 * (size_t)(3 * PT + NTW * 3) * kFragBytes;
     static_assert(lds <= VD_LDS_BYTES, "LDS");
-    auto kern = gemm_split3_kernel<BM, BN, TPM, TPN, RES, RELU, PROBE, OCC>;
+    auto kern = gemm_split3_kernel<BM, BN, TPM, TPN, RES, RELU, PROBE, OCC, NW>;
     static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  (int)lds) == hipSuccess;
@@ -364,19 +375,19 @@ int launch_cfg(const float *A, int M, int K, const uint4 *Wp, int N, const float
     const int64_t num_tiles = (int64_t)tiles_m * tiles_n;
     if (num_tiles >= (1ll << 31) - 8) return VD_ERR_SHAPE;
     const int64_t grid = (num_tiles + 7) / 8 * 8;
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), lds, s, A, Wp, bias, R, D, M, N,
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NW), lds, s, A, Wp, bias, R, D, M, N,
                        K, tiles_n, (int)num_tiles, H, W, SH, SW, cb, rch, A2, K2);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
-template <int BM, int BN, int TPM, int TPN, int OCC>
+template <int BM, int BN, int TPM, int TPN, int OCC, int NW = 4>
 int launch_epi(const float *A, int M, int K, const uint4 *Wp, int N, const float *bias,
                const float *R, int relu, float *D, int H, int W, int SH, int SW, hipStream_t s,
                const float *A2, int K2) {
 #define VD_S3_RELU(RES_)                                                                       \
-    return relu ? launch_cfg<BM, BN, TPM, TPN, RES_, true, 0, OCC>(                            \
+    return relu ? launch_cfg<BM, BN, TPM, TPN, RES_, true, 0, OCC, NW>(                        \
                       A, M, K, Wp, N, bias, R, D, H, W, SH, SW, s, nullptr, nullptr, A2, K2)   \
-                : launch_cfg<BM, BN, TPM, TPN, RES_, false, 0, OCC>(                           \
+                : launch_cfg<BM, BN, TPM, TPN, RES_, false, 0, OCC, NW>(                       \
                       A, M, K, Wp, N, bias, R, D, H, W, SH, SW, s, nullptr, nullptr, A2, K2)
     if (R && H > 0) VD_S3_RELU(2);
     if (R) VD_S3_RELU(1);
@@ -400,8 +411,9 @@ int launch_gemm_split3_weight(const float *W, int N, int K, void *Wp, hipStream_
 }
 
 // cfg: 0 = auto, 1 = 256 x 256 (one workgroup per CU), 2 = 256 x 128, 3 = 256 x 64 (two
-// per CU), 4 = 128 x 128 (three per CU) -- pixels x channels per workgroup; waves of
-// 128 x 128 / 128 x 64 / 128 x 32 / 64 x 64
+// per CU), 4 = 128 x 128 (three per CU), 5 = 256 x 256 with 8 waves (one per CU) --
+// pixels x channels per workgroup; waves of 128 x 128 / 128 x 64 / 128 x 32 / 64 x 64 /
+// 128 x 64
 // up_h / up_w > 0: R is the top-down map of an images x up_h x up_w level (M = images
 // x up_h x up_w, both even), read at the nearest-2x row of each pixel.  sub_h / sub_w
 // > 0: A is an images x sub_h x sub_w map read at stride 2 (M = images x ceil(sub_h / 2)
@@ -429,7 +441,18 @@ int launch_gemm_split3(const float *A, int M, int K, const float *A2, int K2, co
         // the step's shapes), the 256 x 256 single workgroup only for very deep K
         // (fc6, K = 12,544: 4 % faster), 256 x 64 where N is not a multiple of 128
         // (profiles/r06/gemm_split3/)
-        cfg = (N % 256 == 0 && K >= 4096) ? 1 : (N % 128 == 0 ? 2 : 3);
+        cfg = N % 128 == 0 ? 2 : 3;
+        // 256 x 256 tiles with eight 128 x 64 waves (one workgroup per CU, the A split
+        // shared by twice the channels) for deep K, large M, and fc7-like shapes: 2-7 %
+        // faster than 256 x 128 there, slower on the few-tile res4 / res5 shapes
+        // (VOSDET_SPLIT3_WIDE=0 keeps 256 x 128: A/B runs)
+        static const bool wide = [] {
+            const char *e = getenv("VOSDET_SPLIT3_WIDE");
+            return !(e && e[0] == '0');
+        }();
+        if (wide && N % 256 == 0 &&
+            (K >= 4096 || M >= 500000 || (N >= 1024 && M <= 65536 && K >= 1024)))
+            cfg = 5;
         // 128 x 128 tiles at three workgroups per CU where 256 x 128 would give fewer
         // than three workgroups per slot (res4 / res5 at 32 frames, N <= 512): more
         // workgroups in flight, 5-15 % faster there (profiles/r06/gemm_split3/)
@@ -444,6 +467,10 @@ int launch_gemm_split3(const float *A, int M, int K, const float *A2, int K2, co
         if (N % 128) return VD_ERR_SHAPE;
         return launch_epi<256, 128, 4, 2, 2>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
                                              s, A2, K2);
+    case 5:
+        if (N % 256) return VD_ERR_SHAPE;
+        return launch_epi<256, 256, 4, 2, 1, 8>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h,
+                                                sub_w, s, A2, K2);
     case 4:
         if (N % 128) return VD_ERR_SHAPE;
         return launch_epi<128, 128, 2, 2, 3>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
@@ -457,6 +484,10 @@ int launch_gemm_split3(const float *A, int M, int K, const float *A2, int K2, co
         if (cfg == 11) return launch_cfg<256, 256, 4, 4, 0, true, 1>(A, M, K, w, N, bias, R, D, 0, 0, 0, 0, s);
         if (cfg == 12) return launch_cfg<256, 256, 4, 4, 0, true, 2>(A, M, K, w, N, bias, R, D, 0, 0, 0, 0, s);
         return launch_cfg<256, 256, 4, 4, 0, true, 3>(A, M, K, w, N, bias, R, D, 0, 0, 0, 0, s);
+    case 14: case 15:  // cfg 2: MFMA stream alone (fragments read once), without / with barriers
+        if (N % 128 || R || !relu) return VD_ERR_SHAPE;
+        if (cfg == 14) return launch_cfg<256, 128, 4, 2, 0, true, 4, 2>(A, M, K, w, N, bias, R, D, 0, 0, 0, 0, s);
+        return launch_cfg<256, 128, 4, 2, 0, true, 5, 2>(A, M, K, w, N, bias, R, D, 0, 0, 0, 0, s);
     case 16: case 17: case 18:  // the same probes of cfg 2
         if (N % 128 || R || !relu) return VD_ERR_SHAPE;
         if (cfg == 16) return launch_cfg<256, 128, 4, 2, 0, true, 1, 2>(A, M, K, w, N, bias, R, D, 0, 0, 0, 0, s);
@@ -474,9 +505,10 @@ int launch_gemm_split3_mask_logits(const float *A, int M, int K, const void *Wp,
     if (M == 0) return VD_OK;
     if (N != 4 * 256 || !gemm_split3_supported(K, N)) return VD_ERR_SHAPE;
     if (P < 1 || M % (P * P) || !cls_w || !cls_b || !roi_ch || !masks) return VD_ERR_ARG;
-    return launch_cfg<256, 256, 4, 4, 3, true, 0, 1>(A, M, K, reinterpret_cast<const uint4 *>(Wp),
-                                                     N, bias, cls_w, masks, P, P, 0, 0, s,
-                                                     cls_b, roi_ch);
+    return launch_cfg<256, 256, 4, 2, 3, true, 0, 1, 8>(A, M, K,
+                                                        reinterpret_cast<const uint4 *>(Wp), N,
+                                                        bias, cls_w, masks, P, P, 0, 0, s, cls_b,
+                                                        roi_ch);
 }
 
 }  // namespace vd
