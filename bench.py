@@ -423,6 +423,44 @@ def measure_dominant_conv(dev, F, H, W, C=256, iters=None):
 MFMA_BF16_PEAK_TFS = 2516.6  # dense bf16 matrix peak: 256 CUs x 4 SIMDs x 1024 flop/clk x 2.4 GHz
 
 
+def measure_split_gemm(dev, M=32000, N=1024, K=12544, iters=10):
+    """The largest split-bf16 GEMM of the step, fc6 of the 32-frame box head (32,000 RoIs
+    x 12,544 -> 1,024, ReLU), timed alone with HIP events on its stream: fp32 work per
+    second, and the bf16 matrix-core work it executes (six bf16 products per fp32 MAC)
+    as a fraction of the dense bf16 peak."""
+    from vosdetectron_amd import ops
+    if not ops.split3_enabled():
+        return None
+    g = torch.Generator(device=dev).manual_seed(5)
+    a = torch.randn((M, K), generator=g, device=dev).relu_()
+    w = torch.randn((N, K), generator=g, device=dev) / K ** .5
+    b = torch.zeros((N,), device=dev)
+    wp = ops.gemm_split3_weight(w)
+    out = torch.empty((M, N), device=dev)
+    for _ in range(2):
+        ops.gemm_split3_bias_act(a, wp, b, out=out)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        ops.gemm_split3_bias_act(a, wp, b, out=out)
+    e1.record(s)
+    e1.synchronize()
+    t = e0.elapsed_time(e1) / 1e3 / iters
+    flops = 2.0 * M * N * K
+    del a, w, wp, out
+    return {"kernel": "vd::gemm_split3_kernel (three-piece bf16 split, six "
+                      "v_mfma_f32_32x32x16_bf16 products per fp32 MAC)",
+            "shape": [M, N, K], "avg_launch_us": round(t * 1e6, 1),
+            "fp32_work_TFs": round(flops / t / 1e12, 1),
+            "fp32_matrix_peak_TFs": MFMA_FP32_PEAK_TFS,
+            "bf16_executed_TFs": round(6 * flops / t / 1e12, 1),
+            "bf16_peak_TFs": MFMA_BF16_PEAK_TFS,
+            "frac": round(6 * flops / t / 1e12 / MFMA_BF16_PEAK_TFS, 4),
+            "how": "HIP events over %d launches; frac = executed bf16 MFMA work / the dense "
+                   "bf16 peak (fp32_work_TFs exceeds the fp32 matrix peak by design)" % iters}
+
+
 def step_roofline(flops_frame, dets_cpu, frames, ms_per_step, engine_launch, frame_hw, blob_hw,
                   wino_flops_frame=0, wino4_flops_frame=0, split3_flops_frame=0):
     """the FPS as a fraction of the roofline = sum of per-stage
@@ -1157,6 +1195,7 @@ def main():
         if not vos and cfg.FPN.FPN_ON:
             extra["dominant_kernel"] = measure_dominant_conv(
                 dev, F, getattr(pipe, "Hp", fh) // 4, getattr(pipe, "Wp", fw) // 4)
+            extra["split_gemm"] = measure_split_gemm(dev, M=F * 1000)
         nthr = torch.get_num_threads()
         torch.set_num_threads(cpu_share()[0])
         flops, dets_cpu, wino_flops, wino4_flops, split3_flops = frame_flops(sd, cfg, F)

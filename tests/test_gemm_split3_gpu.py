@@ -238,3 +238,22 @@ def test_split3_two_operands(M, K1, K2, N):
     ref = (torch.cat([h, x], 1).double() @ w.double().t() + b.double()).relu()
     mx, _ = _errs(got, ref)
     assert mx <= 2e-5, mx
+
+
+def test_split3_weight_image_is_the_rne_split():
+    """vd_gemm_split3_weight's image holds, bit for bit, the round-to-nearest-even bf16
+    pieces torch's own conversion gives (tests/test_split3_cpu.py's arithmetic), in the
+    [K/16][N/32][piece][lane = 32 h + r][8] order: W[32 t + r][16 s + 8 h + j]."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(7)
+    N, K = 128, 64
+    w = (torch.randn(N, K, device=DEV, generator=g) *
+         torch.logspace(-20, 20, K, device=DEV)[None, :])
+    img = ops.gemm_split3_weight(w).view(torch.int16).view(K // 16, N // 32, 3, 2, 32, 8)
+    x0 = w.to(torch.bfloat16).float()
+    x1 = (w - x0).to(torch.bfloat16).float()
+    x2 = (w - x0 - x1).to(torch.bfloat16).float()
+    for p, piece in enumerate((x0, x1, x2)):
+        ref = piece.to(torch.bfloat16).view(torch.int16)           # [N][K]
+        ref = ref.view(N // 32, 32, K // 16, 2, 8).permute(2, 0, 3, 1, 4)  # [s][t][h][r][j]
+        assert torch.equal(img[:, :, p], ref), p
