@@ -461,6 +461,16 @@ int vd_stem_weight_pack(const float *w, float *packed, void *stream);
 int vd_stem_conv_pool(const float *x, int N, int H, int W, const float *packed, const float *bias,
                       float *y, void *stream);
 
+/* The same stem with conv1 on the bf16 matrix cores at fp32 accuracy (round 6; the
+ * three-piece bf16 split of gemm_split3, six piece products per fp32 product, fp32
+ * accumulate): vd_stem_split_weight_pack splits the PyTorch weight [64][3][7][7] into
+ * vd_stem_split_weight_size() bytes once; vd_stem_split_conv_pool takes that image and
+ * is otherwise vd_stem_conv_pool. */
+size_t vd_stem_split_weight_size(void);
+int vd_stem_split_weight_pack(const float *w, void *packed, void *stream);
+int vd_stem_split_conv_pool(const float *x, int N, int H, int W, const void *packed,
+                            const float *bias, float *y, void *stream);
+
 /* utils.boxes.soft_nms (lib/utils/boxes.py:336-355 -> cython_nms.soft_nms,
  * cython_nms.pyx:98-203) on the device: dets n x dets_stride (>= 5) float32
  * [x1, y1, x2, y2, score]; method 0 hard / 1 linear / 2 gaussian.  Writes the

@@ -96,6 +96,9 @@ SIGNATURES = {
     "vd_stem_weight_size": (_S, []),
     "vd_stem_weight_pack": (_I, [_P, _P, _P]),
     "vd_stem_conv_pool": (_I, [_P, _I, _I, _I, _P, _P, _P, _P]),
+    "vd_stem_split_weight_size": (_S, []),
+    "vd_stem_split_weight_pack": (_I, [_P, _P, _P]),
+    "vd_stem_split_conv_pool": (_I, [_P, _I, _I, _I, _P, _P, _P, _P]),
     "vd_soft_nms": (_I, [_P, _I, _I, _F, _F, _F, _I, _P, _P, _P, _P]),
     "vd_box_voting": (_I, [_P, _I, _I, _P, _I, _I, _F, _I, _F, _P, _P]),
     "vd_image_to_blob": (_I, [_P, _I, _I, _I, _P, _I, _I, _I, _P, _P]),

@@ -389,6 +389,20 @@ int vd_stem_conv_pool(const float *x, int N, int H, int W, const float *packed, 
     return launch_stem_conv_pool(x, N, H, W, packed, bias, y, 0, VD_STREAM(stream));
 }
 
+size_t vd_stem_split_weight_size(void) { return stem_weight_split_bytes(); }
+
+int vd_stem_split_weight_pack(const float *w, void *packed, void *stream) {
+    if (!w || !packed) return VD_ERR_ARG;
+    return launch_stem_weight_split(w, packed, VD_STREAM(stream));
+}
+
+int vd_stem_split_conv_pool(const float *x, int N, int H, int W, const void *packed,
+                            const float *bias, float *y, void *stream) {
+    if ((int64_t)N * H * W > 0 && (!x || !packed || !bias || !y)) return VD_ERR_ARG;
+    return launch_stem_conv_pool(x, N, H, W, static_cast<const float *>(packed), bias, y, 0,
+                                 VD_STREAM(stream), true);
+}
+
 int vd_soft_nms(const float *dets, int n, int dets_stride, float sigma, float overlap_thresh,
                 float score_thresh, int method, float *dets_out, int64_t *keep_out,
                 int32_t *count_out, void *stream) {

@@ -23,6 +23,22 @@ namespace vd {
 namespace {
 
 typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// two fp32 -> three packed bf16 pairs, round to nearest even (gemm_split3.hip)
+__device__ __forceinline__ void split_pair(float x0, float x1, uint32_t &p0, uint32_t &p1,
+                                           uint32_t &p2) {
+    const f2v x = {x0, x1};
+    const uint32_t uh = __builtin_bit_cast(uint32_t, __builtin_convertvector(x, bf16x2));
+    const f2v r1 = x - f2v{__uint_as_float(uh << 16), __uint_as_float(uh & 0xffff0000u)};
+    const uint32_t um = __builtin_bit_cast(uint32_t, __builtin_convertvector(r1, bf16x2));
+    const f2v r2 = r1 - f2v{__uint_as_float(um << 16), __uint_as_float(um & 0xffff0000u)};
+    p0 = uh;
+    p1 = um;
+    p2 = __builtin_bit_cast(uint32_t, __builtin_convertvector(r2, bf16x2));
+}
 
 constexpr int kPY = 7, kPX = 8;                       // pooled outputs per tile
 constexpr int kCY = 2 * kPY + 1, kCX = 2 * kPX + 1;   // 15 x 17 conv outputs
@@ -31,9 +47,9 @@ constexpr int kIY = 2 * (kCY - 1) + 7, kIX = 2 * (kCX - 1) + 7;  // 35 x 39 inpu
 constexpr int kRow = 3 * kIX;                         // 117 floats per patch row
 constexpr int kPatch = kIY * kRow;                    // 4095 floats
 constexpr int kKS = 37;                               // k-steps of 4 (K = 147 + 1 zero)
-constexpr int kThreads = 256;
-constexpr int kPB = 4;                                // conv-pixel blocks per wave
-constexpr int kPer = (kPatch + kThreads - 1) / kThreads;  // 16 patch floats per thread
+constexpr int kKS3 = 5;                               // SPLIT: k-steps of 32 (K = 160)
+constexpr int kThreadsF = 256;                        // fp32 core: 4 waves of 4 pixel blocks
+constexpr int kThreadsS = 512;                        // SPLIT: 8 waves (2 a SIMD) of 2
 constexpr int kOutPitch = 68;                         // floats per conv pixel in LDS
 
 // patch offset (floats) of k = (ky, kx, ci) = 21 ky + 3 kx + ci; k = 147 is the
@@ -44,22 +60,43 @@ __device__ __forceinline__ int koff(int k) {
     return k + (kRow - 21) * ky;
 }
 
-__global__ __launch_bounds__(kThreads, 1) void stem_conv_pool_kernel(
+// SPLIT (round 6, the default): conv1 on the bf16 matrix cores at fp32 accuracy --
+// v_mfma_f32_16x16x32_bf16 over K = 160 (5 k-steps; k >= 147 zero weights), every fp32
+// operand split into three bf16 pieces and the six largest piece products accumulated
+// (gemm_split3.hip's scheme): the weights pre-split once (stem_weight_split_kernel,
+// 240 dwords a lane held for the workgroup's lifetime), each pixel's eight patch
+// values of a k-step split as they are read.  6 x 80 bf16 MFMAs of 16 cycles per
+// wave and tile against 592 fp32 MFMAs of 32.
+template <bool SPLIT, int NT>
+__global__ __launch_bounds__(NT, 1) void stem_conv_pool_kernel(
     const float *__restrict__ X, int N, int H, int W, const float *__restrict__ Wp,
     const float *__restrict__ bias, float *__restrict__ Y, int Hc, int Wc, int Hp, int Wp_,
     int tiles_y, int tiles_x, int ntiles) {
     __shared__ __attribute__((aligned(16))) float patch[kPatch + 1];
     __shared__ __attribute__((aligned(16))) float outs[256 * kOutPitch];
+    constexpr int kThreads = NT;
+    constexpr int kPB = 1024 / NT;  // conv-pixel blocks per wave (16 blocks of 16)
+    constexpr int kPer = (kPatch + NT - 1) / NT;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int j = lane & 15, q = lane >> 4;
 
-    // the lane's weights: A[co = 16 b + j][k = 4 s + q]
-    float wr[kKS][4];
+    // the lane's weights: A[co = 16 b + j][k = 4 s + q] (fp32), or (SPLIT) the three
+    // bf16 pieces of A[co = 16 b + j][k = 32 s + 8 q .. + 7]
+    constexpr int kWS = SPLIT ? 1 : kKS;
+    float wr[kWS][4];
+    // (SPLIT: the 61 KiB split image sits in LDS, lane-linear 16-byte fragments read
+    // with ds_read_b128 -- held in registers it spills)
+    __shared__ __attribute__((aligned(16))) uint4 wl[SPLIT ? kKS3 * 4 * 3 * 64 : 1];
+    if constexpr (SPLIT) {
+        const uint4 *w4 = reinterpret_cast<const uint4 *>(Wp);
+        for (int i = tid; i < kKS3 * 4 * 3 * 64; i += kThreads) wl[i] = w4[i];
+    } else {
 #pragma unroll
-    for (int s = 0; s < kKS; ++s)
+        for (int s = 0; s < kKS; ++s)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) wr[s][b] = Wp[(s * 4 + b) * 64 + lane];
+            for (int b = 0; b < 4; ++b) wr[s][b] = Wp[(s * 4 + b) * 64 + lane];
+    }
 
     // the lane's conv pixels (column j of blocks kPB wave + pb): patch base
     // offsets; pixel 255 is padding and reads pixel 254
@@ -114,6 +151,46 @@ __global__ __launch_bounds__(kThreads, 1) void stem_conv_pool_kernel(
         for (int pb = 0; pb < kPB; ++pb)
 #pragma unroll
             for (int b = 0; b < 4; ++b) acc[pb][b] = f4v{0.f, 0.f, 0.f, 0.f};
+        if constexpr (SPLIT) {
+#pragma unroll
+            for (int s = 0; s < kKS3; ++s) {
+                int ko[8];  // patch offsets of the lane's k values
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) ko[jj] = koff(32 * s + 8 * q + jj);
+                bf16x8 bp[kPB][3];  // the pixels' pieces
+#pragma unroll
+                for (int pb = 0; pb < kPB; ++pb) {
+                    float v[8];
+#pragma unroll
+                    for (int jj = 0; jj < 8; ++jj) v[jj] = patch[pbase[pb] + ko[jj]];
+                    uint32_t p0[4], p1[4], p2[4];
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+                        split_pair(v[2 * jj], v[2 * jj + 1], p0[jj], p1[jj], p2[jj]);
+                    bp[pb][0] = __builtin_bit_cast(bf16x8, make_uint4(p0[0], p0[1], p0[2], p0[3]));
+                    bp[pb][1] = __builtin_bit_cast(bf16x8, make_uint4(p1[0], p1[1], p1[2], p1[3]));
+                    bp[pb][2] = __builtin_bit_cast(bf16x8, make_uint4(p2[0], p2[1], p2[2], p2[3]));
+                }
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    bf16x8 w[3];
+#pragma unroll
+                    for (int pc = 0; pc < 3; ++pc)
+                        w[pc] = __builtin_bit_cast(bf16x8, wl[((s * 4 + b) * 3 + pc) * 64 + lane]);
+#pragma unroll
+                    for (int pb = 0; pb < kPB; ++pb) {
+                        f4v x = acc[pb][b];
+                        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2], bp[pb][0], x, 0, 0, 0);
+                        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], bp[pb][1], x, 0, 0, 0);
+                        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], bp[pb][2], x, 0, 0, 0);
+                        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], bp[pb][0], x, 0, 0, 0);
+                        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], bp[pb][1], x, 0, 0, 0);
+                        x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], bp[pb][0], x, 0, 0, 0);
+                        acc[pb][b] = x;
+                    }
+                }
+            }
+        } else {
 #pragma unroll
         for (int s = 0; s < kKS; ++s) {
             const int o = koff(4 * s + q);
@@ -126,6 +203,7 @@ __global__ __launch_bounds__(kThreads, 1) void stem_conv_pool_kernel(
                 for (int b = 0; b < 4; ++b)
                     acc[pb][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[s][b], v[pb], acc[pb][b],
                                                                       0, 0, 0);
+        }
         }
         // D[co = 16 b + 4 q + r][pixel j] -> outs[pixel][co]
 #pragma unroll
@@ -192,9 +270,42 @@ __global__ void stem_weight_kernel(const float *__restrict__ w, float *__restric
     Wp[i] = v;
 }
 
+// SPLIT weights: Wp3[s][b][piece][lane][8 bf16] = piece of w[co = 16 b + lane % 16]
+// [k = 32 s + 8 (lane / 16) + j], k = (ky, kx, ci); k >= 147 -> 0
+__global__ void stem_weight_split_kernel(const float *__restrict__ w, uint4 *__restrict__ Wp3) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= kKS3 * 4 * 64) return;
+    const int lane = i & 63, b = (i >> 6) & 3, s = i >> 8;
+    const int co = 16 * b + (lane & 15), k0 = 32 * s + 8 * (lane >> 4);
+    float v[8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+        const int k = k0 + jj;
+        v[jj] = 0.f;
+        if (k < 147) {
+            const int ky = k / 21, r = k - (k / 21) * 21, kx = r / 3, ci = r - (r / 3) * 3;
+            v[jj] = w[((co * 3 + ci) * 7 + ky) * 7 + kx];
+        }
+    }
+    uint32_t p[3][4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) split_pair(v[2 * jj], v[2 * jj + 1], p[0][jj], p[1][jj], p[2][jj]);
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc)
+        Wp3[((s * 4 + b) * 3 + pc) * 64 + lane] = make_uint4(p[pc][0], p[pc][1], p[pc][2], p[pc][3]);
+}
+
 }  // namespace
 
 size_t stem_weight_floats() { return (size_t)kKS * 4 * 64; }
+
+size_t stem_weight_split_bytes() { return (size_t)kKS3 * 4 * 3 * 64 * 16; }
+
+int launch_stem_weight_split(const float *w, void *Wp3, hipStream_t s) {
+    hipLaunchKernelGGL(stem_weight_split_kernel, dim3((kKS3 * 256 + 255) / 256), dim3(256), 0, s,
+                       w, reinterpret_cast<uint4 *>(Wp3));
+    return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
+}
 
 int launch_stem_weight(const float *w, float *Wp, hipStream_t s) {
     hipLaunchKernelGGL(stem_weight_kernel, dim3((kKS * 256 + 255) / 256), dim3(256), 0, s, w, Wp);
@@ -202,7 +313,7 @@ int launch_stem_weight(const float *w, float *Wp, hipStream_t s) {
 }
 
 int launch_stem_conv_pool(const float *X, int N, int H, int W, const float *Wp, const float *bias,
-                          float *Y, int num_cus, hipStream_t s) {
+                          float *Y, int num_cus, hipStream_t s, bool split) {
     if (N < 0 || H < 0 || W < 0) return VD_ERR_SHAPE;
     if ((int64_t)N * H * W == 0) return VD_OK;
     const int Hc = (H - 1) / 2 + 1, Wc = (W - 1) / 2 + 1;   // (H + 6 - 7) / 2 + 1
@@ -223,8 +334,14 @@ int launch_stem_conv_pool(const float *X, int N, int H, int W, const float *Wp, 
     int g = num_cus;
     g = g / 8 * 8;
     if (g < 8) g = 8;
-    hipLaunchKernelGGL(stem_conv_pool_kernel, dim3(g), dim3(kThreads), 0, s, X, N, H, W, Wp, bias,
-                       Y, Hc, Wc, Hp, Wp_, tiles_y, tiles_x, (int)ntiles);
+    if (split)
+        hipLaunchKernelGGL((stem_conv_pool_kernel<true, kThreadsS>), dim3(g), dim3(kThreadsS), 0, s,
+                           X, N, H, W,
+                           Wp, bias, Y, Hc, Wc, Hp, Wp_, tiles_y, tiles_x, (int)ntiles);
+    else
+        hipLaunchKernelGGL((stem_conv_pool_kernel<false, kThreadsF>), dim3(g), dim3(kThreadsF), 0, s,
+                           X, N, H, W,
+                           Wp, bias, Y, Hc, Wc, Hp, Wp_, tiles_y, tiles_x, (int)ntiles);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 

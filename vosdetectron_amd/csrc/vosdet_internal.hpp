@@ -134,8 +134,10 @@ int launch_box_detections(const float *rois, const float *cls_prob, const float 
 size_t box_detections_workspace_bytes(int R_cap, int num_images, int num_classes);
 size_t stem_weight_floats();
 int launch_stem_weight(const float *w, float *Wp, hipStream_t s);
+size_t stem_weight_split_bytes();
+int launch_stem_weight_split(const float *w, void *Wp3, hipStream_t s);
 int launch_stem_conv_pool(const float *X, int N, int H, int W, const float *Wp, const float *bias,
-                          float *Y, int num_cus, hipStream_t s);
+                          float *Y, int num_cus, hipStream_t s, bool split = false);
 int launch_soft_nms(const float *dets, int n, int stride, float sigma, float overlap_thresh,
                     float score_thresh, int method, float *dets_out, int64_t *keep_out,
                     int32_t *count_out, hipStream_t s);

@@ -517,7 +517,9 @@ def _fold(conv: nn.Conv2d, aff: AffineChannel2d) -> nn.Conv2d:
 
 class _StemEpilogue(nn.Module):
     """Folded stem: conv1 + bias + ReLU + max-pool in one MFMA kernel
-    (vd_stem_conv_pool; VOSDET_STEM=miopen: conv1 on MIOpen + one epilogue pass)."""
+    (VOSDET_STEM=split, the default: vd_stem_split_conv_pool, conv1 on the bf16 matrix
+    cores at fp32 accuracy; =fused: vd_stem_conv_pool, fp32 MFMA; =miopen: conv1 on
+    MIOpen + one epilogue pass)."""
 
     def __init__(self, conv1, maxpool):
         super().__init__()
@@ -525,7 +527,8 @@ class _StemEpilogue(nn.Module):
 
     def _fused_ok(self, x):
         c = self.conv1
-        return (os.environ.get("VOSDET_STEM", "fused") == "fused" and c.bias is not None
+        return (os.environ.get("VOSDET_STEM", "split") in ("split", "fused")
+                and c.bias is not None
                 and tuple(c.weight.shape) == (64, 3, 7, 7) and c.stride == (2, 2)
                 and c.padding == (3, 3) and c.dilation == (1, 1) and c.groups == 1
                 and x.shape[1] == 3 and x.is_contiguous(memory_format=torch.channels_last)
@@ -534,9 +537,10 @@ class _StemEpilogue(nn.Module):
     def forward(self, x):
         if x.is_cuda:
             if self._fused_ok(x):  # conv + bias + ReLU + max-pool in one MFMA kernel
-                key = (self.conv1.weight.data_ptr(), self.conv1.weight._version)
+                split = os.environ.get("VOSDET_STEM", "split") == "split"
+                key = (self.conv1.weight.data_ptr(), self.conv1.weight._version, split)
                 if getattr(self, "_stem_key", None) != key:
-                    self._stem_packed = ops.stem_pack(self.conv1.weight)
+                    self._stem_packed = ops.stem_pack(self.conv1.weight, split=split)
                     self._stem_key = key
                 return ops.stem_conv_pool(x, self._stem_packed, self.conv1.bias)
             h = _conv_nb(self.conv1, x)

@@ -1245,11 +1245,18 @@ def bias_relu_maxpool(x_raw: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def stem_pack(weight: torch.Tensor) -> torch.Tensor:
-    """conv1's weight [64, 3, 7, 7] in vd_stem_conv_pool's register order (once)."""
+def stem_pack(weight: torch.Tensor, split: bool = False) -> torch.Tensor:
+    """conv1's weight [64, 3, 7, 7] in vd_stem_conv_pool's register order (once), or
+    (split) its three-piece bf16 image for vd_stem_split_conv_pool (a uint8 tensor)."""
     w = _need(weight, "weight")
     if tuple(w.shape) != (64, 3, 7, 7):
         raise ValueError("stem weight must be 64 x 3 x 7 x 7, got %s" % (tuple(w.shape),))
+    if split:
+        out = torch.empty((lib().vd_stem_split_weight_size(),), dtype=torch.uint8,
+                          device=w.device)
+        check(lib().vd_stem_split_weight_pack(w.data_ptr(), out.data_ptr(), _stream()),
+              "vd_stem_split_weight_pack")
+        return out
     out = torch.empty((lib().vd_stem_weight_size() // 4,), dtype=torch.float32, device=w.device)
     check(lib().vd_stem_weight_pack(w.data_ptr(), out.data_ptr(), _stream()),
           "vd_stem_weight_pack")
@@ -1257,7 +1264,8 @@ def stem_pack(weight: torch.Tensor) -> torch.Tensor:
 
 
 def stem_conv_pool(x: torch.Tensor, packed: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
-    """ResNet stem in one kernel (vd_stem_conv_pool): MaxPool2d(3, 2, 1)(relu(conv1 7x7/2
+    """ResNet stem in one kernel (vd_stem_conv_pool, or vd_stem_split_conv_pool for a
+    split image from stem_pack(w, split=True)): MaxPool2d(3, 2, 1)(relu(conv1 7x7/2
     pad 3 (x) + bias)) for a channels_last N x 3 x H x W blob; returns channels_last
     N x 64 x Ho x Wo (the conv output never leaves LDS)."""
     N, C, H, W = x.shape
@@ -1267,12 +1275,17 @@ def stem_conv_pool(x: torch.Tensor, packed: torch.Tensor, bias: torch.Tensor) ->
     b = _need(bias, "bias")
     if b.numel() != 64:
         raise ValueError("bias must have 64 entries")
+    split = packed.dtype == torch.uint8
+    need = lib().vd_stem_split_weight_size() if split else lib().vd_stem_weight_size()
+    if not packed.is_cuda or packed.numel() * packed.element_size() != need:
+        raise ValueError("packed must be stem_pack's device image (%d bytes)" % need)
     Hc, Wc = (H - 1) // 2 + 1, (W - 1) // 2 + 1
     Ho, Wo = (Hc - 1) // 2 + 1, (Wc - 1) // 2 + 1
     out = torch.empty((N, 64, Ho, Wo), dtype=torch.float32, device=x.device,
                       memory_format=torch.channels_last)
-    check(lib().vd_stem_conv_pool(x.data_ptr(), N, H, W, packed.data_ptr(), b.data_ptr(),
-                                  out.data_ptr(), _stream()), "vd_stem_conv_pool")
+    fn = lib().vd_stem_split_conv_pool if split else lib().vd_stem_conv_pool
+    check(fn(x.data_ptr(), N, H, W, packed.data_ptr(), b.data_ptr(), out.data_ptr(), _stream()),
+          "vd_stem_split_conv_pool" if split else "vd_stem_conv_pool")
     return out
 
 
