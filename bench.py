@@ -312,6 +312,9 @@ class _WinoFlops(torch.overrides.TorchFunctionMode):
                 if tuple(w.shape[2:]) == (1, 1) and w.shape[1] >= ops.SPLIT3_MIN_K and \
                         w.shape[1] % 16 == 0 and w.shape[0] % 64 == 0:
                     self.split3 += 2 * out.numel() * w.shape[1]
+                elif (tuple(w.shape) == (64, 3, 7, 7)
+                      and os.environ.get("VOSDET_STEM", "split") == "split"):
+                    self.split3 += 2 * out.numel() * 147  # the split-bf16 stem
             elif func in (torch.nn.functional.conv_transpose2d, torch.conv_transpose2d):
                 x, w = args[0], args[1]  # w: Cin x Cout x kh x kw
                 n = w.shape[1] * w.shape[2] * w.shape[3]
@@ -1220,7 +1223,8 @@ def main():
             "value": round(fps, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-            "arith": "fp32 tensors end to end; the 1x1 convs / fc layers with K >= %d run on "
+            "arith": "fp32 tensors end to end; the 1x1 convs / fc layers with K >= %d and "
+                     "the stem's conv1 run on "
                      "the bf16 matrix cores with each fp32 operand split into three bf16 "
                      "pieces (six products, fp32 accumulate: error vs fp64 at or below the "
                      "fp32 GEMM's, tests/test_gemm_split3_gpu.py)%s" % (
