@@ -249,6 +249,16 @@ int vd_conv3x3_wino4_mosaic_bias_act(const float *X, int N, int H, int W, int C,
 int vd_conv3x3_wino4_rows_bias_act(const float *X, int N, int H, int W, int C, const float *U,
                                    int Cout, const float *bias, int relu, float *Y,
                                    void *stream);
+/* The same over N maps laid out as a 2-D grid at a pitch of (H + 1) x (W + 1) -- one
+ * zero row / column shared between neighbours, g maps per grid row chosen for the
+ * fewest 16 x 32 output blocks (round 6; the mask head's 14 x 14 RoI maps: 32 per
+ * 480-column row, 87 % of each block real output against 77 % for map pairs).  Tiles
+ * straddle maps, so the result equals vd_conv3x3_wino4_bias_act's within Winograd
+ * rounding, not bitwise; each output is still its own map's zero-padded convolution.
+ * VD_ERR_SHAPE when N H W C >= 2^31 or H, W > 255. */
+int vd_conv3x3_wino4_grid_bias_act(const float *X, int N, int H, int W, int C, const float *U,
+                                   int Cout, const float *bias, int relu, float *Y,
+                                   void *stream);
 
 /* The Winograd convolution of R images of seg_h x W pixels stored back to back
  * (R x seg_h x W x C, i.e. one H = R * seg_h image), each padded by its own zeros:

@@ -54,7 +54,7 @@ def test_bench_batch_routes(bench_setup):
     """The benched shapes take the hand-written routes (not a silent fallback):
     every 3x3 conv of the benched step ran on a Winograd kernel -- res2 / res3
     / res4 / res5 conv2 (stride-1 blocks), FPN posthoc P2-P4 and the RPN conv on
-    P2-P4 on F(4x4); the mask head's four convs on F(4x4) two maps per block; P5 /
+    P2-P4 on F(4x4); the mask head's four convs on the F(4x4) map grid; P5 /
     P6 on F(2x2) mosaics."""
     from vosdetectron_amd import modeling
     cfg, sd, pipe, frames, out, routes = bench_setup
@@ -65,7 +65,7 @@ def test_bench_batch_routes(bench_setup):
     assert modeling.conv3x3_route(BATCH, 256, 256, 200, 336) == ("wino4", "rows")
     assert modeling.conv3x3_route(BATCH, 256, 256, 100, 168) == ("wino4", "rows")
     assert modeling.conv3x3_route(BATCH, 256, 256, 25, 42) == ("wino", "2d")
-    assert modeling.conv3x3_route(BATCH * 100, 256, 256, 14, 14) == ("wino4", "pair")
+    assert modeling.conv3x3_route(BATCH * 100, 256, 256, 14, 14) == ("wino4", "grid")
     assert modeling.conv3x3_route(8000, 512, 512, 7, 7) == ("wino4", "pair")  # C4 res5 head: octets
     assert routes.get("igemm", 0) == 0 and routes.get("miopen", 0) == 0, routes
     n_wino = routes.get("wino", 0) + routes.get("wino_rows", 0) + routes.get("wino_2d", 0)
@@ -73,7 +73,7 @@ def test_bench_batch_routes(bench_setup):
     # mask head's four convs as map pairs; F(2x2): posthoc P5 + RPN P5 / P6 at least
     assert routes.get("wino4", 0) + routes.get("wino4_rows", 0) >= 6 + 3 + 3 + 5 + 2, routes
     assert routes.get("wino4_rows", 0) >= 10, routes  # P3 / P4 posthoc + RPN, res3 / res4 conv2s
-    assert routes.get("wino4_pair", 0) == 4, routes
+    assert routes.get("wino4_grid", 0) == 4, routes
     assert n_wino >= 3 and routes.get("wino_2d", 0) >= 3, routes
     # the P2-P4 top-down lateral steps each as one launch with the nearest-2x add fused:
     # on the bf16 matrix cores at fp32 accuracy (split3), or with VOSDET_GEMM_SPLIT3=0

@@ -119,10 +119,11 @@ def test_winograd4_route_gate():
     for args in [(32, 256, 256, 25, 42), (32, 256, 256, 13, 21), (1000, 512, 512, 7, 7),
                  (1, 256, 256, 200, 336), (32, 256, 96, 200, 336), (100, 256, 256, 14, 14)]:
         assert r(*args)[0] != "wino4", args
-    # the mask head's RoI maps: F(4x4) two per block (>= 1024 workgroups, maps >= half
+    # the mask head's RoI maps: F(4x4) on the shared-separator grid (>= 1024 pair
+    # workgroups, maps >= half
     # a 16 x 16 cell); VOSDET_WINO4_MOSAIC=0 keeps the F(2x2) 2-D mosaic
-    assert r(3200, 256, 256, 14, 14) == ("wino4", "pair")
-    assert r(1600, 256, 256, 14, 14) == ("wino4", "pair")
+    assert r(3200, 256, 256, 14, 14) == ("wino4", "grid")
+    assert r(1600, 256, 256, 14, 14) == ("wino4", "grid")
     assert r(3200, 256, 256, 14, 14, mosaic=False)[0] != "wino4"
     # C4's res5 head: 7 x 7 maps eight per block (8 x 8 cells, 77 % real)
     assert r(8000, 512, 512, 7, 7) == ("wino4", "pair")

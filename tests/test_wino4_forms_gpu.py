@@ -152,3 +152,53 @@ def test_wino4_octet_mosaic_bit_identical(N, C, H, W, Co):
     ref = F.relu(F.conv2d(x[:64], w, b, padding=1))
     err = float((y2[:64] - ref).abs().max())
     assert err <= 5e-5 * max(1., float(ref.abs().max())), err
+
+
+@pytest.mark.parametrize("N,C,H,W,Co", [(3200, 256, 14, 14, 256), (37, 64, 9, 11, 64),
+                                        (1, 8, 14, 14, 64), (100, 24, 14, 14, 128),
+                                        (5, 64, 7, 7, 64), (33, 64, 15, 15, 64),
+                                        (50, 8, 1, 1, 64), (70, 16, 3, 40, 64)])
+def test_wino4_grid_mosaic(N, C, H, W, Co):
+    """vd_conv3x3_wino4_grid_bias_act (maps at an (H + 1) x (W + 1) pitch in a 2-D grid,
+    tiles straddling maps): every output written, each map its own zero-padded conv --
+    within the F(4x4) tolerance of torch on every map, and (maps of 4 px and more) as
+    close to an fp64 evaluation as one map per block (mean within 1.25x, max 2x)."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(N * 3 + C + H * W)
+    x = torch.randn(N, C, H, W, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    w = torch.randn(Co, C, 3, 3, device="cuda", generator=g) / (3. * C ** .5)
+    b = torch.randn(Co, device="cuda", generator=g)
+    u = ops.conv3x3_wino4_weight(w)
+    y1 = ops.conv3x3_wino4_bias_act(x, u, b, relu=True)
+    out = torch.full((N, Co, H, W), float("nan"), device="cuda").contiguous(
+        memory_format=torch.channels_last)
+    y2 = ops.conv3x3_wino4_bias_act(x, u, b, relu=True, mosaic="grid", out=out)
+    torch.cuda.synchronize()
+    assert y2 is not None and not bool(torch.isnan(y2).any())
+    sel = torch.arange(N, device="cuda") if N <= 128 else torch.cat(
+        [torch.arange(64, device="cuda"), torch.arange(N - 64, N, device="cuda")])
+    xs = x[sel]
+    ref = F.relu(F.conv2d(xs, w, b, padding=1))
+    err = float((y2[sel] - ref).abs().max())
+    assert err <= 5e-5 * max(1., float(ref.abs().max())), err
+    r64 = F.relu(F.conv2d(xs.double(), w.double(), b.double(), padding=1))
+    e1, e2 = (y1[sel].double() - r64).abs(), (y2[sel].double() - r64).abs()
+    if min(H, W) >= 4:  # (maps under 4 px put one map per block at the tile's most
+        # accurate output positions only; the grid mixes all of them)
+        assert float(e2.mean()) <= 1.25 * float(e1.mean()) + 1e-12, (float(e2.mean()),
+                                                                       float(e1.mean()))
+        assert float(e2.max()) <= 2 * float(e1.max()) + 1e-12
+    assert float(e2.max()) <= 2e-5 * max(1., float(r64.abs().max()))
+    # deterministic
+    assert torch.equal(y2, ops.conv3x3_wino4_bias_act(x, u, b, relu=True, mosaic="grid"))
+
+
+def test_wino4_mask_head_routes_to_grid(monkeypatch):
+    """The mask head's 14 x 14 RoI maps take the grid (1410 blocks per 3200 maps vs 1600
+    as pairs); VOSDET_WINO4_GRID=0 keeps pairs; octets stay octets."""
+    from vosdetectron_amd import modeling
+    assert modeling.conv3x3_route(3200, 256, 256, 14, 14) == ("wino4", "grid")
+    assert modeling.conv3x3_route(8000, 512, 512, 7, 7) == ("wino4", "pair")
+    monkeypatch.setenv("VOSDET_WINO4_GRID", "0")
+    assert modeling.conv3x3_route(3200, 256, 256, 14, 14) == ("wino4", "pair")

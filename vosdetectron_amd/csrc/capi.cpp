@@ -204,6 +204,14 @@ int vd_conv3x3_wino4_rows_bias_act(const float *X, int N, int H, int W, int C, c
     return launch_conv3x3_wino4(X, N, H, W, C, U, Cout, bias, relu, Y, VD_STREAM(stream), 2);
 }
 
+int vd_conv3x3_wino4_grid_bias_act(const float *X, int N, int H, int W, int C, const float *U,
+                                   int Cout, const float *bias, int relu, float *Y,
+                                   void *stream) {
+    if (N < 0 || H < 1 || W < 1 || C < 1 || Cout < 1 || !U || !Y || (N > 0 && !X))
+        return VD_ERR_ARG;
+    return launch_conv3x3_wino4(X, N, H, W, C, U, Cout, bias, relu, Y, VD_STREAM(stream), 4);
+}
+
 int vd_conv3x3_wino_seg_bias_act(const float *X, int H, int W, int C, const float *U, int Cout,
                                  const float *bias, int relu, int seg_h, float *Y, void *stream) {
     if (H < 1 || W < 1 || C < 1 || Cout < 1 || seg_h < 2 || !U || !Y || !X) return VD_ERR_ARG;

@@ -178,10 +178,17 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     // pitch, the rows past a map zero), one image of N hp rows
     // mos == 3: octets -- maps of at most 7 x 7, eight per block in 8 x 8 cells (2 rows
     // of 4), map n + 4 (y >> 3) + (x >> 3)
-    const bool pair = mos == 1, oct = mos == 3;
-    const int hp = mos >> 2;
-    if (sp >= (pair ? (N + 1) >> 1 : oct ? (N + 7) >> 3 : (hp ? tby * tbx : N * tby * tbx))) return;
-    const int n = pair ? 2 * sp : oct ? 8 * sp : (hp ? 0 : sp / (tby * tbx));
+    // (mos & 3) == 2: grid (vd_conv3x3_wino4_grid_bias_act, round 6) -- the maps at a
+    // pitch of (H + 1) x (W + 1) in rows of gG = mos >> 2 (map gG gy + gx at row gy,
+    // column gx), one zero row / column between neighbours: tiles straddle maps, taps
+    // in a separator or past the last map read zero and separator outputs are not
+    // stored, so every output is its map's own padded convolution (in other tile
+    // positions than one map per block: equal within Winograd rounding, not bitwise)
+    const bool pair = mos == 1, oct = mos == 3, grid = (mos & 3) == 2;
+    const int hp = (mos & 3) == 0 ? mos >> 2 : 0;
+    const int gG = grid ? mos >> 2 : 0, gPh = H + 1, gPw = W + 1;
+    if (sp >= (pair ? (N + 1) >> 1 : oct ? (N + 7) >> 3 : ((hp || grid) ? tby * tbx : N * tby * tbx))) return;
+    const int n = pair ? 2 * sp : oct ? 8 * sp : ((hp || grid) ? 0 : sp / (tby * tbx));
     const int rem = (pair || oct) ? 0 : sp - n * tby * tbx;
     const int tyb = rem / tbx, txb = rem - (rem / tbx) * tbx;
     const int oy0 = 4 * k4TR * tyb, ox0 = 4 * k4TC * txb;
@@ -213,15 +220,17 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
         const int m = u / 5, r5 = u - 5 * m;
         const int Cc = 2 * m + (r5 >> 1), hf = r5 & 1;
         const int y = iy0 + R, x = ix0 + Cc;
+        // grid: map column gx = x / (W + 1), map row gy = y / (H + 1)
+        const int gx = (grid && x >= 0) ? x / gPw : 0, gy = (grid && y >= 0) ? y / gPh : 0;
         // mosaic: cell x >> 4 (map n + cell), column x & 15 of that map
-        const int cell = pair ? (x >> 4) : oct ? (x >> 3) : 0;
-        const int xm = pair ? (x & 15) : oct ? (x & 7) : x;
+        const int cell = pair ? (x >> 4) : oct ? (x >> 3) : grid ? gx : 0;
+        const int xm = pair ? (x & 15) : oct ? (x & 7) : grid ? x - gx * gPw : x;
         // row stack: map y / hp, its row y % hp (octets: map row 4 (y >> 3), row y & 7)
-        const int mr = (hp && y >= 0) ? y / hp : (oct && y >= 0) ? 4 * (y >> 3) : 0;
-        const int ly = hp ? y - mr * hp : oct ? (y & 7) : y;
+        const int mr = (hp && y >= 0) ? y / hp : (oct && y >= 0) ? 4 * (y >> 3) : grid ? gG * gy : 0;
+        const int ly = hp ? y - mr * hp : oct ? (y & 7) : grid ? y - gy * gPh : y;
         const bool ok = R < k4PR && r5 < 4 && Cc < k4PC && (unsigned)ly < (unsigned)H &&
                         y >= 0 && x >= 0 && (unsigned)xm < (unsigned)W && n + cell + mr < N &&
-                        (!oct || (cell < 4 && mr < 8));
+                        (!oct || (cell < 4 && mr < 8)) && (!grid || gx < gG);
         poff[kPS * k] = ok ? (uint32_t)((((cell + mr) * H + ly) * W + xm) * C + 4 * hf)
                            : 0x80000000u | (uint32_t)(4 * hf);
         srcp[k] = ok ? Xn + (((cell + mr) * H + ly) * W + xm) * C + 4 * hf : zero + 4 * hf;
@@ -524,15 +533,17 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int yv = oy0 + 4 * tr + i;
-        const int mr = hp ? yv / hp : oct ? 4 * (yv >> 3) : 0;
-        const int yy = hp ? yv - mr * hp : oct ? (yv & 7) : yv;
+        const int gy = grid ? yv / gPh : 0;
+        const int mr = hp ? yv / hp : oct ? 4 * (yv >> 3) : grid ? gG * gy : 0;
+        const int yy = hp ? yv - mr * hp : oct ? (yv & 7) : grid ? yv - gy * gPh : yv;
         if (yy >= H || n + mr >= N) continue;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int xc = ox0 + 4 * tc + k;
-            const int ncell = pair ? n + (xc >> 4) : oct ? n + mr + (xc >> 3) : n + mr;
-            const int xx = pair ? (xc & 15) : oct ? (xc & 7) : xc;
-            if (xx >= W || ncell >= N) continue;
+            const int gx = grid ? xc / gPw : 0;
+            const int ncell = pair ? n + (xc >> 4) : oct ? n + mr + (xc >> 3) : n + mr + gx;
+            const int xx = pair ? (xc & 15) : oct ? (xc & 7) : grid ? xc - gx * gPw : xc;
+            if (xx >= W || ncell >= N || (grid && gx >= gG)) continue;
             float4 v = make_float4(o[4 * i + k][0] + bv.x, o[4 * i + k][1] + bv.y,
                                    o[4 * i + k][2] + bv.z, o[4 * i + k][3] + bv.w);
             if (RELU) {
@@ -919,9 +930,26 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
             return VD_ERR_SHAPE;
         mos = hp << 2;
     }
+    // the grid: maps at a (H + 1) x (W + 1) pitch, g per mosaic row, g chosen for the
+    // fewest 16 x 32 blocks (14 x 14: 32 maps = 480 columns = 15 blocks exactly)
+    int gG = 0;
+    if (mos == 4) {
+        if ((int64_t)N * H * W * C >= ((int64_t)1 << 31) || H > 255 || W > 255) return VD_ERR_SHAPE;
+        int64_t best = -1;
+        for (int g = 1; g <= 64 && g <= N; ++g) {
+            const int64_t rows = (int64_t)(N + g - 1) / g * (H + 1);
+            const int64_t b = (rows + 4 * k4TR - 1) / (4 * k4TR) *
+                              (((int64_t)g * (W + 1) + 4 * k4TC - 1) / (4 * k4TC));
+            if (best < 0 || b < best) best = b, gG = g;
+        }
+        if ((int64_t)(N + gG - 1) / gG * (H + 1) >= ((int64_t)1 << 30)) return VD_ERR_SHAPE;
+    }
     const bool cells = mos == 1 || mos == 3;
-    const int tby = cells ? 1 : ((mos ? N * hp : H) + 4 * k4TR - 1) / (4 * k4TR);
-    const int tbx = cells ? 1 : (W + 4 * k4TC - 1) / (4 * k4TC);
+    const int tby = cells ? 1
+                    : gG ? (int)(((int64_t)(N + gG - 1) / gG * (H + 1) + 4 * k4TR - 1) / (4 * k4TR))
+                         : ((mos ? N * hp : H) + 4 * k4TR - 1) / (4 * k4TR);
+    const int tbx = cells ? 1 : ((gG ? gG * (W + 1) : W) + 4 * k4TC - 1) / (4 * k4TC);
+    if (gG) mos = (gG << 2) | 2;
     const int64_t nsp = mos == 1 ? ((int64_t)N + 1) / 2
                                  : mos == 3 ? ((int64_t)N + 7) / 8
                                             : (int64_t)(mos ? 1 : N) * tby * tbx;

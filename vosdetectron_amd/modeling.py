@@ -183,6 +183,24 @@ def _wino4_pair_ok(N: int, Cin: int, Cout: int, H: int, W: int) -> bool:
     return -(-N // per) * (Cout // 64) >= _WINO4_MIN_WGS
 
 
+def _wino4_grid_blocks(N: int, H: int, W: int) -> int:
+    """16 x 32 output blocks of the F(4x4) grid layout (launch_conv3x3_wino4, mos 4):
+    maps at an (H + 1) x (W + 1) pitch, g per grid row for the fewest blocks."""
+    return min(-(-(-(-N // g) * (H + 1)) // 16) * -(-(g * (W + 1)) // 32)
+               for g in range(1, min(64, N) + 1))
+
+
+def _wino4_grid_better(N: int, Cin: int, H: int, W: int) -> bool:
+    """The map-pair / octet mosaic's maps as a shared-separator grid instead, where
+    that needs fewer blocks (14 x 14 RoI maps: 1410 vs 1600 blocks per 3200 maps).
+    VOSDET_WINO4_GRID=0 keeps pairs / octets."""
+    if (os.environ.get("VOSDET_WINO4_GRID", "1") == "0" or N * H * W * Cin >= (1 << 31)
+            or H > 255 or W > 255):
+        return False
+    cells = -(-N // 8) if (H <= 7 and W <= 7) else -(-N // 2)
+    return _wino4_grid_blocks(N, H, W) < cells
+
+
 def conv3x3_route(N: int, Cin: int, Cout: int, H: int, W: int, mosaic=True):
     """(algorithm, mosaic) the engine runs a 3x3 / stride-1 / pad-1 fp32 conv of an
     N x Cin x H x W channels_last batch with: ('wino4', None) -- Winograd F(4x4,3x3),
@@ -199,7 +217,7 @@ def conv3x3_route(N: int, Cin: int, Cout: int, H: int, W: int, mosaic=True):
     if w4 is not None:
         return "wino4", (w4 or None)
     if wino and mosaic and _wino4_pair_ok(N, Cin, Cout, H, W):
-        return "wino4", "pair"
+        return "wino4", ("grid" if _wino4_grid_better(N, Cin, H, W) else "pair")
     if wino and npx >= _WINO_MIN_PIXELS and use >= _WINO_MIN_BLOCK_USE:
         return "wino", mos
     if npx < _CONV3X3_MIN_PIXELS:
@@ -248,7 +266,8 @@ def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=True):
             conv._vd_u4_key = key
         y = ops.conv3x3_wino4_bias_act(x, conv._vd_u4, b, relu=relu, mosaic=mos or False)
         if y is not None:
-            _count_route({"pair": "wino4_pair", "rows": "wino4_rows"}.get(mos, "wino4"))
+            _count_route({"pair": "wino4_pair", "rows": "wino4_rows",
+                          "grid": "wino4_grid"}.get(mos, "wino4"))
             return y
         algo, mos = "wino", _pick_mosaic(x.shape[0], x.shape[2], x.shape[3], mosaic)[0]
     if algo == "wino":

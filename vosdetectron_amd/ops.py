@@ -834,8 +834,9 @@ def conv3x3_wino4_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torc
     F(4x4,3x3) (vd_conv3x3_wino4_bias_act); u from conv3x3_wino4_weight.  mosaic
     True / "pair": maps of at most 15 x 15 two per output block
     (vd_conv3x3_wino4_mosaic_bias_act); "rows": the maps stacked in one column at a
-    4-row pitch (vd_conv3x3_wino4_rows_bias_act); both bit-identical.  None for a
-    shape the kernel does not serve."""
+    4-row pitch (vd_conv3x3_wino4_rows_bias_act); both bit-identical.  "grid": the
+    maps as a 2-D grid at an (H + 1) x (W + 1) pitch (vd_conv3x3_wino4_grid_bias_act;
+    equal within Winograd rounding).  None for a shape the kernel does not serve."""
     if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 4 \
             or not x.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("x must be a channels_last fp32 device tensor")
@@ -852,7 +853,8 @@ def conv3x3_wino4_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torc
                           memory_format=torch.channels_last)
     fn = {False: lib().vd_conv3x3_wino4_bias_act, True: lib().vd_conv3x3_wino4_mosaic_bias_act,
           "pair": lib().vd_conv3x3_wino4_mosaic_bias_act,
-          "rows": lib().vd_conv3x3_wino4_rows_bias_act}[mosaic]
+          "rows": lib().vd_conv3x3_wino4_rows_bias_act,
+          "grid": lib().vd_conv3x3_wino4_grid_bias_act}[mosaic]
     st = fn(x.data_ptr(), N, H, W, C, u_.data_ptr(), Cout,
             b_.data_ptr() if b_ is not None else None, int(relu), out.data_ptr(), _stream())
     if st == VD_ERR_SHAPE:
