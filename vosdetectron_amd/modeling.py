@@ -708,8 +708,13 @@ class FPNBody(nn.Module):
         if self.use_gn:
             inner = [self._gn_seq(self.conv_top, c[-1])]
         elif self.epilogue and c[-1].is_cuda and _gemm_ok(c[-1]):
-            w = self.conv_top.weight.reshape(self.conv_top.out_channels, -1)
-            inner = [_gemm_conv1x1(c[-1], w, self.conv_top.bias, relu=False)]
+            # one persistent 2-D view of the weight (the split-bf16 image is cached per
+            # tensor object; a fresh view per call would re-split it every step)
+            cw = self.conv_top.weight
+            if getattr(self, "_vd_top_src", None) is not cw:
+                self._vd_top_w2d = cw.reshape(self.conv_top.out_channels, -1)
+                self._vd_top_src = cw
+            inner = [_gemm_conv1x1(c[-1], self._vd_top_w2d, self.conv_top.bias, relu=False)]
         else:
             inner = [self.conv_top(c[-1])]
         for i in range(3):

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import weakref
 from typing import Optional, Sequence
 
@@ -561,6 +562,11 @@ def split3_weight_cached(w: torch.Tensor) -> Optional[torch.Tensor]:
         if _split3_cache.get(i, (None,))[0] is r:
             del _split3_cache[i]
     ref = weakref.ref(w, _drop)
+    if os.environ.get("VOSDET_SPLIT3_TRACE") == "1":  # research: report every (re)split
+        import traceback
+        sys.stderr.write("split3 weight %s (cache %s)\n%s" % (
+            tuple(w.shape), "stale" if ent is not None else "miss",
+            "".join(traceback.format_stack(limit=6)[:-1])))
     wp = gemm_split3_weight(w)
     _split3_cache[i] = (ref, key, wp)
     return wp
