@@ -1,6 +1,7 @@
 """Winograd F(4x4,3x3), position-split form (csrc/conv3x3_wino4.hip,
 VOSDET_WINO4_PS=1) and the hand-counted-vmcnt form (VOSDET_WINO4_ACC=1) vs the first
-form: the same MFMA operands in the same order and
+form -- and the default form's packed-fp32 input transform (VOSDET_WINO4_PK) against
+its scalar one: the same MFMA operands in the same order and
 the same output transform, so the outputs must be bit-identical -- on the step's
 shapes (incl. ragged blocks: H, W not multiples of 16 / 32), with and without bias
 and ReLU -- and within 5e-5 of torch fp32 (the F(4x4) tolerance)."""
@@ -19,7 +20,11 @@ FORMS = {"first": {"VOSDET_WINO4_PS": "0", "VOSDET_WINO4_ACC": "0", "VOSDET_WINO
          "acc": {"VOSDET_WINO4_PS": "0", "VOSDET_WINO4_ACC": "1", "VOSDET_WINO4_VD": "1"},
          "acc3": {"VOSDET_WINO4_PS": "0", "VOSDET_WINO4_ACC": "1", "VOSDET_WINO4_VD": "3"},
          "il": {"VOSDET_WINO4_PS": "0", "VOSDET_WINO4_ACC": "1", "VOSDET_WINO4_VD": "1",
-                "VOSDET_WINO4_IL": "1"}}
+                "VOSDET_WINO4_IL": "1"},
+         # the default ACC form with the scalar input transform (the packed-fp32 one,
+         # VOSDET_WINO4_PK=1, is the default and is what "acc" runs)
+         "acc_scalar": {"VOSDET_WINO4_PS": "0", "VOSDET_WINO4_ACC": "1", "VOSDET_WINO4_VD": "1",
+                        "VOSDET_WINO4_PK": "0"}}
 
 
 def _run(x, u, b, relu, form):
@@ -43,7 +48,7 @@ def _run(x, u, b, relu, form):
                                         (3, 128, 17, 45, 128), (2, 512, 25, 42, 512),
                                         (1, 8, 9, 9, 64), (4, 24, 33, 31, 128)])
 @pytest.mark.parametrize("bias", [True, False])
-@pytest.mark.parametrize("form", ["ps", "acc", "acc3", "il"])
+@pytest.mark.parametrize("form", ["ps", "acc", "acc3", "il", "acc_scalar"])
 def test_wino4_forms_bit_identical_to_first_form(N, C, H, W, Co, bias, form):
     from vosdetectron_amd import ops
     g = torch.Generator(device="cuda").manual_seed(N * 1000 + C + H)
@@ -62,7 +67,7 @@ def test_wino4_forms_bit_identical_to_first_form(N, C, H, W, Co, bias, form):
     assert err <= 5e-5 * max(1., float(ref.abs().max())), err
 
 
-@pytest.mark.parametrize("form", ["ps", "acc", "acc3", "il"])
+@pytest.mark.parametrize("form", ["ps", "acc", "acc3", "il", "acc_scalar"])
 def test_wino4_forms_benched_p2(form):
     from vosdetectron_amd import ops
     g = torch.Generator(device="cuda").manual_seed(7)

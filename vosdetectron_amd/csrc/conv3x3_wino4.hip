@@ -120,6 +120,22 @@ __device__ __forceinline__ void w4_bt6(const float (&x)[6], float (&y)[6]) {
     y[5] = __builtin_fmaf(4.f, x[1], __builtin_fmaf(-5.f, x[3], x[5]));
 }
 
+// w4_bt6 on two independent vectors at once (packed fp32: v_pk_fma_f32 / v_pk_add_f32,
+// two lanes' worth of the same IEEE operations, so bit-identical to two w4_bt6 calls)
+__device__ __forceinline__ f2v w4_pfma(float a, f2v b, f2v c) {
+    return __builtin_elementwise_fma(f2v{a, a}, b, c);
+}
+__device__ __forceinline__ void w4_bt6v(const f2v (&x)[6], f2v (&y)[6]) {
+    const f2v t0 = w4_pfma(-4.f, x[2], x[4]), t1 = w4_pfma(-4.f, x[1], x[3]);
+    const f2v t2 = x[4] - x[2], d = x[3] - x[1];
+    y[0] = w4_pfma(4.f, x[0], w4_pfma(-5.f, x[2], x[4]));
+    y[1] = t0 + t1;
+    y[2] = t0 - t1;
+    y[3] = w4_pfma(2.f, d, t2);
+    y[4] = w4_pfma(-2.f, d, t2);
+    y[5] = w4_pfma(4.f, x[1], w4_pfma(-5.f, x[3], x[5]));
+}
+
 // y = A^T m, A^T = [1 1 1 1 1 0; 0 1 -1 2 -2 0; 0 1 1 4 4 0; 0 1 -1 8 -8 1]
 __device__ __forceinline__ void w4_at6(const float (&m)[6], float (&y)[4]) {
     const float s12 = m[1] + m[2], d12 = m[1] - m[2], s34 = m[3] + m[4], d34 = m[3] - m[4];
@@ -145,7 +161,10 @@ __device__ unsigned long long g_wino4_stamps[kStampWg * 8 * kStampNch * 6];
 // reads issued one position ahead), row a of (B^T d) B and its V writes after position
 // 6 + a -- instead of one block before them (the chunk stamps: 3.6 k cycles of
 // transform, during which the SIMD's MFMA pipe is fed by the partner wave alone)
-template <bool RELU, int PROBE, bool ACC = false, int VD = 1, bool STAMP = false, bool IL = false>
+// PK (round 6, the default; VOSDET_WINO4_PK=0 keeps the scalar transform): the input
+// transform in packed fp32, bit-identical
+template <bool RELU, int PROBE, bool ACC = false, int VD = 1, bool STAMP = false, bool IL = false,
+          bool PK = false>
 __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
@@ -273,6 +292,35 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
             : vst + 64 * wave + lane;
     auto transform = [&](int stage) {
         const float *tp = tread + stage * (k4PStageB / 4);
+        float *vp = twrite + stage * (k4VStageB / 4);
+        if (PK) {  // packed fp32: columns (c, c + 1), then rows (a, a + 1), in pairs
+            f2v t[6][3];  // B^T d: t[a][c / 2] = {row a col c, row a col c + 1}
+#pragma unroll
+            for (int c = 0; c < 6; c += 2) {
+                f2v x[6], y[6];
+#pragma unroll
+                for (int r = 0; r < 6; ++r)
+                    x[r] = f2v{tp[(r * k4RP + 2 * c + (c >> 1)) * 4],
+                               tp[(r * k4RP + 2 * (c + 1) + ((c + 1) >> 1)) * 4]};
+                w4_bt6v(x, y);
+#pragma unroll
+                for (int a = 0; a < 6; ++a) t[a][c >> 1] = y[a];
+            }
+#pragma unroll
+            for (int a = 0; a < 6; a += 2) {
+                f2v x[6], y[6];
+#pragma unroll
+                for (int c = 0; c < 6; ++c)
+                    x[c] = f2v{t[a][c >> 1][c & 1], t[a + 1][c >> 1][c & 1]};
+                w4_bt6v(x, y);
+#pragma unroll
+                for (int b = 0; b < 6; ++b) {
+                    vp[(6 * a + b) * 256] = y[b][0];
+                    vp[(6 * (a + 1) + b) * 256] = y[b][1];
+                }
+            }
+            return;
+        }
         float t[6][6];  // B^T d: column c's 6 values
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
@@ -283,7 +331,6 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
 #pragma unroll
             for (int a = 0; a < 6; ++a) t[a][c] = y[a];
         }
-        float *vp = twrite + stage * (k4VStageB / 4);
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             float y[6];
@@ -1020,7 +1067,12 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
     // VOSDET_WINO4_VD (ACC form): V fragments read 1-3 positions ahead
     const char *vde = getenv("VOSDET_WINO4_VD");
     const int vd = vde ? atoi(vde) : 1;
+    const char *pke = getenv("VOSDET_WINO4_PK");
+    const bool pk = !(pke && pke[0] == '0');
     kern_t kacc = relu ? conv3x3_wino4_kernel<true, 0, true, 1> : conv3x3_wino4_kernel<false, 0, true, 1>;
+    if (pk)
+        kacc = relu ? conv3x3_wino4_kernel<true, 0, true, 1, false, false, true>
+                    : conv3x3_wino4_kernel<false, 0, true, 1, false, false, true>;
     if (vd == 2)
         kacc = relu ? conv3x3_wino4_kernel<true, 0, true, 2> : conv3x3_wino4_kernel<false, 0, true, 2>;
     if (vd == 3)
