@@ -955,8 +955,11 @@ def dry_run(args, world, rank):
 # 3.0 % more frames/s than 16 on one box (344.0 -> 354.3, profiles/r04/batch32/) --
 # the step's latency-bound tail (proposal select, class NMS) and the small
 # kernels are amortised over twice the frames; per-step latency doubles (~90 ms).
-# The VOS and C4 engines stay at 16.  --batch overrides.
-DEFAULT_FRAMES = 32
+# The VOS and C4 engines stay at 16.  --batch overrides.  Round 6: 64 frames, +2.2 %
+# over 32 on one box (456.7-457.6 -> 466.6-468.0 frames/s, 48: 462.1-462.6,
+# profiles/r06/batch64/): the tail and the small P5 / P6 / res5 kernels amortised
+# again, per-step latency ~137 ms.
+DEFAULT_FRAMES = 64
 
 
 def default_frames(cfg) -> int:
@@ -1005,7 +1008,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=None,
-                    help="frames per GPU per step (default: DEFAULT_FRAMES = 32 for the FPN "
+                    help="frames per GPU per step (default: DEFAULT_FRAMES = 64 for the FPN "
                          "engines, 16 for VOS / C4)")
     ap.add_argument("--config", default="e2e_mask_rcnn_R-50-FPN_1x")
     ap.add_argument("--layout", default="nhwc", choices=["nchw", "nhwc"])

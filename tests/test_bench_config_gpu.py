@@ -1,7 +1,7 @@
 """The configuration bench.py measures, tested as benched (VERDICT r2 item 2,
 VERDICT r3 weak #2).
 
-bench.py runs e2e_mask_rcnn_R-50-FPN_1x at BATCH = bench.DEFAULT_FRAMES (32)
+bench.py runs e2e_mask_rcnn_R-50-FPN_1x at BATCH = bench.DEFAULT_FRAMES (64)
 synthetic 800x1333 frames per step on the channels_last engine.  At that batch the 3x3 convolutions route to
 the hand-written Winograd MFMA kernels (modeling.conv3x3_route): F(4x4,3x3)
 (csrc/conv3x3_wino4.hip) for P2 / P3 / P4 and res2-res5 conv2 (>= 1024 workgroups,
@@ -64,17 +64,21 @@ def test_bench_batch_routes(bench_setup):
     assert all(int(c) > 0 for c in out["counts_host"])
     assert modeling.conv3x3_route(BATCH, 256, 256, 200, 336) == ("wino4", "rows")
     assert modeling.conv3x3_route(BATCH, 256, 256, 100, 168) == ("wino4", "rows")
-    assert modeling.conv3x3_route(BATCH, 256, 256, 25, 42) == ("wino", "2d")
+    # P5: F(2x2) 2-D mosaic at 32 frames, the F(4x4) row stack from 64 (>= 1024 workgroups)
+    assert modeling.conv3x3_route(BATCH, 256, 256, 25, 42) == (
+        ("wino4", "rows") if BATCH >= 64 else ("wino", "2d"))
     assert modeling.conv3x3_route(BATCH * 100, 256, 256, 14, 14) == ("wino4", "grid")
     assert modeling.conv3x3_route(8000, 512, 512, 7, 7) == ("wino4", "pair")  # C4 res5 head: octets
     assert routes.get("igemm", 0) == 0 and routes.get("miopen", 0) == 0, routes
     n_wino = routes.get("wino", 0) + routes.get("wino_rows", 0) + routes.get("wino_2d", 0)
     # F(4x4): FPN posthoc + RPN conv on P2-P4 (6) and the body's stride-1 conv2s, the
-    # mask head's four convs as map pairs; F(2x2): posthoc P5 + RPN P5 / P6 at least
+    # mask head's four convs on the map grid
     assert routes.get("wino4", 0) + routes.get("wino4_rows", 0) >= 6 + 3 + 3 + 5 + 2, routes
     assert routes.get("wino4_rows", 0) >= 10, routes  # P3 / P4 posthoc + RPN, res3 / res4 conv2s
     assert routes.get("wino4_grid", 0) == 4, routes
-    assert n_wino >= 3 and routes.get("wino_2d", 0) >= 3, routes
+    # F(2x2) 2-D mosaics: posthoc P5 + RPN P5 / P6 at 32 frames; the RPN's P6 at 64
+    n2d = 1 if BATCH >= 64 else 3
+    assert n_wino >= n2d and routes.get("wino_2d", 0) >= n2d, routes
     # the P2-P4 top-down lateral steps each as one launch with the nearest-2x add fused:
     # on the bf16 matrix cores at fp32 accuracy (split3), or with VOSDET_GEMM_SPLIT3=0
     # P2 on the fp32 MFMA kernel (modeling._fpn_lateral_fused_k)
@@ -126,7 +130,10 @@ def test_conv3x3_wino_benched_shapes(N, C, H, W, bias):
         got = ops.conv3x3_wino_bias_act(x, ops.conv3x3_wino_weight(w), b, relu=bias,
                                         mosaic=mos)
     assert got is not None, "benched shape fell off the Winograd route"
-    ref = F.conv2d(x, w, b, padding=1)
+    # the torch reference in chunks of at most 16 maps x 200 x 336 (a 4.4 GB
+    # 64-frame P2 batch in one MIOpen call came out wrong on the box, round 6)
+    step = max(1, (16 * 200 * 336) // (H * W))
+    ref = torch.cat([F.conv2d(x[i:i + step], w, b, padding=1) for i in range(0, N, step)])
     if bias:
         ref = F.relu(ref)
     torch.cuda.synchronize()
