@@ -369,7 +369,7 @@ MFMA_FP32_PEAK_TFS = 157.3  # MI355X dense fp32 matrix peak
 def measure_dominant_conv(dev, F, H, W, C=256, iters=None):
     """The step's dominant kernel by time: the P2 3x3 256 -> 256 convolution (FPN
     posthoc and RPN conv) on the kernel the engine routes it to
-    (modeling.conv3x3_route: Winograd F(4x4,3x3) at the benched 32 frames, F(2x2)
+    (modeling.conv3x3_route: Winograd F(4x4,3x3) at the benched 64 frames, F(2x2)
     below its workgroup gate), timed alone at the benched shape with HIP events on
     its stream.  Algorithmic FLOPs are the direct convolution's 2*9*C*Cout per
     output pixel (what the reference computes; Winograd takes the rate past the
@@ -427,7 +427,7 @@ MFMA_BF16_PEAK_TFS = 2516.6  # dense bf16 matrix peak: 256 CUs x 4 SIMDs x 1024 
 
 
 def measure_split_gemm(dev, M=32000, N=1024, K=12544, iters=10):
-    """The largest split-bf16 GEMM of the step, fc6 of the 32-frame box head (32,000 RoIs
+    """The largest split-bf16 GEMM of the step, fc6 of the box head (F x 1000 RoIs
     x 12,544 -> 1,024, ReLU), timed alone with HIP events on its stream: fp32 work per
     second, and the bf16 matrix-core work it executes (six bf16 products per fp32 MAC)
     as a fraction of the dense bf16 peak."""
@@ -689,9 +689,9 @@ def measure_step_post(pipe, frames_dev, reps=20):
                 "avg_us": round(t_d * 1e6, 1), "frames": F, "rois_per_frame": post,
                 "us_per_frame": round(t_d * 1e6 / F, 2)},
             "how": "HIP events over %d launches on the engine's own step tensors" % reps,
-            "rocprof": "profiles/r06/head_d/trace/post_launches.txt (32 frames): rpn_proposals "
-                       "51.7 (+ 6 rpn_sel_hist, rpn_sel_compact) + rpn_nms_mask 123.8 + "
-                       "rpn_nms_finish 33.9 us; class_nms 447.2 + det_limit 42.7 us per launch "
+            "rocprof": "profiles/r06/head_f/trace/post_launches.txt (64 frames): rpn_proposals "
+                       "85.2 (+ 6 rpn_sel_hist, rpn_sel_compact) + rpn_nms_mask 243.3 + "
+                       "rpn_nms_finish 64.5 us; class_nms 825.4 + det_limit 41.9 us per launch "
                        "(rocprofv3 --kernel-trace, 36 calls)"}
 
 
