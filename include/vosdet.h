@@ -182,14 +182,18 @@ int vd_gemm_bias_act(const float *A, int M, int K, const float *W, int N, const 
  * the downsample shortcut) without the subsampled copy.  cfg 0 picks the tile shape
  * (1: 256 pixels x 256 channels, 2: 256 x 128, 3: 256 x 64, 4: 128 x 128, 5: 256 x 256 in
  * eight waves per workgroup;
- * VD_ERR_SHAPE when N does not divide by the tile's channels).  Replaces the same
+ * VD_ERR_SHAPE when N does not divide by the tile's channels).  a_bias (K - K2 floats,
+ * or NULL): A's channels enter as relu(A + a_bias[k]) -- the bias + ReLU of the layer
+ * that produced A, applied in fp32 before the split (bit-identical to a separate
+ * pass; ResNeXt's grouped conv2 runs on MIOpen without them).  Replaces the same
  * fp32 convolutions / Linear layers as vd_gemm_bias_act (ResNet.py:246-294
  * bottleneck 1x1s, fast_rcnn_heads.py fc6 / fc7, mask_rcnn_heads.py upconv5). */
 size_t vd_gemm_split3_weight_size(int N, int K);
 int vd_gemm_split3_weight(const float *W, int N, int K, void *Wp, void *stream);
-int vd_gemm_split3_bias_act(const float *A, int M, int K, const float *A2, int K2, const void *Wp,
-                            int N, const float *bias, const float *residual, int up_h, int up_w,
-                            int sub_h, int sub_w, int relu, float *D, int cfg, void *stream);
+int vd_gemm_split3_bias_act(const float *A, int M, int K, const float *A2, int K2,
+                            const float *a_bias, const void *Wp, int N, const float *bias,
+                            const float *residual, int up_h, int up_w, int sub_h, int sub_w,
+                            int relu, float *D, int cfg, void *stream);
 
 /* The mask head's tail in one split-bf16 GEMM launch: the 2x2 / 2 transposed conv
  * upconv5 + ReLU (mask_rcnn_heads.py:62-68) and the class-selected 1x1 mask logits +

@@ -257,3 +257,72 @@ def test_split3_weight_image_is_the_rne_split():
         ref = piece.to(torch.bfloat16).view(torch.int16)           # [N][K]
         ref = ref.view(N // 32, 32, K // 16, 2, 8).permute(2, 0, 3, 1, 4)  # [s][t][h][r][j]
         assert torch.equal(img[:, :, p], ref), p
+
+
+@pytest.mark.parametrize("M,K,N,cfg", [(5000, 256, 256, 0), (1237, 512, 1024, 0),
+                                       (4099, 1024, 256, 2), (999, 256, 128, 3),
+                                       (3000, 512, 512, 4), (2048, 2048, 512, 5)])
+def test_split3_a_bias_prologue_bit_identical(M, K, N, cfg):
+    """a_bias: A enters as relu(A + a_bias) -- bit-identical to applying the bias + ReLU
+    in a separate fp32 pass and splitting that (ResNeXt's grouped conv2 epilogue fused
+    into conv3's A load), with and without a residual; with a second operand the bias
+    touches A's channels only; with a stride-2 A as well."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    a = torch.randn(M, K, device=DEV, generator=g)  # raw conv output: both signs
+    ab = torch.randn(K, device=DEV, generator=g) * .5
+    w = torch.randn(N, K, device=DEV, generator=g) / K ** .5
+    b = torch.randn(N, device=DEV, generator=g) * .1
+    r = torch.randn(M, N, device=DEV, generator=g)
+    wp = ops.gemm_split3_weight(w)
+    pre = torch.relu(a + ab)
+    for res in (None, r):
+        got = ops.gemm_split3_bias_act(a, wp, b, residual=res, cfg=cfg, a_bias=ab)
+        want = ops.gemm_split3_bias_act(pre, wp, b, residual=res, cfg=cfg)
+        torch.cuda.synchronize()
+        assert torch.equal(got, want), float((got - want).abs().max())
+    # the ops.gemm_bias_act route passes it through
+    assert torch.equal(ops.gemm_bias_act(a, w, b, relu=True, a_bias=ab),
+                       ops.gemm_bias_act(pre, w, b, relu=True))
+    # two operands: the bias covers A's K1 channels, not A2's
+    K1 = K // 2
+    got = ops.gemm_split3_bias_act(a[:, :K1].contiguous(), wp, b,
+                                   a2=a[:, K1:].contiguous(), a_bias=ab[:K1].contiguous())
+    want = ops.gemm_split3_bias_act(pre[:, :K1].contiguous(), wp, b,
+                                    a2=a[:, K1:].contiguous())
+    assert torch.equal(got, want)
+    with pytest.raises(ValueError):
+        ops.gemm_split3_bias_act(a, wp, b, a_bias=ab[:K1].contiguous())
+
+
+def test_split3_a_bias_stride2():
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(5)
+    n, C, H, W, N = 3, 256, 21, 34, 512
+    x = torch.randn(n, H, W, C, device=DEV, generator=g)
+    ab = torch.randn(C, device=DEV, generator=g)
+    w = torch.randn(N, C, device=DEV, generator=g) / C ** .5
+    b = torch.randn(N, device=DEV, generator=g)
+    wp = ops.gemm_split3_weight(w)
+    got = ops.gemm_split3_bias_act(x.reshape(-1, C), wp, b, sub_hw=(H, W), a_bias=ab)
+    want = ops.gemm_split3_bias_act(torch.relu(x + ab).reshape(-1, C), wp, b, sub_hw=(H, W))
+    assert torch.equal(got, want)
+
+
+def test_resnext_block_conv2_prologue_bit_identical(monkeypatch):
+    """X-101-32x8d's body (grouped conv2 on MIOpen): conv2's bias + ReLU applied by
+    conv3's split GEMM (the default) == the separate bias / ReLU pass
+    (VOSDET_CONV2_PROLOGUE=0), bit for bit, on the res2-res5 stages."""
+    from vosdetectron_amd import config as vcfg
+    from vosdetectron_amd.weights import build_model
+    cfg = vcfg.get("e2e_mask_rcnn_X-101-32x8d-FPN_1x")
+    model, _ = build_model(cfg, seed=0, device=DEV, channels_last=True)
+    x = (torch.rand((2, 3, 256, 320)) * 255 - 120).to(DEV).contiguous(
+        memory_format=torch.channels_last)
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("VOSDET_CONV2_PROLOGUE", flag)
+        with torch.no_grad():
+            outs[flag] = [t.clone() for t in model.Conv_Body(x)]
+    for p, q in zip(outs["1"], outs["0"]):
+        assert torch.equal(p, q), float((p - q).abs().max())

@@ -63,8 +63,8 @@ SIGNATURES = {
     "vd_gemm_split3_weight_size": (_S, [_I, _I]),
     "vd_mask_head_upconv_logits": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _I, _P, _P]),
     "vd_gemm_split3_weight": (_I, [_P, _I, _I, _P, _P]),
-    "vd_gemm_split3_bias_act": (_I, [_P, _I, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I,
-                                     _P, _I, _P]),
+    "vd_gemm_split3_bias_act": (_I, [_P, _I, _I, _P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _I,
+                                    _I, _P, _I, _P]),
     "vd_fpn_lateral_weight": (_I, [_P, _I, _I, _P, _P]),
     "vd_fpn_lateral_topdown": (_I, [_P, _L, _I, _P, _I, _P, _P, _I, _I, _P, _P]),
     "vd_conv3x3_bias_act": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P]),

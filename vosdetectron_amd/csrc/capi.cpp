@@ -140,13 +140,14 @@ int vd_gemm_split3_weight(const float *W, int N, int K, void *Wp, void *stream) 
     return launch_gemm_split3_weight(W, N, K, Wp, VD_STREAM(stream));
 }
 
-int vd_gemm_split3_bias_act(const float *A, int M, int K, const float *A2, int K2, const void *Wp,
-                            int N, const float *bias, const float *residual, int up_h, int up_w,
-                            int sub_h, int sub_w, int relu, float *D, int cfg, void *stream) {
+int vd_gemm_split3_bias_act(const float *A, int M, int K, const float *A2, int K2,
+                            const float *a_bias, const void *Wp, int N, const float *bias,
+                            const float *residual, int up_h, int up_w, int sub_h, int sub_w,
+                            int relu, float *D, int cfg, void *stream) {
     if (M < 0 || K < 1 || N < 1 || !Wp || !bias || !D || (M > 0 && !A) || cfg < 0 || cfg > 19)
         return VD_ERR_ARG;
     return launch_gemm_split3(A, M, K, A2, K2, Wp, N, bias, residual, up_h, up_w, sub_h, sub_w,
-                              relu, D, cfg, VD_STREAM(stream));
+                              relu, D, cfg, VD_STREAM(stream), a_bias);
 }
 
 int vd_mask_head_upconv_logits(const float *X, int M, int K, const void *Wp, const float *bias,

@@ -119,7 +119,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_split3_kernel(
     const float *__restrict__ A, const uint4 *__restrict__ Wp, const float *__restrict__ bias,
     const float *__restrict__ R, float *__restrict__ D, int M, int N, int K, int tiles_n,
     int num_tiles, int H, int W, int SH, int SW, const float *__restrict__ cb,
-    const int32_t *__restrict__ rch, const float *__restrict__ A2, int K2) {
+    const int32_t *__restrict__ rch, const float *__restrict__ A2, int K2,
+    const float *__restrict__ abias) {
     constexpr int WM = BM / (32 * TPM), WN = BN / (32 * TPN), NTH = 64 * NW;
     static_assert(WM * WN == NW, "one (pixel, channel) block per wave");
     constexpr int PT = BM / 32, NTW = BN / 32;                 // pixel / channel tiles
@@ -171,6 +172,11 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_split3_kernel(
 
     float4 ar[AL];
     uint4 wr[WL];
+    // abias (A prologue): A's first K1 channels enter as relu(A + abias[k]) -- the
+    // bias + ReLU of the layer that produced A (a grouped 3x3 conv MIOpen runs without
+    // them), applied in fp32 before the split, so bit-identical to a separate pass
+    float4 abr = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool aon = false;
     // stage s's A rows and weight slice into registers (s clamped: the loads past
     // the last stage reread it and are never stored)
 #define S3_LOAD(s_)                                                                       \
@@ -179,6 +185,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_split3_kernel(
         const int k0_ = kStep * s;                                                        \
         _Pragma("unroll") for (int j = 0; j < AL; ++j) ar[j] =                            \
             *reinterpret_cast<const float4 *>(k0_ < K1 ? arow[j] + k0_ : arow2[j] + (k0_ - K1)); \
+        aon = abias != nullptr && k0_ < K1;                                               \
+        if (aon) abr = *reinterpret_cast<const float4 *>(abias + k0_ + 4 * kq);            \
         _Pragma("unroll") for (int j = 0; j < WL; ++j) {                                  \
             const int i = t + NTH * j;                                                    \
             wr[j] = (WCELLS % NTH == 0 || i < WCELLS) ? wsrc[s * wstep + i]               \
@@ -189,6 +197,14 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_split3_kernel(
 #define S3_STORE(buf)                                                                     \
     do {                                                                                  \
         unsigned char *base_ = lds + (buf) * BUF;                                         \
+        if (aon) {                                                                        \
+            _Pragma("unroll") for (int j = 0; j < AL; ++j) {                              \
+                ar[j].x = fmaxf(ar[j].x + abr.x, 0.f);                                    \
+                ar[j].y = fmaxf(ar[j].y + abr.y, 0.f);                                    \
+                ar[j].z = fmaxf(ar[j].z + abr.z, 0.f);                                    \
+                ar[j].w = fmaxf(ar[j].w + abr.w, 0.f);                                    \
+            }                                                                             \
+        }                                                                                 \
         _Pragma("unroll") for (int j = 0; j < AL; ++j) {                                  \
             const int row = (t >> 2) + RPJ * j, pt = row >> 5, r = row & 31;              \
             uint32_t p00, p10, p20, p01, p11, p21;                                        \
@@ -362,7 +378,7 @@ template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0, i
 int launch_cfg(const float *A, int M, int K, const uint4 *Wp, int N, const float *bias,
                const float *R, float *D, int H, int W, int SH, int SW, hipStream_t s,
                const float *cb = nullptr, const int32_t *rch = nullptr,
-               const float *A2 = nullptr, int K2 = 0) {
+               const float *A2 = nullptr, int K2 = 0, const float *abias = nullptr) {
     constexpr int PT = BM / 32, NTW = BN / 32;
     constexpr size_t lds = 2 * (size_t)(3 * PT + NTW * 3) * kFragBytes;
     static_assert(lds <= VD_LDS_BYTES, "LDS");
@@ -376,19 +392,21 @@ int launch_cfg(const float *A, int M, int K, const uint4 *Wp, int N, const float
     if (num_tiles >= (1ll << 31) - 8) return VD_ERR_SHAPE;
     const int64_t grid = (num_tiles + 7) / 8 * 8;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NW), lds, s, A, Wp, bias, R, D, M, N,
-                       K, tiles_n, (int)num_tiles, H, W, SH, SW, cb, rch, A2, K2);
+                       K, tiles_n, (int)num_tiles, H, W, SH, SW, cb, rch, A2, K2, abias);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 
 template <int BM, int BN, int TPM, int TPN, int OCC, int NW = 4>
 int launch_epi(const float *A, int M, int K, const uint4 *Wp, int N, const float *bias,
                const float *R, int relu, float *D, int H, int W, int SH, int SW, hipStream_t s,
-               const float *A2, int K2) {
+               const float *A2, int K2, const float *abias) {
 #define VD_S3_RELU(RES_)                                                                       \
     return relu ? launch_cfg<BM, BN, TPM, TPN, RES_, true, 0, OCC, NW>(                        \
-                      A, M, K, Wp, N, bias, R, D, H, W, SH, SW, s, nullptr, nullptr, A2, K2)   \
+                      A, M, K, Wp, N, bias, R, D, H, W, SH, SW, s, nullptr, nullptr, A2, K2,   \
+                      abias)                                                                   \
                 : launch_cfg<BM, BN, TPM, TPN, RES_, false, 0, OCC, NW>(                       \
-                      A, M, K, Wp, N, bias, R, D, H, W, SH, SW, s, nullptr, nullptr, A2, K2)
+                      A, M, K, Wp, N, bias, R, D, H, W, SH, SW, s, nullptr, nullptr, A2, K2,   \
+                      abias)
     if (R && H > 0) VD_S3_RELU(2);
     if (R) VD_S3_RELU(1);
     VD_S3_RELU(0);
@@ -418,9 +436,11 @@ int launch_gemm_split3_weight(const float *W, int N, int K, void *Wp, hipStream_
 // x up_h x up_w, both even), read at the nearest-2x row of each pixel.  sub_h / sub_w
 // > 0: A is an images x sub_h x sub_w map read at stride 2 (M = images x ceil(sub_h / 2)
 // x ceil(sub_w / 2)): a stride-2 pad-0 1x1 convolution without the subsampled copy.
+// a_bias (K - K2 floats, or null): A's channels enter as relu(A + a_bias[k]).
 int launch_gemm_split3(const float *A, int M, int K, const float *A2, int K2, const void *Wp,
                        int N, const float *bias, const float *R, int up_h, int up_w, int sub_h,
-                       int sub_w, int relu, float *D, int cfg, hipStream_t s) {
+                       int sub_w, int relu, float *D, int cfg, hipStream_t s,
+                       const float *a_bias) {
     if (M == 0) return VD_OK;
     if (!gemm_split3_supported(K, N)) return VD_ERR_SHAPE;
     if (K2 < 0 || K2 >= K || (K2 && (!A2 || K2 % kStep || sub_h || sub_w))) return VD_ERR_ARG;
@@ -462,22 +482,22 @@ int launch_gemm_split3(const float *A, int M, int K, const float *A2, int K2, co
     case 1:
         if (N % 256) return VD_ERR_SHAPE;
         return launch_epi<256, 256, 4, 4, 1>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
-                                             s, A2, K2);
+                                             s, A2, K2, a_bias);
     case 2:
         if (N % 128) return VD_ERR_SHAPE;
         return launch_epi<256, 128, 4, 2, 2>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
-                                             s, A2, K2);
+                                             s, A2, K2, a_bias);
     case 5:
         if (N % 256) return VD_ERR_SHAPE;
         return launch_epi<256, 256, 4, 2, 1, 8>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h,
-                                                sub_w, s, A2, K2);
+                                                sub_w, s, A2, K2, a_bias);
     case 4:
         if (N % 128) return VD_ERR_SHAPE;
         return launch_epi<128, 128, 2, 2, 3>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
-                                             s, A2, K2);
+                                             s, A2, K2, a_bias);
     case 3:
         return launch_epi<256, 64, 4, 1, 2>(A, M, K, w, N, bias, R, relu, D, up_h, up_w, sub_h, sub_w,
-                                             s, A2, K2);
+                                             s, A2, K2, a_bias);
 #ifdef VD_RESEARCH_PROBES
     case 11: case 12: case 13:  // speed-of-light probes of cfg 1 (wrong results by design)
         if (N % 256 || R || !relu) return VD_ERR_SHAPE;

@@ -61,7 +61,8 @@ size_t gemm_split3_weight_bytes(int N, int K);
 int launch_gemm_split3_weight(const float *W, int N, int K, void *Wp, hipStream_t s);
 int launch_gemm_split3(const float *A, int M, int K, const float *A2, int K2, const void *Wp,
                        int N, const float *bias, const float *R, int up_h, int up_w, int sub_h,
-                       int sub_w, int relu, float *D, int cfg, hipStream_t s);
+                       int sub_w, int relu, float *D, int cfg, hipStream_t s,
+                       const float *a_bias = nullptr);
 int launch_gemm_split3_mask_logits(const float *A, int M, int K, const void *Wp, int N,
                                    const float *bias, const float *cls_w, const float *cls_b,
                                    const int32_t *roi_ch, int P, float *masks, hipStream_t s);

@@ -367,7 +367,15 @@ class Bottleneck(nn.Module):
         if out is None:
             out = _conv_epi(self.f1, x)
         y = _conv3x3_mfma(self.f2, out, relu=True)  # res2 / res3 3x3s (>= 2^18 px)
-        out = y if y is not None else _conv_epi(self.f2, out)
+        pre = None  # conv2's bias, applied (+ ReLU) by conv3's split GEMM as it loads A
+        if y is not None:
+            out = y
+        elif _conv2_prologue_ok(self.f2, self.w3):
+            # ResNeXt's grouped conv2 (MIOpen, no epilogue): its bias + ReLU ride on
+            # conv3's A load instead of a separate pass over the conv2 output
+            out, pre = _conv_nb(self.f2, out), self.f2.bias
+        else:
+            out = _conv_epi(self.f2, out)
         if self.downsample is not None:
             if self.fd.stride == (1, 1) and x.is_contiguous(memory_format=torch.channels_last):
                 # conv3 and the stride-1 downsample as one two-operand MFMA GEMM
@@ -377,19 +385,22 @@ class Bottleneck(nn.Module):
                         out.shape[1] % 16 == 0 and self.w3d.shape[0] % 64 == 0:
                     # round 6: on the bf16 matrix cores at fp32 accuracy (split GEMM, A2)
                     y = ops.gemm_split3_bias_act(_nhwc2d(out), ops.split3_weight_cached(self.w3d),
-                                                 self.b3d, a2=_nhwc2d(x))
+                                                 self.b3d, a2=_nhwc2d(x), a_bias=pre)
                 else:
+                    if pre is not None:
+                        out, pre = ops.bias_act_(out, pre, relu=True), None
                     y = ops.gemm_dual_bias_act(_nhwc2d(out), _nhwc2d(x), self.w3d, self.b3d)
                 if y is not None:
                     return y.view(N, H, W, -1).permute(0, 3, 1, 2)
             if s2:  # relu(h W3^T + b3 + (x[::2, ::2] Wd^T + bd))
                 r = _gemm_conv1x1_s2(x, self.wd, self.fd.bias, relu=False)
-                return _gemm_conv1x1(out, self.w3, self.f3.bias, relu=True, res=r)
+                return _gemm_conv1x1(out, self.w3, self.f3.bias, relu=True, res=r, a_bias=pre)
             if xs is not None:  # relu(h W3^T + b3 + (xs Wd^T + bd))
                 r = _gemm_conv1x1(xs, self.wd, self.fd.bias, relu=False)
-                return _gemm_conv1x1(out, self.w3, self.f3.bias, relu=True, res=r)
-            return _gemm_conv1x1(out, self.w3, self.b3d, relu=True, res=_conv_nb(self.fd, x))
-        return _gemm_conv1x1(out, self.w3, self.f3.bias, relu=True, res=x)
+                return _gemm_conv1x1(out, self.w3, self.f3.bias, relu=True, res=r, a_bias=pre)
+            return _gemm_conv1x1(out, self.w3, self.b3d, relu=True, res=_conv_nb(self.fd, x),
+                                 a_bias=pre)
+        return _gemm_conv1x1(out, self.w3, self.f3.bias, relu=True, res=x, a_bias=pre)
 
 
 def _is_1x1(conv: nn.Conv2d) -> bool:
@@ -434,16 +445,31 @@ def _nhwc2d(x):
     return x.permute(0, 2, 3, 1).reshape(N * H * W, C)
 
 
-def _gemm_conv1x1(x, w2d, bias, relu=True, res=None):
-    """Stride-1 1x1 conv of a channels_last NCHW tensor as act(X W^T + b [+ res])."""
+def _conv2_prologue_ok(conv2: nn.Conv2d, w3) -> bool:
+    """A grouped conv2 (ResNeXt, on MIOpen) whose bias + ReLU conv3's split-bf16 GEMM
+    applies as it loads its input (ops.gemm_split3_bias_act a_bias), instead of a
+    separate pass: conv3 must take the split GEMM (K = conv2's channels >= SPLIT3_MIN_K,
+    K % 16, N % 64).  VOSDET_CONV2_PROLOGUE=0 keeps the separate pass."""
+    import os
+    k = conv2.out_channels
+    return (conv2.groups > 1 and conv2.bias is not None and ops.split3_enabled()
+            and k >= ops.SPLIT3_MIN_K and k % 16 == 0 and w3.shape[0] % 64 == 0
+            and w3.shape[1] == k and os.environ.get("VOSDET_CONV2_PROLOGUE", "1") != "0")
+
+
+def _gemm_conv1x1(x, w2d, bias, relu=True, res=None, a_bias=None):
+    """Stride-1 1x1 conv of a channels_last NCHW tensor as act(X W^T + b [+ res]);
+    a_bias: X enters as relu(X + a_bias) (the producing conv's epilogue, fused)."""
     N, C, H, W = x.shape
     r = None
     if res is not None:
         if not res.is_contiguous(memory_format=torch.channels_last):
             res = res.contiguous(memory_format=torch.channels_last)
         r = _nhwc2d(res)
-    y = ops.gemm_bias_act(_nhwc2d(x), w2d, bias, residual=r, relu=relu)
+    y = ops.gemm_bias_act(_nhwc2d(x), w2d, bias, residual=r, relu=relu, a_bias=a_bias)
     if y is None:  # no GEMM algorithm for the shape: MIOpen's 1x1 conv + torch epilogue
+        if a_bias is not None:
+            x = ops.bias_act_(x, a_bias, relu=True)
         y = F.conv2d(x, w2d.view(w2d.shape[0], C, 1, 1), bias)
         if res is not None:
             y = y + res

@@ -574,13 +574,16 @@ def split3_weight_cached(w: torch.Tensor) -> Optional[torch.Tensor]:
 
 def gemm_bias_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
                   residual: Optional[torch.Tensor] = None, relu: bool = True,
-                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  out: Optional[torch.Tensor] = None,
+                  a_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """act(a @ w.T + bias (+ residual)) in one GEMM launch: a [M,K], w [N,K], bias [N],
     residual / out [M,N], all fp32 contiguous.  From K = SPLIT3_MIN_K (N a multiple
     of 64) on the bf16 matrix cores at fp32 accuracy (gemm_split3_bias_act, the
     weight's split image cached per tensor); otherwise vd_gemm_bias_act (hipBLASLt
     with the epilogue fused, or the hand-written fp32 MFMA kernel where it is
-    faster).  Returns None when nothing serves the shape (the caller falls back)."""
+    faster).  a_bias [K]: a enters as relu(a + a_bias) (fused into the split GEMM's A
+    load; a separate pass before the other kernels).  Returns None when nothing serves
+    the shape (the caller falls back, a_bias not applied)."""
     a_ = _need(a, "a")
     w_ = _need(w, "w")
     b_ = _need(bias, "bias")
@@ -601,7 +604,10 @@ def gemm_bias_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
     if K >= SPLIT3_MIN_K and N % 64 == 0 and K % 16 == 0 and M > 0 and split3_enabled():
         wp = split3_weight_cached(w if w.is_contiguous() else w_)
         if wp is not None:
-            return gemm_split3_bias_act(a_, wp, b_, residual=r_, relu=relu, out=out)
+            return gemm_split3_bias_act(a_, wp, b_, residual=r_, relu=relu, out=out,
+                                        a_bias=a_bias)
+    if a_bias is not None:
+        a_ = torch.relu(a_ + _need(a_bias, "a_bias"))
     ws = gemm_workspace(a_.device)
     st = lib().vd_gemm_bias_act(a_.data_ptr(), M, K, w_.data_ptr(), N, b_.data_ptr(),
                                 r_.data_ptr() if r_ is not None else None, int(relu),
@@ -633,7 +639,8 @@ def gemm_split3_bias_act(a: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor,
                          out: Optional[torch.Tensor] = None, cfg: int = 0,
                          up_hw: Optional[Sequence[int]] = None,
                          sub_hw: Optional[Sequence[int]] = None,
-                         a2: Optional[torch.Tensor] = None) -> torch.Tensor:
+                         a2: Optional[torch.Tensor] = None,
+                         a_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """act(a @ w.T + bias (+ residual)) with the fp32 operands split into three bf16
     pieces on the bf16 matrix cores (vd_gemm_split3_bias_act, fp32 accuracy):
     a [M,K], wp from gemm_split3_weight(w [N,K]), bias [N], out [M,N]; residual
@@ -642,7 +649,8 @@ def gemm_split3_bias_act(a: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor,
     sub_hw = (H, W): a is an images x H x W map's rows [images H W, K] read at
     stride 2, M = images x ceil(H/2) x ceil(W/2) output rows (a stride-2 1x1 conv).
     With a2 [M, K2]: w's last K2 input channels multiply a2 (a is [M, K - K2]): two
-    1x1 convs of two inputs summed in one GEMM."""
+    1x1 convs of two inputs summed in one GEMM.  With a_bias [K - K2]: a enters as
+    relu(a + a_bias) (the producing layer's bias + ReLU, fused into the A load)."""
     a_ = _need(a, "a")
     N, K = wp.split3_shape
     M = a_.shape[0]
@@ -663,6 +671,11 @@ def gemm_split3_bias_act(a: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor,
     if a_.dim() != 2 or a_.shape[1] + K2 != K or b_.numel() != N:
         raise ValueError("gemm_split3_bias_act: a %s, w (%d, %d), bias %s"
                          % (tuple(a_.shape), N, K, tuple(b_.shape)))
+    ab_ = None
+    if a_bias is not None:
+        ab_ = _need(a_bias, "a_bias")
+        if ab_.numel() != K - K2:
+            raise ValueError("a_bias must have %d entries, got %d" % (K - K2, ab_.numel()))
     r_ = None
     uh = uw = 0
     if residual is not None:
@@ -681,6 +694,7 @@ def gemm_split3_bias_act(a: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor,
         raise ValueError("out must be a contiguous %s tensor" % ((M, N),))
     check(lib().vd_gemm_split3_bias_act(a_.data_ptr(), M, K,
                                         a2_.data_ptr() if a2_ is not None else None, K2,
+                                        ab_.data_ptr() if ab_ is not None else None,
                                         wp.data_ptr(), N, b_.data_ptr(),
                                         r_.data_ptr() if r_ is not None else None, uh, uw,
                                         sh, sw, int(relu), out.data_ptr(), int(cfg), _stream()),
