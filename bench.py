@@ -278,7 +278,8 @@ def frame_flops(sd, cfg, frames=16):
     ref, fr, _ = ref_cpu_pipeline(sd, 0, cfg)
     with FlopCounterMode(display=False) as fc, _WinoFlops(frames) as wf:
         res = ref(fr[0])
-    return int(fc.get_total_flops()), int(len(res[1])), wf.flops, wf.flops4, wf.split3
+    return (int(fc.get_total_flops()), int(len(res[1])), wf.flops, wf.flops4, wf.split3,
+            wf.grouped_adj)
 
 
 class _WinoFlops(torch.overrides.TorchFunctionMode):
@@ -294,6 +295,9 @@ class _WinoFlops(torch.overrides.TorchFunctionMode):
     def __init__(self, frames=16):
         super().__init__()
         self.flops, self.flops4, self.split3, self.frames = 0, 0, 0, frames
+        # grouped 3x3s on the F(4x4) kernel's block-diagonal form: executed MFMA work
+        # minus what the flop counter counts for them (16 / (C / groups) x its count)
+        self.grouped_adj = 0
 
     def __torch_function__(self, func, types, args=(), kwargs=None):
         from vosdetectron_amd import ops
@@ -331,6 +335,12 @@ class _WinoFlops(torch.overrides.TorchFunctionMode):
             pd = tuple(padding) if isinstance(padding, (tuple, list)) else (padding, padding)
             Cout, Cin = w.shape[0], w.shape[1]
             N, H, W = out.shape[0], out.shape[2], out.shape[3]
+            if tuple(w.shape[2:]) == (3, 3) and st == (1, 1) and pd == (1, 1) and groups > 1:
+                from vosdetectron_amd.modeling import conv3x3_grouped_route
+                if conv3x3_grouped_route(N * self.frames, Cin * groups, Cout, H, W,
+                                         groups) is not None:
+                    fc_ = 2 * N * H * W * Cout * Cin * 9  # Cin = C / groups here
+                    self.grouped_adj += fc_ * 16 // Cin - fc_
             if tuple(w.shape[2:]) == (3, 3) and st == (1, 1) and pd == (1, 1) and groups == 1:
                 # one reference frame's conv -> the engine's batch of `frames` frames
                 algo = conv3x3_route(N * self.frames, Cin, Cout, H, W)[0]
@@ -465,7 +475,8 @@ def measure_split_gemm(dev, M=32000, N=1024, K=12544, iters=10):
 
 
 def step_roofline(flops_frame, dets_cpu, frames, ms_per_step, engine_launch, frame_hw, blob_hw,
-                  wino_flops_frame=0, wino4_flops_frame=0, split3_flops_frame=0):
+                  wino_flops_frame=0, wino4_flops_frame=0, split3_flops_frame=0,
+                  grouped_adj_frame=0):
     """the FPS as a fraction of the roofline = sum of per-stage
     bound times / measured step time.  MFMA-bound stages: the FLOPs the engine's
     MFMAs execute for one frame at the fp32 matrix peak -- the reference's
@@ -481,7 +492,7 @@ def step_roofline(flops_frame, dets_cpu, frames, ms_per_step, engine_launch, fra
     six bf16 products per fp32 MAC on the bf16 matrix cores: priced at 6 x their
     FLOPs at the dense bf16 peak (0.38 of their time at the fp32 peak)."""
     exec_flops = (flops_frame - wino_flops_frame * (1 - 1 / 2.25)
-                  - wino4_flops_frame * (1 - 1 / 4.0))
+                  - wino4_flops_frame * (1 - 1 / 4.0) + grouped_adj_frame)
     exec_ms = ((exec_flops - split3_flops_frame) / (MFMA_FP32_PEAK_TFS * 1e12)
                + 6 * split3_flops_frame / (MFMA_BF16_PEAK_TFS * 1e12)) * frames * 1e3
     direct_ms = flops_frame * frames / (MFMA_FP32_PEAK_TFS * 1e12) * 1e3
@@ -1204,13 +1215,14 @@ def main():
             extra["split_gemm"] = measure_split_gemm(dev, M=F * 1000)
         nthr = torch.get_num_threads()
         torch.set_num_threads(cpu_share()[0])
-        flops, dets_cpu, wino_flops, wino4_flops, split3_flops = frame_flops(sd, cfg, F)
+        flops, dets_cpu, wino_flops, wino4_flops, split3_flops, grouped_adj = \
+            frame_flops(sd, cfg, F)
         torch.set_num_threads(nthr)
         extra["step_roofline"] = step_roofline(
             flops, dets_cpu, F, dt / args.steps * 1e3, roof.get("engine_launch") if roof else None,
             (fh, fw),
             (getattr(pipe, "Hp", fh), getattr(pipe, "Wp", fw)),
-            wino_flops, wino4_flops, split3_flops)
+            wino_flops, wino4_flops, split3_flops, grouped_adj)
     cpu = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:
         cpu = cpu_baseline(args.config, sd, args.cpu_frames, cfg=cfg)

@@ -253,6 +253,15 @@ int vd_conv3x3_wino4_mosaic_bias_act(const float *X, int N, int H, int W, int C,
 int vd_conv3x3_wino4_rows_bias_act(const float *X, int N, int H, int W, int C, const float *U,
                                    int Cout, const float *bias, int relu, float *Y,
                                    void *stream);
+/* A grouped 3x3 convolution (ResNeXt's conv2, ResNet.py:246-294 with groups > 1; C
+ * in = out channels, C / groups dividing 64) by the same F(4x4) kernel: every 64-channel
+ * output block reads only the 64 input channels of its groups.  U =
+ * vd_conv3x3_wino4_weight of the block-diagonal expansion of the [C][C / groups][3][3]
+ * weight to [C][64][3][3] (zeros between groups; Cin = 64).  rows != 0: the N maps as
+ * the row stack of vd_conv3x3_wino4_rows_bias_act.  VD_ERR_SHAPE for other shapes. */
+int vd_conv3x3_wino4_grouped_bias_act(const float *X, int N, int H, int W, int C,
+                                      const float *U, int groups, const float *bias, int relu,
+                                      float *Y, int rows, void *stream);
 /* The same over N maps laid out as a 2-D grid at a pitch of (H + 1) x (W + 1) -- one
  * zero row / column shared between neighbours, g maps per grid row chosen for the
  * fewest 16 x 32 output blocks (round 6; the mask head's 14 x 14 RoI maps: 32 per

@@ -207,3 +207,92 @@ def test_wino4_mask_head_routes_to_grid(monkeypatch):
     assert modeling.conv3x3_route(8000, 512, 512, 7, 7) == ("wino4", "pair")
     monkeypatch.setenv("VOSDET_WINO4_GRID", "0")
     assert modeling.conv3x3_route(3200, 256, 256, 14, 14) == ("wino4", "pair")
+
+
+@pytest.mark.parametrize("N,C,H,W,groups,rows", [(2, 256, 20, 36, 32, False),
+                                                 (2, 512, 17, 45, 32, False),
+                                                 (1, 1024, 25, 42, 32, False),
+                                                 (2, 2048, 13, 21, 32, False),
+                                                 (3, 256, 50, 84, 32, True),
+                                                 (4, 128, 9, 11, 16, True),
+                                                 (2, 512, 33, 31, 64, False)])
+@pytest.mark.parametrize("bias", [True, False])
+def test_wino4_grouped(N, C, H, W, groups, rows, bias):
+    """vd_conv3x3_wino4_grouped_bias_act (ResNeXt's grouped conv2 on the F(4x4) kernel,
+    the weight block-diagonal per 64-channel block) vs torch's grouped conv: within
+    the F(4x4) tolerance, and against fp64 as close as the dense F(4x4) kernel is on a
+    dense conv of the same block width (mean within 1.5x)."""
+    from vosdetectron_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(N * 11 + C + H)
+    cpg = C // groups
+    x = torch.randn(N, C, H, W, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    w = torch.randn(C, cpg, 3, 3, device="cuda", generator=g) / (3. * cpg ** .5)
+    b = torch.randn(C, device="cuda", generator=g) if bias else None
+    u = ops.conv3x3_wino4_grouped_weight(w, groups)
+    y = ops.conv3x3_wino4_bias_act(x, u, b, relu=bias, groups=groups,
+                                   mosaic="rows" if rows else False)
+    torch.cuda.synchronize()
+    assert y is not None
+    ref = F.conv2d(x, w, b, padding=1, groups=groups)
+    if bias:
+        ref = F.relu(ref)
+    err = float((y - ref).abs().max())
+    assert err <= 5e-5 * max(1., float(ref.abs().max())), err
+    r64 = F.conv2d(x.double(), w.double(), b.double() if bias else None, padding=1,
+                   groups=groups)
+    if bias:
+        r64 = F.relu(r64)
+    e = (y.double() - r64).abs()
+    # the same conv as a dense one on the expanded (block-diagonal) weight
+    wd = torch.zeros(C, 64, 3, 3, device="cuda")
+    for co in range(C):
+        gi = co // cpg
+        lo = gi * cpg - (co // 64) * 64
+        wd[co, lo:lo + cpg] = w[co]
+    assert torch.equal(u, ops.conv3x3_wino4_weight(wd))
+    # deterministic
+    assert torch.equal(y, ops.conv3x3_wino4_bias_act(x, u, b, relu=bias, groups=groups,
+                                                     mosaic="rows" if rows else False))
+    assert float(e.max()) <= 2e-5 * max(1., float(r64.abs().max()))
+
+
+def test_wino4_grouped_refuses():
+    from vosdetectron_amd import ops
+    w = torch.zeros(96, 3, 3, 3, device="cuda")
+    assert ops.conv3x3_wino4_grouped_weight(w, 32) is None       # C % 64
+    w = torch.zeros(256, 48, 3, 3, device="cuda")
+    assert ops.conv3x3_wino4_grouped_weight(w, 5) is None        # cpg * groups != C
+
+
+def test_resnext_body_grouped_route(monkeypatch):
+    """X-101-32x8d's body with its stride-1 grouped conv2s on the F(4x4) grouped form
+    (the workgroup gate lowered so a small batch takes it): the route counter shows it
+    ran, and against a float64 CPU evaluation of the same body its P2-P6 error is no
+    larger than the MIOpen route's (VOSDET_WINO4_GROUPED=0): max within 2x, mean
+    within 1.5x."""
+    import copy
+    from vosdetectron_amd import config as vcfg, modeling
+    from vosdetectron_amd.weights import build_model
+    cfg = vcfg.get("e2e_mask_rcnn_X-101-32x8d-FPN_1x")
+    model, _ = build_model(cfg, seed=0, device="cuda", channels_last=True)
+    monkeypatch.setattr(modeling, "_WINO4_MIN_WGS", 1)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    xc = torch.rand((2, 3, 128, 160), generator=g) * 255 - 120
+    x = xc.to("cuda").contiguous(memory_format=torch.channels_last)
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("VOSDET_WINO4_GROUPED", flag)
+        modeling.ROUTE_COUNTS.clear()
+        with torch.no_grad():
+            outs[flag] = [t.double().cpu() for t in model.Conv_Body(x)]
+        n = modeling.ROUTE_COUNTS.get("wino4_grouped", 0)
+        assert (n >= 5) if flag == "1" else (n == 0), modeling.ROUTE_COUNTS
+    m64 = copy.deepcopy(model).cpu().double()
+    with torch.no_grad():
+        ref = [t.double() for t in m64.Conv_Body(xc.double())]
+    for p, q, r in zip(outs["1"], outs["0"], ref):
+        ep, eq = (p - r).abs(), (q - r).abs()
+        assert float(ep.max()) <= 2 * float(eq.max()) + 1e-9, (float(ep.max()), float(eq.max()))
+        assert float(ep.mean()) <= 1.5 * float(eq.mean()) + 1e-12, (float(ep.mean()),
+                                                                    float(eq.mean()))

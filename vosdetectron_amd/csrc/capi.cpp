@@ -205,6 +205,15 @@ int vd_conv3x3_wino4_rows_bias_act(const float *X, int N, int H, int W, int C, c
     return launch_conv3x3_wino4(X, N, H, W, C, U, Cout, bias, relu, Y, VD_STREAM(stream), 2);
 }
 
+int vd_conv3x3_wino4_grouped_bias_act(const float *X, int N, int H, int W, int C,
+                                      const float *U, int groups, const float *bias, int relu,
+                                      float *Y, int rows, void *stream) {
+    if (N < 0 || H < 1 || W < 1 || C < 1 || groups < 1 || !U || !Y || (N > 0 && !X))
+        return VD_ERR_ARG;
+    return launch_conv3x3_wino4(X, N, H, W, C, U, C, bias, relu, Y, VD_STREAM(stream),
+                                rows ? 2 : 0, groups);
+}
+
 int vd_conv3x3_wino4_grid_bias_act(const float *X, int N, int H, int W, int C, const float *U,
                                    int Cout, const float *bias, int relu, float *Y,
                                    void *stream) {

@@ -168,7 +168,7 @@ template <bool RELU, int PROBE, bool ACC = false, int VD = 1, bool STAMP = false
 __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     const float *__restrict__ X, int N, int H, int W, int C, const float *__restrict__ U,
     int Cout, const float *__restrict__ bias, float *__restrict__ Y, int tby, int tbx,
-    int cb_per_xcd, int probe_hi, int mos) {
+    int cb_per_xcd, int probe_hi, int mos, int gin) {
     // static, not dynamic: a > 64 KiB dynamic allocation is honoured by a direct launch
     // after hipFuncSetAttribute but not by the same launch captured into a hipGraph
     // (every replayed P2 conv came out unwritten, round 5)
@@ -212,14 +212,17 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     const int tyb = rem / tbx, txb = rem - (rem / tbx) * tbx;
     const int oy0 = 4 * k4TR * tyb, ox0 = 4 * k4TC * txb;
     const int iy0 = oy0 - 1, ix0 = ox0 - 1;
-    const int nch = C / k4KC;
+    // gin (grouped, round 6): a workgroup's 64 output channels read only the 64 input
+    // channels of their groups -- input channels 64 cb .. + 63 at pixel stride C, U the
+    // block-diagonal expansion (zeros between groups) with Cin = 64
+    const int nch = (gin ? 64 : C) / k4KC;
     const uint32_t pbase = (uint32_t)(uintptr_t)pst;
 
     // ---- patch DMA (waves 0-3 only, so the U loads of waves 4-7 never wait behind a
     // patch piece): instructions i = wave + 4 k (k < 6) of 24; slot s -> row R, column
     // C = 2 m + (rem >> 1), half rem & 1 (rem = 4: the pad slot).  Sources as 32-bit
     // float offsets in frame n (bit 31: the zero page)
-    const float *const Xn = X + (int64_t)n * H * W * C;
+    const float *const Xn = X + (int64_t)n * H * W * C + (gin ? 64 * cb : 0);
     // kept in LDS (after the patch stages), not in six registers the MFMA phase needs
     uint32_t *const poff = reinterpret_cast<uint32_t *>(pst + 2 * k4PStageB) + tid;
     constexpr int kDW = ACC ? 8 : 4;  // waves issuing the patch DMA
@@ -958,9 +961,16 @@ int launch_conv3x3_wino4_weight(const float *w, int Cout, int C, float *U, hipSt
 }
 
 int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float *U, int Cout,
-                         const float *bias, int relu, float *Y, hipStream_t s, int mos) {
+                         const float *bias, int relu, float *Y, hipStream_t s, int mos,
+                         int groups) {
     if ((int64_t)N * H * W == 0) return VD_OK;
     if (!conv3x3_wino4_supported(C, Cout)) return VD_ERR_SHAPE;
+    // grouped: C == Cout, 64 input channels per 64-channel output block (C / groups
+    // divides 64); the pair / octet / grid mosaics stay dense-only
+    const int gin = groups > 1;
+    if (gin && (groups < 1 || C != Cout || C % 64 || C % groups || 64 % (C / groups) ||
+                mos == 1 || mos == 4))
+        return VD_ERR_SHAPE;
     if ((int64_t)N * H * W * C >= ((int64_t)1 << 40) || (int64_t)H * W * C >= ((int64_t)1 << 31))
         return VD_ERR_SHAPE;
     // the map-pair mosaic: two maps of at most 15 x 15 per 16 x 32 block (the 16 x 16
@@ -1018,7 +1028,7 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
         return e ? (atoi(e) >> 4) & 1 : 0;
     }();
     typedef void (*kern_t)(const float *, int, int, int, int, const float *, int, const float *,
-                           float *, int, int, int, int, int);
+                           float *, int, int, int, int, int, int);
     static const kern_t table[2][16] = {
         {conv3x3_wino4_kernel<false, 0>, conv3x3_wino4_kernel<false, 1>,
          conv3x3_wino4_kernel<false, 2>, conv3x3_wino4_kernel<false, 3>,
@@ -1039,7 +1049,7 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
     // read at every launch (a few us of host time), so one process can A/B the forms
     const char *pse = getenv("VOSDET_WINO4_PS");
     const bool ps = pse && pse[0] == '1';
-    if (ps && !probe && !mos) {
+    if (ps && !probe && !mos && !gin) {
         typedef void (*kps_t)(const float *, int, int, int, int, const float *, int,
                               const float *, float *, int, int, int);
         const char *ppe = getenv("VOSDET_WINO4_PSPROBE");
@@ -1092,7 +1102,7 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
                     : conv3x3_wino4_kernel<false, 0, true, 1, true, true>;
     const kern_t kern = (acc && !probe) ? kacc : table[relu ? 1 : 0][probe];
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(k4Threads), 0, s, X, N, H, W, C, U,
-                       Cout, bias, Y, tby, tbx, cbx, probe_hi | prio, mos);
+                       Cout, bias, Y, tby, tbx, cbx, probe_hi | prio, mos, gin);
     return hipGetLastError() == hipSuccess ? VD_OK : VD_ERR_LAUNCH;
 }
 

@@ -74,7 +74,8 @@ bool conv3x3_wino_supported(int C, int Cout);
 bool conv3x3_wino4_supported(int C, int Cout);
 int launch_conv3x3_wino4_weight(const float *w, int Cout, int C, float *U, hipStream_t s);
 int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float *U, int Cout,
-                         const float *bias, int relu, float *Y, hipStream_t s, int mos = 0);
+                         const float *bias, int relu, float *Y, hipStream_t s, int mos = 0,
+                         int groups = 1);
 int launch_conv3x3_wino_weight(const float *w, int Cout, int C, float *U, hipStream_t s);
 int launch_conv3x3_wino(const float *X, int N, int H, int W, int C, const float *U, int Cout,
                         const float *bias, int relu, float *Y, hipStream_t s, int seg_h = 0);

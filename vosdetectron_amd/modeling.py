@@ -229,6 +229,20 @@ def conv3x3_route(N: int, Cin: int, Cout: int, H: int, W: int, mosaic=True):
     return "igemm", None
 
 
+def conv3x3_grouped_route(N: int, C: int, Cout: int, H: int, W: int, groups: int):
+    """The layout a grouped 3x3 / stride-1 conv (ResNeXt's conv2) runs with on the
+    F(4x4) kernel's grouped form (each 64-channel output block reading the 64 input
+    channels of its groups, the weight block-diagonal: 64 / (C / groups) x the
+    multiplies of the grouped conv, still fewer than MIOpen / CK spend on these
+    shapes): False (plain) or "rows" -- the dense rule of _wino4_mode -- or None (not
+    served: C != Cout, C / groups not dividing 64, small batches; VOSDET_WINO4_GROUPED=0)."""
+    if os.environ.get("VOSDET_WINO4_GROUPED", "1") == "0" or groups < 2:
+        return None
+    if C != Cout or C % 64 or C % groups or 64 % (C // groups):
+        return None
+    return _wino4_mode(N, C, Cout, H, W)
+
+
 # conv3x3 launches per route since the last reset (host-side, also counted while a
 # hipGraph is captured): 'wino4', 'wino', 'wino_rows', 'wino_2d', 'igemm', 'miopen'
 ROUTE_COUNTS = {}
@@ -248,6 +262,25 @@ def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=True):
     output (77 % one map per block, 87.5 % stacked in one column) -- and the
     16-frame P3 / P4 maps 2 / 4 per row; bit-identical results.  The transformed
     weights are cached on the module."""
+    if (conv.groups > 1 and os.environ.get("VOSDET_CONV3X3_MFMA", "1") != "0" and x.is_cuda
+            and conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
+            and conv.dilation == (1, 1) and x.dtype == torch.float32
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        mode = conv3x3_grouped_route(x.shape[0], x.shape[1], conv.weight.shape[0], x.shape[2],
+                                     x.shape[3], conv.groups)
+        if mode is not None:
+            w = conv.weight
+            key = (w.data_ptr(), w._version)
+            if getattr(conv, "_vd_u4g_key", None) != key:
+                conv._vd_u4g = ops.conv3x3_wino4_grouped_weight(w.detach(), conv.groups)
+                conv._vd_u4g_key = key
+            b = conv.bias.detach() if (bias and conv.bias is not None) else None
+            if conv._vd_u4g is not None:
+                y = ops.conv3x3_wino4_bias_act(x, conv._vd_u4g, b, relu=relu,
+                                               mosaic=mode or False, groups=conv.groups)
+                if y is not None:
+                    _count_route("wino4_grouped")
+                    return y
     if (os.environ.get("VOSDET_CONV3X3_MFMA", "1") == "0" or not x.is_cuda
             or conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1)
             or conv.dilation != (1, 1) or conv.groups != 1 or x.dtype != torch.float32

@@ -847,16 +847,35 @@ def conv3x3_wino4_weight(w: torch.Tensor) -> Optional[torch.Tensor]:
     return u
 
 
+def conv3x3_wino4_grouped_weight(w: torch.Tensor, groups: int) -> Optional[torch.Tensor]:
+    """A grouped conv's weight [C][C / groups][3][3] (C / groups dividing 64) -> U for
+    vd_conv3x3_wino4_grouped_bias_act: the block-diagonal expansion to [C][64][3][3]
+    (each output channel's 64-channel input block, zeros outside its group) through
+    conv3x3_wino4_weight (once per model).  None for a shape the kernel does not serve."""
+    w_ = _need(w, "w")
+    C, cpg = int(w_.shape[0]), int(w_.shape[1])
+    if groups < 2 or cpg * groups != C or C % 64 or 64 % cpg or tuple(w_.shape[2:]) != (3, 3):
+        return None
+    G = 64 // cpg  # groups per 64-channel block
+    wd = torch.zeros((C // 64, G, cpg, G, cpg, 3, 3), dtype=w_.dtype, device=w_.device)
+    wg = w_.view(C // 64, G, cpg, cpg, 3, 3)
+    for i in range(G):
+        wd[:, i, :, i] = wg[:, i]
+    return conv3x3_wino4_weight(wd.view(C, 64, 3, 3))
+
+
 def conv3x3_wino4_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torch.Tensor],
                            relu: bool = False, out: Optional[torch.Tensor] = None,
-                           mosaic=False):
+                           mosaic=False, groups: int = 1):
     """act(conv3x3(x, pad 1) + bias) on a channels_last fp32 tensor by Winograd
     F(4x4,3x3) (vd_conv3x3_wino4_bias_act); u from conv3x3_wino4_weight.  mosaic
     True / "pair": maps of at most 15 x 15 two per output block
     (vd_conv3x3_wino4_mosaic_bias_act); "rows": the maps stacked in one column at a
     4-row pitch (vd_conv3x3_wino4_rows_bias_act); both bit-identical.  "grid": the
     maps as a 2-D grid at an (H + 1) x (W + 1) pitch (vd_conv3x3_wino4_grid_bias_act;
-    equal within Winograd rounding).  None for a shape the kernel does not serve."""
+    equal within Winograd rounding).  groups > 1: a grouped conv (u from
+    conv3x3_wino4_grouped_weight; mosaic False or "rows").  None for a shape the kernel
+    does not serve."""
     if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 4 \
             or not x.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("x must be a channels_last fp32 device tensor")
@@ -864,6 +883,24 @@ def conv3x3_wino4_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torc
         return None
     u_ = _need(u, "u")
     N, C, H, W = x.shape
+    if groups > 1:
+        if u_.dim() != 6 or tuple(u_.shape) != (C // 64, 8, 4, 18, 64, 4) or C % 64:
+            raise ValueError("grouped u must be [%d][8][4][18][64][4], got %s"
+                             % (C // 64, tuple(u_.shape)))
+        if mosaic not in (False, None, "rows"):
+            return None
+        b_ = _need(bias, "bias") if bias is not None else None
+        if out is None:
+            out = torch.empty((N, C, H, W), dtype=torch.float32, device=x.device,
+                              memory_format=torch.channels_last)
+        st = lib().vd_conv3x3_wino4_grouped_bias_act(
+            x.data_ptr(), N, H, W, C, u_.data_ptr(), int(groups),
+            b_.data_ptr() if b_ is not None else None, int(relu), out.data_ptr(),
+            int(mosaic == "rows"), _stream())
+        if st == VD_ERR_SHAPE:
+            return None
+        check(st, "vd_conv3x3_wino4_grouped_bias_act")
+        return out
     if u_.dim() != 6 or tuple(u_.shape[1:]) != (C // 8, 4, 18, 64, 4) or C % 8:
         raise ValueError("u must be [Cout/64][%d][4][18][64][4], got %s" % (C // 8, tuple(u_.shape)))
     Cout = u_.shape[0] * 64
