@@ -114,7 +114,7 @@ __global__ void split3_weight_kernel(const float *__restrict__ W, int N, int K,
 // (the RoI map side), D = masks [RoIs][2P][2P]; the relu'd upconv output never leaves
 // the workgroup.
 template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0, int OCC = 1,
-          int NW = 4>
+          int NW = 4, bool APRO = false>
 __global__ __launch_bounds__(64 * NW, OCC) void gemm_split3_kernel(
     const float *__restrict__ A, const uint4 *__restrict__ Wp, const float *__restrict__ bias,
     const float *__restrict__ R, float *__restrict__ D, int M, int N, int K, int tiles_n,
@@ -185,8 +185,10 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_split3_kernel(
         const int k0_ = kStep * s;                                                        \
         _Pragma("unroll") for (int j = 0; j < AL; ++j) ar[j] =                            \
             *reinterpret_cast<const float4 *>(k0_ < K1 ? arow[j] + k0_ : arow2[j] + (k0_ - K1)); \
-        aon = abias != nullptr && k0_ < K1;                                               \
-        if (aon) abr = *reinterpret_cast<const float4 *>(abias + k0_ + 4 * kq);            \
+        if constexpr (APRO) {                                                             \
+            aon = k0_ < K1;                                                               \
+            if (aon) abr = *reinterpret_cast<const float4 *>(abias + k0_ + 4 * kq);        \
+        }                                                                                 \
         _Pragma("unroll") for (int j = 0; j < WL; ++j) {                                  \
             const int i = t + NTH * j;                                                    \
             wr[j] = (WCELLS % NTH == 0 || i < WCELLS) ? wsrc[s * wstep + i]               \
@@ -197,7 +199,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_split3_kernel(
 #define S3_STORE(buf)                                                                     \
     do {                                                                                  \
         unsigned char *base_ = lds + (buf) * BUF;                                         \
-        if (aon) {                                                                        \
+        if (APRO && aon) {                                                                \
             _Pragma("unroll") for (int j = 0; j < AL; ++j) {                              \
                 ar[j].x = fmaxf(ar[j].x + abr.x, 0.f);                                    \
                 ar[j].y = fmaxf(ar[j].y + abr.y, 0.f);                                    \
@@ -374,7 +376,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void gemm_split3_kernel(
 }
 
 template <int BM, int BN, int TPM, int TPN, int RES, bool RELU, int PROBE = 0, int OCC = 1,
-          int NW = 4>
+          int NW = 4, bool APRO = false>
 int launch_cfg(const float *A, int M, int K, const uint4 *Wp, int N, const float *bias,
                const float *R, float *D, int H, int W, int SH, int SW, hipStream_t s,
                const float *cb = nullptr, const int32_t *rch = nullptr,
@@ -382,7 +384,7 @@ int launch_cfg(const float *A, int M, int K, const uint4 *Wp, int N, const float
     constexpr int PT = BM / 32, NTW = BN / 32;
     constexpr size_t lds = 2 * (size_t)(3 * PT + NTW * 3) * kFragBytes;
     static_assert(lds <= VD_LDS_BYTES, "LDS");
-    auto kern = gemm_split3_kernel<BM, BN, TPM, TPN, RES, RELU, PROBE, OCC, NW>;
+    auto kern = gemm_split3_kernel<BM, BN, TPM, TPN, RES, RELU, PROBE, OCC, NW, APRO>;
     static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  (int)lds) == hipSuccess;
@@ -407,6 +409,15 @@ int launch_epi(const float *A, int M, int K, const uint4 *Wp, int N, const float
                 : launch_cfg<BM, BN, TPM, TPN, RES_, false, 0, OCC, NW>(                       \
                       A, M, K, Wp, N, bias, R, D, H, W, SH, SW, s, nullptr, nullptr, A2, K2,   \
                       abias)
+    if (abias) {  // the A prologue: compiled only where it is used (conv3 after a
+                  // grouped conv2: ReLU, with or without a residual)
+        if (!relu || (R && H > 0)) return VD_ERR_ARG;
+        if (R)
+            return launch_cfg<BM, BN, TPM, TPN, 1, true, 0, OCC, NW, true>(
+                A, M, K, Wp, N, bias, R, D, H, W, SH, SW, s, nullptr, nullptr, A2, K2, abias);
+        return launch_cfg<BM, BN, TPM, TPN, 0, true, 0, OCC, NW, true>(
+            A, M, K, Wp, N, bias, R, D, H, W, SH, SW, s, nullptr, nullptr, A2, K2, abias);
+    }
     if (R && H > 0) VD_S3_RELU(2);
     if (R) VD_S3_RELU(1);
     VD_S3_RELU(0);
