@@ -341,6 +341,16 @@ class _WinoFlops(torch.overrides.TorchFunctionMode):
                                          groups) is not None:
                     fc_ = 2 * N * H * W * Cout * Cin * 9  # Cin = C / groups here
                     self.grouped_adj += fc_ * 16 // Cin - fc_
+            dil = kwargs.get("dilation", rest[2] if rest[2] is not None else 1)
+            dl = tuple(dil) if isinstance(dil, (tuple, list)) else (dil, dil)
+            if (tuple(w.shape[2:]) == (3, 3) and st == (1, 1) and pd == (2, 2) and dl == (2, 2)
+                    and groups == 1 and H % 2 == 0 and W % 2 == 0):
+                # dilation 2: the plain conv of 4 polyphase sub-maps (modeling._conv3x3_mfma)
+                algo = conv3x3_route(4 * N * self.frames, Cin, Cout, H // 2, W // 2)[0]
+                if algo == "wino":
+                    self.flops += 2 * N * H * W * Cout * Cin * 9
+                elif algo == "wino4":
+                    self.flops4 += 2 * N * H * W * Cout * Cin * 9
             if tuple(w.shape[2:]) == (3, 3) and st == (1, 1) and pd == (1, 1) and groups == 1:
                 # one reference frame's conv -> the engine's batch of `frames` frames
                 algo = conv3x3_route(N * self.frames, Cin, Cout, H, W)[0]

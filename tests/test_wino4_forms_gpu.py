@@ -296,3 +296,34 @@ def test_resnext_body_grouped_route(monkeypatch):
         assert float(ep.max()) <= 2 * float(eq.max()) + 1e-9, (float(ep.max()), float(eq.max()))
         assert float(ep.mean()) <= 1.5 * float(eq.mean()) + 1e-12, (float(ep.mean()),
                                                                     float(eq.mean()))
+
+
+@pytest.mark.parametrize("N,C,H,W,Co", [(1600, 256, 14, 14, 256), (5, 64, 14, 14, 64),
+                                        (3, 128, 20, 36, 128), (2, 8, 2, 4, 64)])
+@pytest.mark.parametrize("bias", [True, False])
+def test_dilated2_conv_polyphase(N, C, H, W, Co, bias):
+    """A 3x3 / dilation-2 / pad-2 conv (the VOS mask head) as the plain conv of its
+    four polyphase sub-maps on the Winograd kernels (modeling._conv3x3_mfma): within
+    the F(4x4) tolerance of torch's dilated conv, through the route counter."""
+    import torch.nn as nn
+    from vosdetectron_amd import modeling
+    g = torch.Generator(device="cuda").manual_seed(N + C + H)
+    conv = nn.Conv2d(C, Co, 3, 1, padding=2, dilation=2, bias=bias).cuda()
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(Co, C, 3, 3, device="cuda", generator=g) / (3. * C ** .5))
+        if bias:
+            conv.bias.copy_(torch.randn(Co, device="cuda", generator=g))
+    x = torch.randn(N, C, H, W, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    modeling.ROUTE_COUNTS.clear()
+    y = modeling._conv3x3_mfma(conv, x, bias=bias, relu=bias)
+    assert y is not None and modeling.ROUTE_COUNTS.get("dilated2", 0) == 1
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    step = max(1, 4096 // (H * W))
+    with torch.no_grad():
+        ref = torch.cat([conv(x[i:i + step]) for i in range(0, min(N, 256), step)])
+    if bias:
+        ref = F.relu(ref)
+    n = ref.shape[0]
+    err = float((y[:n] - ref).abs().max())
+    assert err <= 5e-5 * max(1., float(ref.abs().max())), err

@@ -252,6 +252,18 @@ def _count_route(name: str):
     ROUTE_COUNTS[name] = ROUTE_COUNTS.get(name, 0) + 1
 
 
+def _dilated2_ok(conv: nn.Conv2d, x) -> bool:
+    """A 3x3 / dilation-2 / pad-2 conv (the VOS mask head, MRCNN.DILATION = 2) of
+    even-sized channels_last maps, which _conv3x3_mfma runs as the plain 3x3 conv of
+    its four polyphase sub-maps (VOSDET_WINO_DILATED=0 keeps MIOpen)."""
+    return (conv.dilation == (2, 2) and conv.padding == (2, 2) and conv.stride == (1, 1)
+            and conv.kernel_size == (3, 3) and conv.groups == 1 and x.dim() == 4
+            and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and x.is_cuda
+            and x.dtype == torch.float32 and x.is_contiguous(memory_format=torch.channels_last)
+            and os.environ.get("VOSDET_WINO_DILATED", "1") != "0"
+            and os.environ.get("VOSDET_CONV3X3_MFMA", "1") != "0")
+
+
 def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=True):
     """conv (3x3, stride 1, pad 1) of a channels_last fp32 tensor on the
     hand-written MFMA kernels with the bias (+ ReLU) epilogue, or None where
@@ -261,10 +273,36 @@ def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=True):
     maps 8 side by side per 112-column row -- every 8 x 16-pixel block real
     output (77 % one map per block, 87.5 % stacked in one column) -- and the
     16-frame P3 / P4 maps 2 / 4 per row; bit-identical results.  The transformed
-    weights are cached on the module."""
+    weights are cached on the module.  A dilation-2 / pad-2 3x3 conv of even-sized
+    maps (round 6) is the plain pad-1 conv of its four polyphase sub-maps -- output
+    (2i + a, 2j + b) reads only inputs of parity (a, b), the dilated taps are that
+    sub-map's neighbours and its zero padding is one sub-pixel: space-to-batch, the
+    same kernels on 4N maps of H/2 x W/2 (the VOS mask head's 14 x 14 RoI maps become
+    7 x 7 octets), batch-to-space."""
+    if _dilated2_ok(conv, x):
+        N, C, H, W = x.shape
+        xs = x.permute(0, 2, 3, 1).reshape(N, H // 2, 2, W // 2, 2, C).permute(
+            2, 4, 0, 1, 3, 5).reshape(4 * N, H // 2, W // 2, C).permute(0, 3, 1, 2)
+        y = _conv3x3_mfma_core(conv, xs, bias, relu, mosaic, as_plain=True)
+        if y is None:
+            return None
+        Co = y.shape[1]
+        y = y.permute(0, 2, 3, 1).reshape(2, 2, N, H // 2, W // 2, Co).permute(
+            2, 3, 0, 4, 1, 5).reshape(N, H, W, Co).permute(0, 3, 1, 2)
+        _count_route("dilated2")
+        return y
+    return _conv3x3_mfma_core(conv, x, bias, relu, mosaic)
+
+
+def _conv3x3_mfma_core(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=True,
+                       as_plain=False):
+    """_conv3x3_mfma's body; as_plain: a dilation-2 / pad-2 conv taken as the pad-1 conv
+    it is on polyphase sub-maps (the caller has split x)."""
+    dil = (1, 1) if as_plain else conv.dilation
+    pad = (1, 1) if as_plain else conv.padding
     if (conv.groups > 1 and os.environ.get("VOSDET_CONV3X3_MFMA", "1") != "0" and x.is_cuda
-            and conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
-            and conv.dilation == (1, 1) and x.dtype == torch.float32
+            and conv.kernel_size == (3, 3) and conv.stride == (1, 1) and pad == (1, 1)
+            and dil == (1, 1) and x.dtype == torch.float32
             and x.is_contiguous(memory_format=torch.channels_last)):
         mode = conv3x3_grouped_route(x.shape[0], x.shape[1], conv.weight.shape[0], x.shape[2],
                                      x.shape[3], conv.groups)
@@ -282,8 +320,8 @@ def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=True):
                     _count_route("wino4_grouped")
                     return y
     if (os.environ.get("VOSDET_CONV3X3_MFMA", "1") == "0" or not x.is_cuda
-            or conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1)
-            or conv.dilation != (1, 1) or conv.groups != 1 or x.dtype != torch.float32
+            or conv.kernel_size != (3, 3) or conv.stride != (1, 1) or pad != (1, 1)
+            or dil != (1, 1) or conv.groups != 1 or x.dtype != torch.float32
             or not x.is_contiguous(memory_format=torch.channels_last)):
         if conv.kernel_size == (3, 3):
             _count_route("miopen")
@@ -527,8 +565,14 @@ def _gn(dim: int, cfg) -> nn.GroupNorm:
 
 def _gn_epi(conv: nn.Conv2d, gn: nn.GroupNorm, x, act="relu", res=None, res_gn=None, up=False):
     """conv (no bias) -> one vd_group_norm_act: act(GN(conv(x)) + res), the residual
-    optionally normalised by its own GroupNorm (res_gn) or nearest-2x upsampled."""
-    y = _conv_nb(conv, x)
+    optionally normalised by its own GroupNorm (res_gn) or nearest-2x upsampled.  A
+    3x3 / stride-1 conv takes the hand-written Winograd kernels where they serve it
+    (conv3x3_route; VOSDET_GN_WINO=0 keeps MIOpen)."""
+    y = None
+    if os.environ.get("VOSDET_GN_WINO", "1") != "0":
+        y = _conv3x3_mfma(conv, x, bias=False, relu=False)
+    if y is None:
+        y = _conv_nb(conv, x)
     return ops.group_norm_act(y, gn.num_groups, gn.weight, gn.bias, gn.eps, residual=res,
                               residual_gn=(res_gn.weight, res_gn.bias) if res_gn is not None
                               else None, upsample_residual=up, act=act, out=y)

@@ -21,7 +21,20 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import ops
-from .modeling import Generalized_RCNN, _conv_nb
+from .modeling import Generalized_RCNN, _conv3x3_mfma, _conv_nb
+
+
+def _gru_conv(conv, x):
+    """A ConvGRU gate conv (3x3, no bias) on the hand-written Winograd kernels where
+    they serve it (modeling.conv3x3_route: F(4x4) at the P2 / P3 level sizes), else
+    MIOpen (round 6: MIOpen's kernel took 11 ms per P2 gate conv of a 16-frame 480p
+    step).  VOSDET_GRU_WINO=0 keeps MIOpen for all of them."""
+    import os
+    if os.environ.get("VOSDET_GRU_WINO", "1") != "0":
+        y = _conv3x3_mfma(conv, x, bias=False, relu=False)
+        if y is not None:
+            return y
+    return _conv_nb(conv, x)
 
 
 class ConvGRUCell2d(nn.Module):
@@ -55,19 +68,19 @@ class ConvGRUCell2d(nn.Module):
         """The GRU step + the VOS pyramid fusion on the device.  h None = zero
         state.  Returns hn/2 + bilinear_0.5x(finer)/2 (or hn when finer is None)."""
         g = self.bz.num_groups
-        zx = _conv_nb(self.Wz_x, inp)
-        hx = _conv_nb(self.Wh_x, inp)
+        zx = _gru_conv(self.Wz_x, inp)
+        hx = _gru_conv(self.Wh_x, inp)
         if h is None:
             z, _ = ops.convgru_gates(zx, None, None, None, None, g, self.bz.weight, self.bz.bias,
                                      self.br.weight, self.br.bias, self.bz.eps)
             return ops.convgru_update(hx, None, z, None, g, self.bh.weight, self.bh.bias,
                                       finer=finer, eps=self.bh.eps)
-        rx = _conv_nb(self.Wr_x, inp)
-        zh = _conv_nb(self.Wz_h, h)
-        rh = _conv_nb(self.Wr_h, h)
+        rx = _gru_conv(self.Wr_x, inp)
+        zh = _gru_conv(self.Wz_h, h)
+        rh = _gru_conv(self.Wr_h, h)
         z, hr = ops.convgru_gates(zx, rx, h, zh, rh, g, self.bz.weight, self.bz.bias,
                                   self.br.weight, self.br.bias, self.bz.eps)
-        hh = _conv_nb(self.Wh_h, hr)
+        hh = _gru_conv(self.Wh_h, hr)
         return ops.convgru_update(hx, hh, z, h, g, self.bh.weight, self.bh.bias, finer=finer,
                                   eps=self.bh.eps)
 
