@@ -327,3 +327,28 @@ def test_dilated2_conv_polyphase(N, C, H, W, Co, bias):
     n = ref.shape[0]
     err = float((y[:n] - ref).abs().max())
     assert err <= 5e-5 * max(1., float(ref.abs().max())), err
+
+
+@pytest.mark.parametrize("N,C,H,W,Co", [(1600, 256, 14, 14, 256), (5, 64, 14, 14, 64),
+                                        (3, 128, 20, 36, 128), (7, 64, 28, 30, 64)])
+def test_dilated2_inplace_equals_copies(N, C, H, W, Co, monkeypatch):
+    """The dilation-2 conv read / written in place by the kernel
+    (vd_conv3x3_wino4_dilated2_bias_act) == the same kernel on copied polyphase
+    sub-maps (VOSDET_DILATED_INPLACE=0), bit for bit (same sub-map order, same blocks)."""
+    import torch.nn as nn
+    from vosdetectron_amd import modeling
+    g = torch.Generator(device="cuda").manual_seed(N * 5 + C + H)
+    conv = nn.Conv2d(C, Co, 3, 1, padding=2, dilation=2, bias=True).cuda()
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(Co, C, 3, 3, device="cuda", generator=g) / (3. * C ** .5))
+        conv.bias.copy_(torch.randn(Co, device="cuda", generator=g))
+    x = torch.randn(N, C, H, W, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    monkeypatch.setenv("VOSDET_DILATED_INPLACE", "1")
+    y1 = modeling._conv3x3_mfma(conv, x, bias=True, relu=True)
+    monkeypatch.setenv("VOSDET_DILATED_INPLACE", "0")
+    y0 = modeling._conv3x3_mfma(conv, x, bias=True, relu=True)
+    torch.cuda.synchronize()
+    assert y1 is not None and y0 is not None
+    assert y1.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(y1, y0), float((y1 - y0).abs().max())

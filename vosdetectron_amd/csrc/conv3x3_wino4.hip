@@ -215,14 +215,27 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
     // gin (grouped, round 6): a workgroup's 64 output channels read only the 64 input
     // channels of their groups -- input channels 64 cb .. + 63 at pixel stride C, U the
     // block-diagonal expansion (zeros between groups) with Cin = 64
-    const int nch = (gin ? 64 : C) / k4KC;
+    const int nch = ((gin & 1) ? 64 : C) / k4KC;
     const uint32_t pbase = (uint32_t)(uintptr_t)pst;
 
     // ---- patch DMA (waves 0-3 only, so the U loads of waves 4-7 never wait behind a
     // patch piece): instructions i = wave + 4 k (k < 6) of 24; slot s -> row R, column
     // C = 2 m + (rem >> 1), half rem & 1 (rem = 4: the pad slot).  Sources as 32-bit
     // float offsets in frame n (bit 31: the zero page)
-    const float *const Xn = X + (int64_t)n * H * W * C + (gin ? 64 * cb : 0);
+    // gin bit 1 (polyphase, round 6): the N maps are the 4 polyphase sub-maps (parity a,
+    // b = sub-map / (N / 4)) of N / 4 maps of 2H x 2W -- a dilation-2 conv run as the
+    // plain conv of its sub-maps, read and written at their places in the full maps
+    const bool pph = (gin & 2) != 0;
+    const int pNr = N >> 2;
+    const float *const Xn = X + (pph ? 0 : (int64_t)n * H * W * C) + ((gin & 1) ? 64 * cb : 0);
+    // element offset of (sub-)map m, row y, column x
+    auto px_off = [&](int m, int y, int x) -> int64_t {
+        if (pph) {
+            const int ab = m / pNr, nr = m - ab * pNr;
+            return (((int64_t)nr * 2 * H + 2 * y + (ab >> 1)) * (2 * W) + 2 * x + (ab & 1));
+        }
+        return ((int64_t)m * H + y) * W + x;
+    };
     // kept in LDS (after the patch stages), not in six registers the MFMA phase needs
     uint32_t *const poff = reinterpret_cast<uint32_t *>(pst + 2 * k4PStageB) + tid;
     constexpr int kDW = ACC ? 8 : 4;  // waves issuing the patch DMA
@@ -253,9 +266,10 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
         const bool ok = R < k4PR && r5 < 4 && Cc < k4PC && (unsigned)ly < (unsigned)H &&
                         y >= 0 && x >= 0 && (unsigned)xm < (unsigned)W && n + cell + mr < N &&
                         (!oct || (cell < 4 && mr < 8)) && (!grid || gx < gG);
-        poff[kPS * k] = ok ? (uint32_t)((((cell + mr) * H + ly) * W + xm) * C + 4 * hf)
+        const int64_t po = pph ? px_off(n + cell + mr, ly, xm) : px_off(cell + mr, ly, xm);
+        poff[kPS * k] = ok ? (uint32_t)(po * C + 4 * hf)
                            : 0x80000000u | (uint32_t)(4 * hf);
-        srcp[k] = ok ? Xn + (((cell + mr) * H + ly) * W + xm) * C + 4 * hf : zero + 4 * hf;
+        srcp[k] = ok ? Xn + po * C + 4 * hf : zero + 4 * hf;
     }
     auto dma = [&](int ch, int stage) {
         if constexpr (ACC) {  // ch: the chunk whose data the pieces copy (clamped by the caller)
@@ -605,7 +619,7 @@ __global__ __launch_bounds__(k4Threads) void conv3x3_wino4_kernel(
             // probe_hi bit 0 (research, VOSDET_WINO4_PROBE bit 4): no output stores (a
             // store the data never takes keeps the values live)
             if (!(probe_hi & 1) || v.x == 1234.5678f)
-                *reinterpret_cast<float4 *>(Y + (((int64_t)ncell * H + yy) * W + xx) * Cout + co) = v;
+                *reinterpret_cast<float4 *>(Y + px_off(ncell, yy, xx) * Cout + co) = v;
         }
     }
 }
@@ -967,10 +981,18 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
     if (!conv3x3_wino4_supported(C, Cout)) return VD_ERR_SHAPE;
     // grouped: C == Cout, 64 input channels per 64-channel output block (C / groups
     // divides 64); the pair / octet / grid mosaics stay dense-only
-    const int gin = groups > 1;
-    if (gin && (groups < 1 || C != Cout || C % 64 || C % groups || 64 % (C / groups) ||
-                mos == 1 || mos == 4))
+    // groups == -2: polyphase (X / Y are N / 4 maps of 2H x 2W; the N sub-maps of H x W
+    // their parity planes): plain, pair / octet layouts only
+    int gin = groups > 1;
+    if (groups == -2) {
+        if (N % 4 || mos == 2 || mos == 4 || (int64_t)N * H * W * (C > Cout ? C : Cout) >=
+                                                 ((int64_t)1 << 31))
+            return VD_ERR_SHAPE;
+        gin = 2;
+    } else if (gin && (groups < 1 || C != Cout || C % 64 || C % groups ||
+                       64 % (C / groups) || mos == 1 || mos == 4)) {
         return VD_ERR_SHAPE;
+    }
     if ((int64_t)N * H * W * C >= ((int64_t)1 << 40) || (int64_t)H * W * C >= ((int64_t)1 << 31))
         return VD_ERR_SHAPE;
     // the map-pair mosaic: two maps of at most 15 x 15 per 16 x 32 block (the 16 x 16

@@ -281,6 +281,20 @@ def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=True):
     7 x 7 octets), batch-to-space."""
     if _dilated2_ok(conv, x):
         N, C, H, W = x.shape
+        algo, mos = conv3x3_route(4 * N, C, conv.weight.shape[0], H // 2, W // 2, mosaic)
+        if (algo == "wino4" and mos == "pair"
+                and os.environ.get("VOSDET_DILATED_INPLACE", "1") != "0"):
+            # the kernel reads / writes the sub-maps in place: no polyphase copies
+            w = conv.weight
+            key = (w.data_ptr(), w._version)
+            if getattr(conv, "_vd_u4_key", None) != key:
+                conv._vd_u4 = ops.conv3x3_wino4_weight(w.detach())
+                conv._vd_u4_key = key
+            b = conv.bias.detach() if (bias and conv.bias is not None) else None
+            y = ops.conv3x3_wino4_dilated2_bias_act(x, conv._vd_u4, b, relu=relu)
+            if y is not None:
+                _count_route("dilated2")
+                return y
         xs = x.permute(0, 2, 3, 1).reshape(N, H // 2, 2, W // 2, 2, C).permute(
             2, 4, 0, 1, 3, 5).reshape(4 * N, H // 2, W // 2, C).permute(0, 3, 1, 2)
         y = _conv3x3_mfma_core(conv, xs, bias, relu, mosaic, as_plain=True)
