@@ -710,9 +710,9 @@ def measure_step_post(pipe, frames_dev, reps=20):
                 "avg_us": round(t_d * 1e6, 1), "frames": F, "rois_per_frame": post,
                 "us_per_frame": round(t_d * 1e6 / F, 2)},
             "how": "HIP events over %d launches on the engine's own step tensors" % reps,
-            "rocprof": "profiles/r06/head_f/trace/post_launches.txt (64 frames): rpn_proposals "
-                       "85.2 (+ 6 rpn_sel_hist, rpn_sel_compact) + rpn_nms_mask 243.3 + "
-                       "rpn_nms_finish 64.5 us; class_nms 825.4 + det_limit 41.9 us per launch "
+            "rocprof": "profiles/r06/head_i/trace/post_launches.txt (64 frames): rpn_proposals "
+                       "85.5 (+ 6 rpn_sel_hist, rpn_sel_compact) + rpn_nms_mask 244.0 + "
+                       "rpn_nms_finish 64.7 us; class_nms 818.7 + det_limit 41.6 us per launch "
                        "(rocprofv3 --kernel-trace, 36 calls)"}
 
 
