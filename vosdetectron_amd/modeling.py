@@ -577,6 +577,30 @@ def _gn(dim: int, cfg) -> nn.GroupNorm:
     return nn.GroupNorm(group_gn(dim, cfg), dim, eps=cfg.GROUP_NORM.EPSILON)
 
 
+def _gn_conv1x1(conv: nn.Conv2d, x):
+    """A GN model's bias-free 1x1 conv (stride 1, or 2 read in place) as a split-bf16
+    GEMM (a zero bias; the GroupNorm follows), or None where the GEMM does not serve it
+    (MIOpen then: with its NHWC layout copies around a CK kernel, round 6's VOS trace)."""
+    if (not _is_1x1(conv) or conv.bias is not None or not x.is_cuda
+            or x.dtype != torch.float32 or not x.is_contiguous(memory_format=torch.channels_last)
+            or not ops.split3_enabled()):
+        return None
+    w = conv.weight
+    if getattr(conv, "_vd_gn_src", None) is not w:
+        conv._vd_gn_w2d = w.detach().reshape(w.shape[0], -1)
+        conv._vd_gn_zb = torch.zeros(w.shape[0], dtype=w.dtype, device=w.device)
+        conv._vd_gn_src = w
+    w2d = conv._vd_gn_w2d
+    K, N = w2d.shape[1], w2d.shape[0]
+    if K < ops.SPLIT3_MIN_K or K % 16 or N % 64 or x.shape[1] != K:
+        return None
+    if conv.stride == (1, 1):
+        return _gemm_conv1x1(x, w2d, conv._vd_gn_zb, relu=False)
+    if conv.stride == (2, 2) and _split3_s2_ok(x, w2d):
+        return _gemm_conv1x1_s2(x, w2d, conv._vd_gn_zb, relu=False)
+    return None
+
+
 def _gn_epi(conv: nn.Conv2d, gn: nn.GroupNorm, x, act="relu", res=None, res_gn=None, up=False):
     """conv (no bias) -> one vd_group_norm_act: act(GN(conv(x)) + res), the residual
     optionally normalised by its own GroupNorm (res_gn) or nearest-2x upsampled.  A
@@ -585,6 +609,8 @@ def _gn_epi(conv: nn.Conv2d, gn: nn.GroupNorm, x, act="relu", res=None, res_gn=N
     y = None
     if os.environ.get("VOSDET_GN_WINO", "1") != "0":
         y = _conv3x3_mfma(conv, x, bias=False, relu=False)
+    if y is None and os.environ.get("VOSDET_GN_GEMM", "1") != "0":
+        y = _gn_conv1x1(conv, x)
     if y is None:
         y = _conv_nb(conv, x)
     return ops.group_norm_act(y, gn.num_groups, gn.weight, gn.bias, gn.eps, residual=res,
