@@ -266,11 +266,12 @@ int vd_conv3x3_wino4_grouped_bias_act(const float *X, int N, int H, int W, int C
  * mask_rcnn_heads.py:178-188) of N maps of H x W (H, W even) by the same F(4x4) kernel:
  * it is the plain pad-1 conv of the 4 N polyphase sub-maps of H/2 x W/2 (output (2i +
  * a, 2j + b) reads only parity-(a, b) inputs at sub-map distance 1), which the kernel
- * reads and writes in place in the full maps (pairs / octets of sub-maps per block).
- * U from vd_conv3x3_wino4_weight of the same weight. */
+ * reads and writes in place in the full maps.  layout: the sub-maps one per block (0),
+ * as pairs / octets (1, H/2, W/2 <= 15) or as the shared-separator grid (2).  U from
+ * vd_conv3x3_wino4_weight of the same weight. */
 int vd_conv3x3_wino4_dilated2_bias_act(const float *X, int N, int H, int W, int C,
                                        const float *U, int Cout, const float *bias, int relu,
-                                       float *Y, void *stream);
+                                       float *Y, int layout, void *stream);
 /* The same over N maps laid out as a 2-D grid at a pitch of (H + 1) x (W + 1) -- one
  * zero row / column shared between neighbours, g maps per grid row chosen for the
  * fewest 16 x 32 output blocks (round 6; the mask head's 14 x 14 RoI maps: 32 per

@@ -75,7 +75,8 @@ SIGNATURES = {
     "vd_conv3x3_wino4_mosaic_bias_act": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
     "vd_conv3x3_wino4_rows_bias_act": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
     "vd_conv3x3_wino4_grid_bias_act": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
-    "vd_conv3x3_wino4_dilated2_bias_act": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _I, _P, _P]),
+    "vd_conv3x3_wino4_dilated2_bias_act": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _I, _P, _I,
+                                                _P]),
     "vd_conv3x3_wino4_grouped_bias_act": (_I, [_P, _I, _I, _I, _I, _P, _I, _P, _I, _P, _I,
                                                _P]),
     "vd_conv3x3_wino_seg_bias_act": (_I, [_P, _I, _I, _I, _P, _I, _P, _I, _I, _P, _P]),

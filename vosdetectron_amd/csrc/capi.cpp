@@ -216,16 +216,18 @@ int vd_conv3x3_wino4_grouped_bias_act(const float *X, int N, int H, int W, int C
 
 int vd_conv3x3_wino4_dilated2_bias_act(const float *X, int N, int H, int W, int C,
                                        const float *U, int Cout, const float *bias, int relu,
-                                       float *Y, void *stream) {
+                                       float *Y, int layout, void *stream) {
     if (N < 0 || H < 2 || W < 2 || (H & 1) || (W & 1) || C < 1 || Cout < 1 || !U || !Y ||
         (N > 0 && !X))
         return VD_ERR_ARG;
     if ((int64_t)N * H * W == 0) return VD_OK;
     if ((int64_t)4 * N >= ((int64_t)1 << 30)) return VD_ERR_SHAPE;
     const int h = H / 2, w = W / 2;
-    // the sub-maps as pairs / octets where they fit a 16 x 16 cell, else one per block
+    // layout of the sub-maps: 0 one per block, 1 pairs / octets (h, w <= 15), 2 the
+    // shared-separator grid
+    if (layout < 0 || layout > 2 || (layout == 1 && (h > 15 || w > 15))) return VD_ERR_ARG;
     return launch_conv3x3_wino4(X, 4 * N, h, w, C, U, Cout, bias, relu, Y, VD_STREAM(stream),
-                                (h <= 15 && w <= 15) ? 1 : 0, -2);
+                                layout == 2 ? 4 : layout, -2);
 }
 
 int vd_conv3x3_wino4_grid_bias_act(const float *X, int N, int H, int W, int C, const float *U,

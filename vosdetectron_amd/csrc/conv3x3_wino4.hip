@@ -985,7 +985,7 @@ int launch_conv3x3_wino4(const float *X, int N, int H, int W, int C, const float
     // their parity planes): plain, pair / octet layouts only
     int gin = groups > 1;
     if (groups == -2) {
-        if (N % 4 || mos == 2 || mos == 4 || (int64_t)N * H * W * (C > Cout ? C : Cout) >=
+        if (N % 4 || mos == 2 || (int64_t)N * H * W * (C > Cout ? C : Cout) >=
                                                  ((int64_t)1 << 31))
             return VD_ERR_SHAPE;
         gin = 2;

@@ -282,7 +282,7 @@ def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=True):
     if _dilated2_ok(conv, x):
         N, C, H, W = x.shape
         algo, mos = conv3x3_route(4 * N, C, conv.weight.shape[0], H // 2, W // 2, mosaic)
-        if (algo == "wino4" and mos == "pair"
+        if (algo == "wino4" and mos in ("pair", "grid", None)
                 and os.environ.get("VOSDET_DILATED_INPLACE", "1") != "0"):
             # the kernel reads / writes the sub-maps in place: no polyphase copies
             w = conv.weight
@@ -291,7 +291,8 @@ def _conv3x3_mfma(conv: nn.Conv2d, x, bias=True, relu=False, mosaic=True):
                 conv._vd_u4 = ops.conv3x3_wino4_weight(w.detach())
                 conv._vd_u4_key = key
             b = conv.bias.detach() if (bias and conv.bias is not None) else None
-            y = ops.conv3x3_wino4_dilated2_bias_act(x, conv._vd_u4, b, relu=relu)
+            y = ops.conv3x3_wino4_dilated2_bias_act(x, conv._vd_u4, b, relu=relu,
+                                                    layout=mos or False)
             if y is not None:
                 _count_route("dilated2")
                 return y

@@ -922,14 +922,18 @@ def conv3x3_wino4_bias_act(x: torch.Tensor, u: torch.Tensor, bias: Optional[torc
 
 def conv3x3_wino4_dilated2_bias_act(x: torch.Tensor, u: torch.Tensor,
                                     bias: Optional[torch.Tensor], relu: bool = False,
-                                    out: Optional[torch.Tensor] = None):
+                                    out: Optional[torch.Tensor] = None, layout=False):
     """act(conv3x3(x, dilation 2, pad 2) + bias) of channels_last fp32 maps (H, W even)
     on the F(4x4) kernel as the plain conv of the polyphase sub-maps, read and written in
     place (vd_conv3x3_wino4_dilated2_bias_act); u from conv3x3_wino4_weight.  None for a
-    shape the kernel does not serve."""
+    shape the kernel does not serve.  layout: the sub-maps' block layout, False (one
+    per block), "pair" (pairs / octets) or "grid"."""
     if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 4 \
             or not x.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("x must be a channels_last fp32 device tensor")
+    lay = {False: 0, None: 0, "pair": 1, True: 1, "grid": 2}.get(layout)
+    if lay is None:
+        return None
     u_ = _need(u, "u")
     N, C, H, W = x.shape
     if u_.dim() != 6 or tuple(u_.shape[1:]) != (C // 8, 4, 18, 64, 4) or C % 8 or H % 2 or W % 2:
@@ -941,7 +945,7 @@ def conv3x3_wino4_dilated2_bias_act(x: torch.Tensor, u: torch.Tensor,
                           memory_format=torch.channels_last)
     st = lib().vd_conv3x3_wino4_dilated2_bias_act(
         x.data_ptr(), N, H, W, C, u_.data_ptr(), Cout, b_.data_ptr() if b_ is not None else None,
-        int(relu), out.data_ptr(), _stream())
+        int(relu), out.data_ptr(), lay, _stream())
     if st == VD_ERR_SHAPE:
         return None
     check(st, "vd_conv3x3_wino4_dilated2_bias_act")
