@@ -481,8 +481,10 @@ int launch_gemm_split3(const float *A, int M, int K, const float *A2, int K2, co
             const char *e = getenv("VOSDET_SPLIT3_WIDE");
             return !(e && e[0] == '0');
         }();
+        // (N, K >= 1024 at any M: ResNeXt's 1024-wide res4 1x1s at 64 frames, 2.76 ->
+        // 2.51 ms, profiles/r06/split3_cfg/)
         if (wide && N % 256 == 0 &&
-            (K >= 4096 || M >= 500000 || (N >= 1024 && M <= 65536 && K >= 1024)))
+            (K >= 4096 || M >= 500000 || (N >= 1024 && K >= 1024)))
             cfg = 5;
         // 128 x 128 tiles at three workgroups per CU where 256 x 128 would give fewer
         // than three workgroups per slot (res4 / res5 at 32 frames, N <= 512): more
