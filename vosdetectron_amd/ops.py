@@ -608,6 +608,8 @@ def gemm_bias_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor,
                                         a_bias=a_bias)
     if a_bias is not None:
         a_ = torch.relu(a_ + _need(a_bias, "a_bias"))
+    if os.environ.get("VOSDET_GEMM_TRACE") == "1":  # research: the fp32-kernel GEMMs
+        sys.stderr.write("fp32 gemm M=%d N=%d K=%d res=%d\n" % (M, N, K, r_ is not None))
     ws = gemm_workspace(a_.device)
     st = lib().vd_gemm_bias_act(a_.data_ptr(), M, K, w_.data_ptr(), N, b_.data_ptr(),
                                 r_.data_ptr() if r_ is not None else None, int(relu),
