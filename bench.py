@@ -105,7 +105,8 @@ ROIALIGN_KERNEL = {"3": "vd::roi_align_fpn_nhwc_kernel<7,2,2> (reference order)"
 # passes per counter group; FETCH_SIZE doubled per the MI355X guide): L2<->fabric
 # bytes per launch, committed under profiles/ and reported as "traffic".
 ROIALIGN_PMC = {"8": "r02_roialign_pmc/separable_v8_xcd.json",
-                "10": "r03/roialign_pmc/separable_buf_v10_xcd.json"}
+                # re-measured at the end of round 6 (1,530,243,616 B; round 3: 1,531,124,880)
+                "10": "r06/roialign_pmc/separable_buf_v10_xcd.json"}
 
 
 def measure_roialign_roofline(dev, frames=8, R=1000, C=256, P=7, sr=2, iters=None,
